@@ -1,0 +1,439 @@
+"""Shared test helpers: corpus regeneration, a Python reading of the reference's
+on-disk formats, pf_corpus_desc marshalling, fixture readers and the oracle.
+
+Test infrastructure only.  The CSV reader here restates the reference loaders
+(user_loader.cpp:10-96, utils.cpp:36-68/123-142, graph_builder.cpp:39-59,
+user_loader.cpp:98-140) so that the oracle sees exactly the corpus the
+reference saw; the product has its own C++ loaders, checked against the same
+fixtures.
+"""
+import ctypes
+import gzip
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import synth  # noqa: E402
+
+NUM_FIXED = 7
+FIXED_KEYS = ["public", "gender", "completion", "age", "region", "clubs", "friends"]
+PF_MODE_FOF, PF_MODE_ALL = 0, 1
+PF_FOF_GRAPH, PF_FOF_COLLAB = 0, 1
+PF_IDF_FROM_PROFILES, PF_IDF_EXPLICIT = 0, 1
+
+
+# --------------------------------------------------------------------------- desc
+class PfCorpusDesc(ctypes.Structure):
+    P = ctypes.c_void_p
+    _fields_ = [("n_users", ctypes.c_int32), ("n_cols", ctypes.c_int32),
+                ("user_id", P), ("public_flag", P), ("completion", P), ("gender", P), ("age", P),
+                ("region", P), ("club_off", P), ("club_ids", P), ("friend_off", P), ("friend_ids", P),
+                ("tok_off", P), ("tok_tid", P), ("tok_tf", P),
+                ("n_adj", ctypes.c_int32), ("adj_uid", P), ("adj_off", P), ("adj_nbr", P),
+                ("idf_mode", ctypes.c_int32), ("col_has_idf", P), ("idf_off", P), ("idf_tid", P),
+                ("idf_val", P), ("norm_present", P), ("norm_mean", P), ("norm_sd", P)]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Corpus:
+    """numpy-backed corpus; .desc is a PfCorpusDesc pointing into the arrays."""
+
+    def __init__(self, uid, pub, comp, gen, age, region, club_off, clubs, friend_off, friends,
+                 tok_off, tok_tid, tok_tf, adj_uid, adj_off, adj_nbr, n_cols,
+                 norm_present=None, norm_mean=None, norm_sd=None, median=0, col_names=None):
+        c = lambda a, t: np.ascontiguousarray(np.asarray(a, dtype=t))
+        self.uid, self.pub, self.comp = c(uid, np.int32), c(pub, np.int32), c(comp, np.int32)
+        self.gen, self.age, self.region = c(gen, np.int32), c(age, np.int32), c(region, np.int32)
+        self.club_off, self.clubs = c(club_off, np.int64), c(clubs, np.uint32)
+        self.friend_off, self.friends = c(friend_off, np.int64), c(friends, np.uint32)
+        self.tok_off, self.tok_tid, self.tok_tf = c(tok_off, np.int64), c(tok_tid, np.int32), c(tok_tf, np.int32)
+        self.adj_uid, self.adj_off, self.adj_nbr = c(adj_uid, np.int32), c(adj_off, np.int64), c(adj_nbr, np.int32)
+        self.n_cols = n_cols
+        K = NUM_FIXED + n_cols
+        self.norm_present = c(norm_present if norm_present is not None else np.zeros(K), np.uint8)
+        self.norm_mean = c(norm_mean if norm_mean is not None else np.zeros(K), np.float32)
+        self.norm_sd = c(norm_sd if norm_sd is not None else np.zeros(K), np.float32)
+        self.median = median
+        self.col_names = col_names
+        self.desc = PfCorpusDesc()
+        d = self.desc
+        d.n_users, d.n_cols = len(self.uid), n_cols
+        for name in ["user_id", "public_flag", "completion", "gender", "age", "region"]:
+            pass
+        d.user_id, d.public_flag, d.completion = _ptr(self.uid), _ptr(self.pub), _ptr(self.comp)
+        d.gender, d.age, d.region = _ptr(self.gen), _ptr(self.age), _ptr(self.region)
+        d.club_off, d.club_ids = _ptr(self.club_off), _ptr(self.clubs)
+        d.friend_off, d.friend_ids = _ptr(self.friend_off), _ptr(self.friends)
+        d.tok_off, d.tok_tid, d.tok_tf = _ptr(self.tok_off), _ptr(self.tok_tid), _ptr(self.tok_tf)
+        d.n_adj = len(self.adj_uid)
+        d.adj_uid, d.adj_off, d.adj_nbr = _ptr(self.adj_uid), _ptr(self.adj_off), _ptr(self.adj_nbr)
+        d.idf_mode = PF_IDF_FROM_PROFILES
+        d.norm_present, d.norm_mean, d.norm_sd = _ptr(self.norm_present), _ptr(self.norm_mean), _ptr(self.norm_sd)
+
+    @property
+    def n_users(self):
+        return len(self.uid)
+
+    def desc_ptr(self):
+        return ctypes.addressof(self.desc)
+
+    def index(self):
+        return {int(u): i for i, u in enumerate(self.uid)}
+
+
+# ------------------------------------------------------------- reference formats
+def _atoi(s):
+    """C atoi: optional whitespace, sign, digits; stops at the first non-digit."""
+    i, n = 0, len(s)
+    while i < n and s[i] in " \t\n\v\f\r":
+        i += 1
+    sign = 1
+    if i < n and s[i] in "+-":
+        sign = -1 if s[i] == "-" else 1
+        i += 1
+    v = 0
+    while i < n and "0" <= s[i] <= "9":
+        v = v * 10 + ord(s[i]) - 48
+        i += 1
+    v *= sign
+    return ((v + 2**31) % 2**32) - 2**31
+
+
+def _split_csv(line):  # utils.cpp:36-50 — '"' toggles, no escapes
+    out, cur, q = [], [], False
+    for ch in line:
+        if ch == '"':
+            q = not q
+            continue
+        if ch == "," and not q:
+            out.append("".join(cur))
+            cur = []
+        else:
+            cur.append(ch)
+    out.append("".join(cur))
+    return out
+
+
+def _getline_split(s, sep):
+    """std::getline(stringstream, tok, sep) sequence (no trailing empty token)."""
+    if s == "":
+        return []
+    parts = s.split(sep)
+    if parts and parts[-1] == "":
+        parts = parts[:-1]
+    return parts
+
+
+def read_reference_dir(root, cap=100000):
+    """Parse data/ + config/ like api_cli start-up (api_cli.cpp:93-167)."""
+    with open(os.path.join(root, "config", "text_columns.txt")) as f:
+        cols = [ln.rstrip("\n") for ln in f if ln.rstrip("\n") != ""]
+    T = len(cols)
+    profiles = {}  # uid -> record; dict keeps first-insertion order like the map's node history
+    with open(os.path.join(root, "data", "users_encoded.csv"), encoding="latin-1") as f:
+        f.readline()
+        c = 0
+        for raw in f:
+            if c >= cap:
+                break
+            c += 1
+            line = raw.rstrip("\n")
+            if line == "":
+                continue
+            parts = _split_csv(line)
+            uid = _atoi(parts[0])
+            if uid == 0:
+                continue
+            g = lambda k: parts[k] if k < len(parts) else ""
+            rec = {"pub": _atoi(g(1)) if g(1) else -1, "comp": _atoi(g(2)) if g(2) else -1,
+                   "gen": _atoi(g(3)) if g(3) else -1, "age": _atoi(g(5)) if g(5) else 0}
+            rec["clubs"] = [(_atoi(t) & 0xFFFFFFFF) for t in _getline_split(g(6), ";") if t]
+            rec["friends"] = [(_atoi(t) & 0xFFFFFFFF) for t in _getline_split(g(7), ";") if t]
+            reg = [-1, -1, -1]
+            rf = g(4)
+            if rf:
+                if len(rf) >= 2 and rf[0] == '"' and rf[-1] == '"':
+                    rf = rf[1:-1]
+                for pi, tok in enumerate(_getline_split(rf, ";")[:3]):
+                    if tok:
+                        reg[pi] = _atoi(tok)
+            rec["reg"] = reg
+            toks = []
+            for t in range(T):
+                fld = g(8 + t)
+                m = {}
+                if fld:
+                    s = fld
+                    if len(s) >= 2 and s[0] == '"' and s[-1] == '"':
+                        s = s[1:-1]
+                    for tok in _getline_split(s, ";"):
+                        if not tok or ":" not in tok:
+                            continue
+                        p = tok.index(":")
+                        m[_atoi(tok[:p])] = _atoi(tok[p + 1:])  # first position, last value
+                toks.append(m)
+            rec["toks"] = toks
+            if uid in profiles:
+                profiles[uid].update(rec)
+            else:
+                profiles[uid] = rec
+    # adjacency.csv (graph_builder.cpp:39-59): repeated uid lines append
+    adj = {}
+    with open(os.path.join(root, "data", "adjacency.csv")) as f:
+        for raw in f:
+            line = raw.rstrip("\n")
+            if line == "":
+                continue
+            first, uid = True, -1
+            for tok in _getline_split(line, ","):
+                t = tok.strip(" \t\n\v\f\r")
+                if t == "":
+                    continue
+                if first:
+                    uid, first = _atoi(t), False
+                    continue
+                adj.setdefault(uid, []).append(_atoi(t))
+    # median age (user_loader.cpp:98-129) + fill
+    med_path = os.path.join(root, "data", "median_age.txt")
+    if os.path.exists(med_path):
+        with open(med_path) as f:
+            median = _atoi(f.readline())
+    else:
+        ages = sorted(r["age"] for r in profiles.values() if r["age"] > 0)
+        n = len(ages)
+        median = 0 if n == 0 else (ages[n // 2] if n % 2 else (ages[n // 2 - 1] + ages[n // 2]) // 2)
+    for r in profiles.values():
+        if r["age"] == 0:
+            r["age"] = median
+    # normalisers (utils.cpp:123-142), one map feeds both slots (api_cli.cpp:163-165)
+    K = NUM_FIXED + T
+    npres, nmean, nsd = np.zeros(K, np.uint8), np.zeros(K, np.float32), np.zeros(K, np.float32)
+    norm_path = os.path.join(root, "data", "column_normalizers.csv")
+    if os.path.exists(norm_path):
+        keys = {k: i for i, k in enumerate(FIXED_KEYS)}
+        for t, name in enumerate(cols):
+            keys.setdefault(name, NUM_FIXED + t)
+        with open(norm_path) as f:
+            f.readline()
+            for raw in f:
+                line = raw.rstrip("\n")
+                if not line or "," not in line:
+                    continue
+                p1 = line.index(",")
+                p2 = line.find(",", p1 + 1)
+                if p2 < 0:
+                    continue
+                k = line[:p1]
+                if k in keys:
+                    i = keys[k]
+                    npres[i] = 1
+                    nmean[i] = np.float32(float(line[p1 + 1:p2] or 0))
+                    nsd[i] = np.float32(float(line[p2 + 1:] or 0))
+    return build_corpus(profiles, adj, T, npres, nmean, nsd, median, cols)
+
+
+def build_corpus(profiles, adj, T, npres, nmean, nsd, median, cols):
+    uids = list(profiles.keys())
+    n = len(uids)
+    pub = [profiles[u]["pub"] for u in uids]
+    comp = [profiles[u]["comp"] for u in uids]
+    gen = [profiles[u]["gen"] for u in uids]
+    age = [profiles[u]["age"] for u in uids]
+    region = [x for u in uids for x in profiles[u]["reg"]]
+    club_off, clubs, friend_off, friends = [0], [], [0], []
+    tok_off, tid, tf = [0], [], []
+    for u in uids:
+        r = profiles[u]
+        clubs += r["clubs"]
+        club_off.append(len(clubs))
+        friends += r["friends"]
+        friend_off.append(len(friends))
+        for t in range(T):
+            for k, v in r["toks"][t].items():
+                tid.append(k)
+                tf.append(v)
+            tok_off.append(len(tid))
+    adj_uid = list(adj.keys())
+    adj_off, adj_nbr = [0], []
+    for a in adj_uid:
+        adj_nbr += adj[a]
+        adj_off.append(len(adj_nbr))
+    return Corpus(uids, pub, comp, gen, age, region, club_off, clubs, friend_off, friends,
+                  tok_off, tid, tf, adj_uid, adj_off, adj_nbr, T, npres, nmean, nsd, median, cols)
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def regen_reference_dir(name, dest):
+    """Regenerate golden corpus `name` (or 'api') in the reference's formats under dest."""
+    m = manifest()
+    c = m["api_cli"] if name == "api" else m["corpora"][name]
+    corpus = synth.Corpus(n_users=c["n_users"], seed=c["seed"], edge_cases=c["edge_cases"])
+    corpus.write_reference_files(dest, normalizers=c["normalizers"], median=c["median"])
+    corpus.close()
+    return dest
+
+
+_CACHE = {}
+
+
+def golden_corpus(name):
+    """Parsed golden corpus (cached per process)."""
+    if name not in _CACHE:
+        with tempfile.TemporaryDirectory() as d:
+            regen_reference_dir(name, d)
+            _CACHE[name] = read_reference_dir(d)
+    return _CACHE[name]
+
+
+# ------------------------------------------------------------------ fixtures
+def fixture_lines(name, fn):
+    with gzip.open(os.path.join(GOLDEN, name, fn + ".gz"), "rt") as f:
+        return [ln.rstrip("\n") for ln in f]
+
+
+def f32(hexbits):
+    return np.frombuffer(np.uint32(int(hexbits, 16)).tobytes(), np.float32)[0]
+
+
+def golden_pairs(name):
+    a, b, s = [], [], []
+    for ln in fixture_lines(name, "pairs.txt"):
+        x, y, h = ln.split()
+        a.append(int(x)); b.append(int(y)); s.append(int(h, 16))
+    return np.array(a, np.int32), np.array(b, np.int32), np.array(s, np.uint32)
+
+
+def golden_lists(name, fn):
+    """{(tag, uid, topk, limit): [(id, float32 bits), ...]}"""
+    out = {}
+    for ln in fixture_lines(name, fn):
+        p = ln.split()
+        tag, uid, k, lim, n = p[0], int(p[1]), int(p[2]), int(p[3]), int(p[4])
+        items = [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:5 + n]]
+        out[(tag, uid, k, lim)] = items
+    return out
+
+
+def golden_idf(name):
+    lines = fixture_lines(name, "idf.txt")
+    N = int(lines[0].split()[1])
+    rows = [ln.split() for ln in lines[1:]]
+    return N, [(int(t), int(k), int(h, 16)) for t, k, h in rows]
+
+
+# ------------------------------------------------------------------ oracle
+ORACLE_SO = os.path.join(ROOT, "oracle", "librefcpu.so")
+
+
+def oracle_lib():
+    src = os.path.join(ROOT, "oracle", "refcpu.cpp")
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "refcpu"], check=True)
+    L = ctypes.CDLL(ORACLE_SO)
+    V, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.ro_open.argtypes = [V, I32, ctypes.POINTER(V)]
+    L.ro_close.argtypes = [V]
+    L.ro_num_users.argtypes = [V]
+    L.ro_num_users.restype = I32
+    L.ro_idf.argtypes = [V, I32, I32]
+    L.ro_idf.restype = ctypes.c_float
+    L.ro_fas_pairs.argtypes = [V, V, V, I64, V]
+    for fn in ["ro_recommend_collab", "ro_recommend_clubs"]:
+        getattr(L, fn).argtypes = [V, V, I32, I32, I32, V, V, V]
+    L.ro_recommend_interest.argtypes = [V, V, I32, I32, I32, I32, V, V, V]
+    L.ro_fof_candidates.argtypes = [V, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+    L.ro_set_adj.argtypes = [V, I32, V, I32]
+    L.ro_profile_order.argtypes = [V, V, I32]
+    L.ro_holdout_friends.argtypes = [V, I32, V, I32, ctypes.POINTER(I32)]
+    L.ro_recommendation_tests.argtypes = [V, I32, I32, V]
+    return L
+
+
+class Oracle:
+    """ctypes handle on oracle/librefcpu.so (the CPU restatement)."""
+
+    def __init__(self, corpus, max_users=0, desc_ptr=None):
+        self.L = oracle_lib()
+        self.h = ctypes.c_void_p()
+        self.corpus = corpus
+        p = desc_ptr if desc_ptr is not None else corpus.desc_ptr()
+        rc = self.L.ro_open(p, max_users, ctypes.byref(self.h))
+        assert rc == 0
+
+    def close(self):
+        if self.h:
+            self.L.ro_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fas_pairs(self, a, b):
+        a = np.ascontiguousarray(a, np.int32)
+        b = np.ascontiguousarray(b, np.int32)
+        out = np.empty(len(a), np.float32)
+        self.L.ro_fas_pairs(self.h, a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+        return out
+
+    def _topk(self, fn, q, topk, *extra):
+        q = np.ascontiguousarray(np.atleast_1d(q), np.int32)
+        ou = np.zeros(len(q) * topk, np.int32)
+        os_ = np.zeros(len(q) * topk, np.float32)
+        oc = np.zeros(len(q), np.int32)
+        getattr(self.L, fn)(self.h, q.ctypes.data, len(q), topk, *extra, ou.ctypes.data, os_.ctypes.data,
+                            oc.ctypes.data)
+        return [(ou[i * topk:i * topk + oc[i]].copy(), os_[i * topk:i * topk + oc[i]].copy())
+                for i in range(len(q))]
+
+    def interest(self, q, topk, mode=PF_MODE_FOF, limit=10000):
+        return self._topk("ro_recommend_interest", q, topk, mode, limit)
+
+    def collab(self, q, topk, limit=10000):
+        return self._topk("ro_recommend_collab", q, topk, limit)
+
+    def clubs(self, q, topk, limit=10000):
+        return self._topk("ro_recommend_clubs", q, topk, limit)
+
+    def fof(self, uid, limit, flavour):
+        cap = max(limit, 1) + 1
+        out = np.zeros(cap, np.int32)
+        n = ctypes.c_int32()
+        self.L.ro_fof_candidates(self.h, uid, limit, flavour, out.ctypes.data, cap, ctypes.byref(n))
+        return out[:min(n.value, cap)].copy()
+
+    def idf(self, col, tid):
+        return self.L.ro_idf(self.h, col, tid)
+
+    def profile_order(self):
+        n = self.L.ro_num_users(self.h)
+        out = np.zeros(n, np.int32)
+        self.L.ro_profile_order(self.h, out.ctypes.data, n)
+        return out
+
+    def holdout_friends(self, sample):
+        out = np.zeros(max(sample, 1), np.float64)
+        n = ctypes.c_int32()
+        self.L.ro_holdout_friends(self.h, sample, out.ctypes.data, len(out), ctypes.byref(n))
+        return out[:n.value]
+
+    def recommendation_tests(self, sample, topk):
+        m = np.zeros(5, np.float64)
+        self.L.ro_recommendation_tests(self.h, sample, topk, m.ctypes.data)
+        return m

@@ -1,0 +1,685 @@
+// pf_api.cpp — the C ABI (include/pokec_fas.h): context lifetime, device upload,
+// query-image packing, and the host orchestration of the reference's recommenders
+// (recommender_graph.cpp:10-237, recommender_clubs.cpp:10-73) around the gfx950
+// kernels.  The FAS arithmetic itself runs only on the GPU; there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "pf_kernels.h"
+#include "pf_store.h"
+#include "pokec_fas.h"
+
+namespace {
+
+thread_local std::string g_open_error;
+constexpr uint32_t kLdsLimit = 64 * 1024;  // query images above this probe from global memory
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        want = want + want / 4;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+using Ranked = std::vector<std::pair<int32_t, float>>;
+
+void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
+    std::sort(v.begin(), v.end(), [](const std::pair<int32_t, float>& a, const std::pair<int32_t, float>& b) {
+        return a.second == b.second ? a.first < b.first : a.second > b.second;
+    });
+    if ((int)v.size() > topk) v.resize(std::max(topk, 0));
+}
+
+}  // namespace
+
+struct pf_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_scan_ms = 0.f;
+    std::string err;
+    pf::HostCorpus hc;
+    pf::HostStore hs;       // metadata only after upload (stream freed)
+    int64_t stream_bytes = 0;
+    DBuf d_stream, d_tile_off, d_tile_steps, d_hdr0, d_hdr1, d_slot_uid, d_slot_len;
+    pf::DevStore ds{};
+    // workspaces
+    DBuf d_pool, d_refs, d_part, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum;
+    int32_t tile_begin = 0, tile_end = 0;
+    // host sources of in-flight async uploads (kept alive until the next call)
+    std::vector<uint8_t> h_pool;
+    std::vector<pf::QImageRef> h_refs;
+    std::vector<int32_t> h_rows;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hip_fail(hipError_t e, const char* what) {
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return PF_ENODEV;
+    }
+};
+
+namespace {
+
+#define HIPCHK(ctx, expr)                                   \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return (ctx)->hip_fail(_e, #expr); \
+    } while (0)
+
+template <class T>
+hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
+    hipError_t e = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+    if (e != hipSuccess) return e;
+    if (v.empty()) return hipSuccess;
+    return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream);
+}
+
+// Query images -> one byte pool + refs.
+struct Images {
+    std::vector<uint8_t> pool;
+    std::vector<pf::QImageRef> refs;
+    uint32_t max_lds = sizeof(pf::QConst) + 2048;
+};
+
+void add_image(Images& im, const pf::QImageHost& q) {
+    auto align = [&](size_t a) { while (im.pool.size() % a) im.pool.push_back(0); };
+    align(16);
+    pf::QImageRef r{};
+    r.const_off = (uint32_t)im.pool.size();
+    const uint8_t* cp = reinterpret_cast<const uint8_t*>(&q.c);
+    im.pool.insert(im.pool.end(), cp, cp + sizeof(pf::QConst));
+    r.keys_off = (uint32_t)im.pool.size();
+    const uint8_t* kp = reinterpret_cast<const uint8_t*>(q.keys.data());
+    im.pool.insert(im.pool.end(), kp, kp + q.keys.size() * 8);
+    align(16);
+    r.vals_off = (uint32_t)im.pool.size();
+    const uint8_t* vp = reinterpret_cast<const uint8_t*>(q.vals.data());
+    im.pool.insert(im.pool.end(), vp, vp + q.vals.size() * sizeof(pf::QVal));
+    size_t lds = sizeof(pf::QConst) + q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal) + 2048;
+    r.lds_bytes = lds <= kLdsLimit ? (uint32_t)lds : 0u;
+    im.max_lds = std::max<uint32_t>(im.max_lds, r.lds_bytes);
+    im.refs.push_back(r);
+}
+
+// recommender_graph.cpp:10-31 (friends + FoFs, first-seen order, limit after every push)
+std::vector<int32_t> gather_graph(const pf::HostCorpus& hc, int32_t u, int32_t limit) {
+    std::vector<int32_t> out;
+    auto it = hc.adj.find(u);
+    if (it == hc.adj.end()) return out;
+    std::unordered_set<int32_t> seen;
+    for (int32_t f : it->second) {
+        if (f == u) continue;
+        if (seen.insert(f).second) out.push_back(f);
+        if ((int32_t)out.size() >= limit) return out;
+        auto jt = hc.adj.find(f);
+        if (jt == hc.adj.end()) continue;
+        for (int32_t x : jt->second) {
+            if (x == u || !seen.insert(x).second) continue;
+            out.push_back(x);
+            if ((int32_t)out.size() >= limit) return out;
+        }
+    }
+    return out;
+}
+
+// recommender_graph.cpp:114-125 (FoFs only; inner loop breaks at the limit)
+std::vector<int32_t> gather_collab(const pf::HostCorpus& hc, int32_t u, int32_t limit) {
+    std::vector<int32_t> out;
+    auto it = hc.adj.find(u);
+    if (it == hc.adj.end()) return out;
+    std::unordered_set<int32_t> seen;
+    for (int32_t f : it->second) {
+        auto jt = hc.adj.find(f);
+        if (jt == hc.adj.end()) continue;  // skips the limit check too (recommender_graph.cpp:117-118)
+        for (int32_t x : jt->second) {
+            if (x == u) continue;
+            if (seen.insert(x).second) out.push_back(x);
+            if ((int32_t)out.size() >= limit) break;
+        }
+        if ((int32_t)out.size() >= limit) break;
+    }
+    return out;
+}
+
+// FAS(A = qidx[g], B = slots[g][j]) for every group g, on the GPU.
+int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std::vector<int32_t>>& slots,
+              std::vector<std::vector<float>>& out) {
+    out.assign(qidx.size(), {});
+    Images im;
+    std::vector<pf::PairBlock> blocks;
+    std::vector<int32_t> flat;
+    pf::QImageHost qi;
+    for (size_t g = 0; g < qidx.size(); ++g) {
+        out[g].assign(slots[g].size(), 0.f);
+        if (slots[g].empty()) continue;
+        pf::build_query(c->hc, qidx[g], nullptr, qi);
+        const int32_t img = (int32_t)im.refs.size();
+        add_image(im, qi);
+        for (size_t b = 0; b < slots[g].size(); b += 256) {
+            pf::PairBlock pb{img, (int32_t)flat.size(), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
+            blocks.push_back(pb);
+            for (size_t j = b; j < b + (size_t)pb.count; ++j) flat.push_back(slots[g][j]);
+        }
+    }
+    if (flat.empty()) return PF_OK;
+    HIPCHK(c, upload(c, c->d_pool, im.pool));
+    HIPCHK(c, upload(c, c->d_refs, im.refs));
+    HIPCHK(c, upload(c, c->d_blocks, blocks));
+    HIPCHK(c, upload(c, c->d_slots, flat));
+    HIPCHK(c, c->d_scores.ensure(flat.size() * sizeof(float)));
+    HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds,
+                               c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
+                               c->d_scores.as<float>(), c->stream));
+    std::vector<float> res(flat.size());
+    HIPCHK(c, hipMemcpyAsync(res.data(), c->d_scores.p, res.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    size_t o = 0;
+    for (size_t g = 0; g < qidx.size(); ++g)
+        for (size_t j = 0; j < slots[g].size(); ++j) out[g][j] = res[o++];
+    return PF_OK;
+}
+
+void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc) {
+    int n = std::min<int>((int)r.size(), topk);
+    for (int k = 0; k < n; ++k) {
+        ou[(int64_t)i * topk + k] = r[k].first;
+        os[(int64_t)i * topk + k] = r[k].second;
+    }
+    oc[i] = n;
+}
+
+// All-candidates scan for `idx` (valid query indices) into d_keys rows `rows`.
+int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
+             hipStream_t s, bool timed) {
+    if (idx.empty()) return PF_OK;
+    Images im;
+    pf::QImageHost qi;
+    std::vector<int32_t> excl;
+    for (int32_t i : idx) {
+        const int32_t u = c->hc.uid[i];
+        excl.clear();
+        auto it = c->hc.adj.find(u);
+        if (it != c->hc.adj.end()) excl = it->second;
+        excl.push_back(u);
+        pf::build_query(c->hc, i, &excl, qi);
+        add_image(im, qi);
+    }
+    const int nq = (int)idx.size();
+    const int tiles = c->tile_end - c->tile_begin;
+    int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(8, c->num_cus * 8 / nq)));
+    c->h_pool.swap(im.pool);
+    c->h_refs.swap(im.refs);
+    c->h_rows = rows;
+    HIPCHK(c, c->d_pool.ensure(c->h_pool.size()));
+    HIPCHK(c, hipMemcpyAsync(c->d_pool.p, c->h_pool.data(), c->h_pool.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(c, c->d_refs.ensure(c->h_refs.size() * sizeof(pf::QImageRef)));
+    HIPCHK(c, hipMemcpyAsync(c->d_refs.p, c->h_refs.data(), c->h_refs.size() * sizeof(pf::QImageRef),
+                             hipMemcpyHostToDevice, s));
+    HIPCHK(c, c->d_rows.ensure(c->h_rows.size() * sizeof(int32_t)));
+    HIPCHK(c, hipMemcpyAsync(c->d_rows.p, c->h_rows.data(), c->h_rows.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
+    if (timed) HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, pf::launch_scan(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), c->h_refs.data(), nq,
+                              c->tile_begin, c->tile_end, k, blocks, c->d_part.as<uint64_t>(), s));
+    if (timed) HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, pf::launch_merge(c->d_part.as<uint64_t>(), blocks, k, (int64_t)blocks * k, nq, k, d_keys,
+                               c->d_rows.as<int32_t>(), s));
+    return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_abi_version(void) { return PF_ABI_VERSION; }
+
+int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
+    if (!out) { g_open_error = "null out"; return PF_EINVAL; }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        g_open_error = "no HIP device (the FAS engine has no CPU fallback)";
+        return PF_ENODEV;
+    }
+    if (device < 0 || device >= ndev) { g_open_error = "bad device ordinal"; return PF_EINVAL; }
+    pf_ctx* c = new pf_ctx();
+    c->device = device;
+    auto bail = [&](int rc) {
+        g_open_error = c->err;
+        delete c;
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(PF_ENODEV); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+        c->num_cus = prop.multiProcessorCount;
+        if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+            c->err = std::string("device is ") + prop.gcnArchName + ", the kernels are built for gfx950";
+            return bail(PF_ENODEV);
+        }
+    }
+    int rc = pf::build_host_corpus(desc, c->hc, c->err);
+    if (rc != PF_OK) return bail(rc);
+    pf::build_store(c->hc, c->hs);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        c->err = "stream/event creation failed";
+        return bail(PF_ENODEV);
+    }
+    auto& hs = c->hs;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = upload(c, c->d_stream, hs.stream);
+    if (e == hipSuccess) e = upload(c, c->d_tile_off, hs.tile_off);
+    if (e == hipSuccess) e = upload(c, c->d_tile_steps, hs.tile_steps);
+    if (e == hipSuccess) e = upload(c, c->d_hdr0, hs.hdr0);
+    if (e == hipSuccess) e = upload(c, c->d_hdr1, hs.hdr1);
+    if (e == hipSuccess) e = upload(c, c->d_slot_uid, hs.slot_uid);
+    if (e == hipSuccess) e = upload(c, c->d_slot_len, hs.slot_len);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        c->hip_fail(e, "corpus upload");
+        return bail(e == hipErrorOutOfMemory ? PF_ENOMEM : PF_ENODEV);
+    }
+    c->stream_bytes = (int64_t)hs.stream.size() * 16;
+    std::vector<uint4>().swap(hs.stream);
+    c->ds.stream = c->d_stream.as<uint4>();
+    c->ds.tile_off = c->d_tile_off.as<uint64_t>();
+    c->ds.tile_steps = c->d_tile_steps.as<uint32_t>();
+    c->ds.hdr0 = c->d_hdr0.as<uint4>();
+    c->ds.hdr1 = c->d_hdr1.as<uint4>();
+    c->ds.slot_uid = c->d_slot_uid.as<int32_t>();
+    c->ds.slot_len = c->d_slot_len.as<uint32_t>();
+    c->ds.n_slots = c->hc.n;
+    c->ds.n_tiles = (int32_t)hs.tile_steps.size();
+    c->ds.packed = hs.packed ? 1 : 0;
+    c->ds.n_cols = c->hc.T;
+    c->tile_begin = 0;
+    c->tile_end = c->ds.n_tiles;
+    *out = c;
+    return PF_OK;
+}
+
+void pf_close(pf_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : g_open_error.c_str(); }
+int32_t pf_num_users(const pf_ctx* c) { return c ? c->hc.n : 0; }
+float pf_idf(const pf_ctx* c, int32_t col, int32_t tid) {
+    if (!c || col < 0 || col >= c->hc.T) return NAN;
+    return c->hc.idf_of(col, tid);
+}
+
+int pf_fas_pairs(pf_ctx* c, const int32_t* a, const int32_t* b, int64_t n, float* out) {
+    if (!c || n < 0 || (n && (!a || !b || !out))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    std::unordered_map<int32_t, int32_t> group;  // query idx -> group
+    std::vector<int32_t> qidx;
+    std::vector<std::vector<int32_t>> slots;
+    std::vector<std::pair<int32_t, int32_t>> where(n, {-1, -1});
+    for (int64_t i = 0; i < n; ++i) {
+        out[i] = NAN;
+        int32_t ia = c->hc.idx_of(a[i]), ib = c->hc.idx_of(b[i]);
+        if (ia < 0 || ib < 0) continue;
+        auto it = group.find(ia);
+        if (it == group.end()) {
+            it = group.emplace(ia, (int32_t)qidx.size()).first;
+            qidx.push_back(ia);
+            slots.emplace_back();
+        }
+        where[i] = {it->second, (int32_t)slots[it->second].size()};
+        slots[it->second].push_back(c->hs.slot_of_idx[ib]);
+    }
+    std::vector<std::vector<float>> res;
+    int rc = run_pairs(c, qidx, slots, res);
+    if (rc != PF_OK) return rc;
+    for (int64_t i = 0; i < n; ++i)
+        if (where[i].first >= 0) out[i] = res[where[i].first][where[i].second];
+    return PF_OK;
+}
+
+int pf_recommend_interest(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t mode, int32_t limit,
+                          int32_t* ou, float* os, int32_t* oc) {
+    if (!c || nq < 0 || topk < 0 || (nq && (!q || !oc))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    for (int i = 0; i < nq; ++i) oc[i] = 0;
+    if (topk == 0 || nq == 0) return PF_OK;
+    if (mode == PF_MODE_ALL && topk <= pf::kMaxTopK) {
+        std::vector<int32_t> idx, rows;
+        for (int i = 0; i < nq; ++i) {
+            int32_t x = c->hc.idx_of(q[i]);
+            if (x >= 0) { idx.push_back(x); rows.push_back(i); }
+        }
+        HIPCHK(c, c->d_out.ensure((size_t)nq * topk * sizeof(uint64_t)));
+        HIPCHK(c, hipMemsetAsync(c->d_out.p, 0xFF, (size_t)nq * topk * sizeof(uint64_t), c->stream));
+        const int chunk = 256;
+        for (size_t b = 0; b < idx.size(); b += chunk) {
+            std::vector<int32_t> ii(idx.begin() + b, idx.begin() + std::min(idx.size(), b + chunk));
+            std::vector<int32_t> rr(rows.begin() + b, rows.begin() + std::min(rows.size(), b + chunk));
+            int rc = scan_all(c, ii, rr, topk, c->d_out.as<uint64_t>(), c->stream, b == 0);
+            if (rc != PF_OK) return rc;
+        }
+        std::vector<uint64_t> keys((size_t)nq * topk);
+        HIPCHK(c, hipMemcpyAsync(keys.data(), c->d_out.p, keys.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (!idx.empty()) HIPCHK(c, hipEventElapsedTime(&c->last_scan_ms, c->ev0, c->ev1));
+        for (int i = 0; i < nq; ++i) pf_decode_keys(&keys[(size_t)i * topk], topk, ou + (size_t)i * topk, os + (size_t)i * topk, &oc[i]);
+        return PF_OK;
+    }
+    // FoF-limited (reference) mode, or ALL with topk beyond the in-kernel bound
+    std::vector<int32_t> qidx, qrow;
+    std::vector<std::vector<int32_t>> slots, cuid;
+    for (int i = 0; i < nq; ++i) {
+        const int32_t u = q[i];
+        const int32_t iq = c->hc.idx_of(u);
+        if (iq < 0) continue;  // recommender_graph.cpp:39-40
+        std::unordered_set<int32_t> skip;
+        auto it = c->hc.adj.find(u);
+        if (it != c->hc.adj.end()) skip.insert(it->second.begin(), it->second.end());
+        skip.insert(u);
+        std::vector<int32_t> s, us;
+        if (mode == PF_MODE_ALL) {
+            for (int32_t j = 0; j < c->hc.n; ++j)
+                if (!skip.count(c->hc.uid[j])) { s.push_back(c->hs.slot_of_idx[j]); us.push_back(c->hc.uid[j]); }
+        } else {
+            for (int32_t x : gather_graph(c->hc, u, limit)) {
+                if (skip.count(x)) continue;
+                int32_t ix = c->hc.idx_of(x);
+                if (ix < 0) continue;
+                s.push_back(c->hs.slot_of_idx[ix]);
+                us.push_back(x);
+            }
+        }
+        qidx.push_back(iq);
+        qrow.push_back(i);
+        slots.push_back(std::move(s));
+        cuid.push_back(std::move(us));
+    }
+    std::vector<std::vector<float>> res;
+    int rc = run_pairs(c, qidx, slots, res);
+    if (rc != PF_OK) return rc;
+    for (size_t g = 0; g < qidx.size(); ++g) {
+        Ranked r;
+        r.reserve(res[g].size());
+        for (size_t j = 0; j < res[g].size(); ++j) r.emplace_back(cuid[g][j], res[g][j]);
+        rank(r, topk);
+        emit(r, qrow[g], topk, ou, os, oc);
+    }
+    return PF_OK;
+}
+
+// recommender_graph.cpp:105-222
+int pf_recommend_collab(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
+                        float* os, int32_t* oc) {
+    if (!c || nq < 0 || topk < 0 || (nq && (!q || !oc))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    for (int i = 0; i < nq; ++i) {
+        oc[i] = 0;
+        const int32_t u = q[i];
+        std::vector<int32_t> friends;
+        auto it = c->hc.adj.find(u);
+        if (it != c->hc.adj.end()) friends = it->second;
+        std::vector<int32_t> cand = gather_collab(c->hc, u, limit);
+        const int32_t iq = c->hc.idx_of(u);
+        if (iq < 0) continue;
+        // distinct friends with a profile -> matrix rows
+        std::unordered_map<int32_t, int32_t> row_of;
+        std::vector<int32_t> fidx;
+        for (int32_t f : friends) {
+            int32_t ix = c->hc.idx_of(f);
+            if (ix < 0 || row_of.count(f)) continue;
+            row_of.emplace(f, (int32_t)fidx.size());
+            fidx.push_back(ix);
+        }
+        std::vector<int32_t> cslots, cuids;
+        for (int32_t x : cand) {
+            if (x == u) continue;
+            int32_t ix = c->hc.idx_of(x);
+            if (ix < 0) continue;
+            cslots.push_back(c->hs.slot_of_idx[ix]);
+            cuids.push_back(x);
+        }
+        // sim_u_f (float, recommender_graph.cpp:132-136) and M[f][c] on the GPU
+        std::vector<int32_t> qs;
+        std::vector<std::vector<int32_t>> ss;
+        qs.push_back(iq);
+        ss.emplace_back();
+        for (int32_t ix : fidx) ss[0].push_back(c->hs.slot_of_idx[ix]);
+        for (int32_t ix : fidx) { qs.push_back(ix); ss.push_back(cslots); }
+        std::vector<std::vector<float>> res;
+        int rc = run_pairs(c, qs, ss, res);
+        if (rc != PF_OK) return rc;
+        const int F = (int)friends.size(), nc = (int)cslots.size();
+        if (nc == 0) continue;
+        std::vector<float> w(F, 0.f), M((size_t)fidx.size() * nc);
+        std::vector<int32_t> wrow(F, -1);
+        for (int j = 0; j < F; ++j) {
+            auto rt = row_of.find(friends[j]);
+            if (rt == row_of.end()) continue;
+            wrow[j] = rt->second;
+            w[j] = res[0][rt->second];
+        }
+        for (size_t r = 0; r < fidx.size(); ++r) std::copy(res[r + 1].begin(), res[r + 1].end(), M.begin() + r * nc);
+        HIPCHK(c, upload(c, c->d_scores, M));
+        HIPCHK(c, upload(c, c->d_w, w));
+        HIPCHK(c, upload(c, c->d_wrow, wrow));
+        HIPCHK(c, c->d_csum.ensure((size_t)nc * sizeof(float)));
+        HIPCHK(c, pf::launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(), F, nc,
+                                        c->d_csum.as<float>(), c->stream));
+        std::vector<float> sc(nc);
+        HIPCHK(c, hipMemcpyAsync(sc.data(), c->d_csum.p, nc * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        Ranked r;
+        for (int j = 0; j < nc; ++j) r.emplace_back(cuids[j], sc[j]);
+        rank(r, topk);
+        emit(r, i, topk, ou, os, oc);
+    }
+    return PF_OK;
+}
+
+// recommender_clubs.cpp:10-73
+int pf_recommend_clubs(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t /*limit*/, int32_t* ou,
+                       float* os, int32_t* oc) {
+    if (!c || nq < 0 || topk < 0 || (nq && (!q || !oc))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    const auto& hc = c->hc;
+    for (int i = 0; i < nq; ++i) {
+        oc[i] = 0;
+        const int32_t u = q[i];
+        const int32_t iq = hc.idx_of(u);
+        if (iq < 0) continue;
+        std::vector<int32_t> friends;
+        auto it = hc.adj.find(u);
+        if (it != hc.adj.end()) friends = it->second;
+        // pass 1: w_f = FAS(q, f) for distinct friends with a profile
+        std::unordered_map<int32_t, int32_t> fpos;
+        std::vector<int32_t> fidx, fuid;
+        for (int32_t f : friends) {
+            int32_t ix = hc.idx_of(f);
+            if (ix < 0 || fpos.count(f)) continue;
+            fpos.emplace(f, (int32_t)fidx.size());
+            fidx.push_back(ix);
+            fuid.push_back(f);
+        }
+        std::vector<std::vector<float>> res;
+        {
+            std::vector<int32_t> qs{iq};
+            std::vector<std::vector<int32_t>> ss(1);
+            for (int32_t ix : fidx) ss[0].push_back(c->hs.slot_of_idx[ix]);
+            int rc = run_pairs(c, qs, ss, res);
+            if (rc != PF_OK) return rc;
+        }
+        std::vector<float> w(res[0]);
+        // pass 2: FAS(f, fof) for every fof of every positive-weight friend
+        std::vector<int32_t> qs;
+        std::vector<std::vector<int32_t>> ss;
+        std::vector<int32_t> grp(fidx.size(), -1);
+        for (size_t r = 0; r < fidx.size(); ++r) {
+            if ((double)w[r] <= 0.0) continue;
+            auto jt = hc.adj.find(fuid[r]);
+            if (jt == hc.adj.end()) continue;
+            std::vector<int32_t> s;
+            for (int32_t x : jt->second) {
+                if (x == u) continue;
+                int32_t ix = hc.idx_of(x);
+                if (ix < 0) continue;
+                s.push_back(c->hs.slot_of_idx[ix]);
+            }
+            grp[r] = (int32_t)qs.size();
+            qs.push_back(fidx[r]);
+            ss.push_back(std::move(s));
+        }
+        std::vector<std::vector<float>> sff;
+        int rc = run_pairs(c, qs, ss, sff);
+        if (rc != PF_OK) return rc;
+        // club accumulation in the reference's exact loop order (double sums)
+        std::unordered_set<int32_t> own;
+        for (int64_t k = hc.club_off[iq]; k < hc.club_off[iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
+        std::unordered_map<int32_t, double> score;
+        for (int32_t f : friends) {
+            auto pt = fpos.find(f);
+            if (pt == fpos.end()) continue;
+            double wf = w[pt->second];
+            if (wf <= 0.0) continue;
+            int32_t ix = fidx[pt->second];
+            for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
+        }
+        for (int32_t f : friends) {
+            auto pt = fpos.find(f);
+            if (pt == fpos.end()) continue;
+            int32_t g = grp[pt->second];
+            double wf = w[pt->second];
+            if (wf <= 0.0 || g < 0) continue;
+            auto jt = hc.adj.find(f);
+            size_t j = 0;
+            for (int32_t x : jt->second) {
+                if (x == u) continue;
+                int32_t ix = hc.idx_of(x);
+                if (ix < 0) continue;
+                double s = sff[g][j++];
+                if (s <= 0.0) continue;
+                double add = wf * s;
+                for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                    if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += add;
+            }
+        }
+        Ranked r;
+        for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
+        rank(r, topk);
+        emit(r, i, topk, ou, os, oc);
+    }
+    return PF_OK;
+}
+
+int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {
+    if (!c || !n || (cap > 0 && !out)) return PF_EINVAL;
+    std::vector<int32_t> v = flavour == PF_FOF_COLLAB ? gather_collab(c->hc, uid, limit) : gather_graph(c->hc, uid, limit);
+    for (int32_t i = 0; i < (int32_t)v.size() && i < cap; ++i) out[i] = v[i];
+    *n = (int32_t)v.size();
+    return PF_OK;
+}
+
+int pf_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
+    if (!c || (n > 0 && !nbrs)) return PF_EINVAL;
+    if (n < 0) c->hc.adj.erase(uid);
+    else c->hc.adj[uid].assign(nbrs, nbrs + n);
+    return PF_OK;
+}
+
+int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {
+    if (!c || nshards < 1 || shard < 0 || shard >= nshards) return PF_EINVAL;
+    const auto& steps = c->hs.tile_steps;
+    const int T = (int)steps.size();
+    std::vector<uint64_t> pre(T + 1, 0);
+    for (int t = 0; t < T; ++t) pre[t + 1] = pre[t] + steps[t];
+    auto bound = [&](int s) -> int {
+        if (s <= 0) return 0;
+        if (s >= nshards) return T;
+        uint64_t target = pre[T] * (uint64_t)s / (uint64_t)nshards;
+        return (int)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+    };
+    c->tile_begin = bound(shard);
+    c->tile_end = bound(shard + 1);
+    return PF_OK;
+}
+
+int pf_scan_keys_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, uint64_t* d_keys, void* stream) {
+    if (!c || nq < 0 || topk <= 0 || topk > pf::kMaxTopK || (nq && (!q || !d_keys))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipMemsetAsync(d_keys, 0xFF, (size_t)nq * topk * sizeof(uint64_t), s));
+    std::vector<int32_t> idx, rows;
+    for (int i = 0; i < nq; ++i) {
+        int32_t x = c->hc.idx_of(q[i]);
+        if (x >= 0) { idx.push_back(x); rows.push_back(i); }
+    }
+    return scan_all(c, idx, rows, topk, d_keys, s, true);
+}
+
+int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int32_t nq, int32_t topk, uint64_t* d_out,
+                        void* stream) {
+    if (!c || nparts < 1 || nq < 0 || topk <= 0 || topk > pf::kMaxTopK) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, nullptr, s));
+    return PF_OK;
+}
+
+void pf_decode_keys(const uint64_t* keys, int32_t n, int32_t* ou, float* os, int32_t* count) {
+    int32_t m = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        if (keys[i] == ~0ull) break;
+        if (ou) ou[m] = pf::key_uid(keys[i]);
+        if (os) os[m] = pf::key_score(keys[i]);
+        ++m;
+    }
+    if (count) *count = m;
+}
+
+int pf_layout(const pf_ctx* c, pf_layout_stats* o) {
+    if (!c || !o) return PF_EINVAL;
+    o->n_slots = c->hc.n;
+    o->stream_bytes = c->stream_bytes;
+    o->header_bytes = (int64_t)c->hc.n * 32;
+    o->alg_bytes = c->hs.alg_bytes;
+    o->packed_tokens = c->hs.packed ? 1 : 0;
+    o->n_tiles = (int32_t)c->hs.tile_steps.size();
+    return PF_OK;
+}
+
+float pf_last_scan_ms(const pf_ctx* c) { return c ? c->last_scan_ms : 0.f; }
+
+}  // extern "C"

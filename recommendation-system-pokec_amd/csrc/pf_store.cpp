@@ -1,0 +1,405 @@
+// pf_store.cpp — host side of the FAS engine: corpus ingestion from a
+// pf_corpus_desc, float32 IDF (recommender.cpp:43-66), per-row candidate norms,
+// the length-sorted tile-interleaved record stream, and per-query images with
+// host-precomputed sigmoid tables (recommender_similarity.cpp:18-36).
+#include "pf_store.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+namespace pf {
+
+namespace {
+
+template <class F>
+void par_for(int64_t n, F f) {
+    int th = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < 4096 || th <= 1) { f((int64_t)0, n); return; }
+    std::vector<std::thread> ts;
+    int64_t chunk = (n + th - 1) / th;
+    for (int w = 0; w < th; ++w) {
+        int64_t lo = w * chunk, hi = std::min(n, lo + chunk);
+        if (lo >= hi) break;
+        ts.emplace_back(f, lo, hi);
+    }
+    for (auto& t : ts) t.join();
+}
+
+uint32_t next_pow2(uint32_t v) {
+    uint32_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+// recommender_similarity.cpp:18-26 (stable two-branch logistic, double)
+double ref_sigmoid(double x) {
+    if (x >= 0) {
+        double e = std::exp(-x);
+        return 1.0 / (1.0 + e);
+    }
+    double e = std::exp(x);
+    return e / (1.0 + e);
+}
+
+int32_t HostCorpus::idx_of(int32_t u) const {
+    auto it = std::lower_bound(uid.begin(), uid.end(), u);
+    if (it == uid.end() || *it != u) return -1;
+    return (int32_t)(it - uid.begin());
+}
+
+float HostCorpus::idf_of(int t, int32_t k) const {
+    if (!has_idf[t]) return NAN;
+    auto it = idf[t].find(k);
+    return it == idf[t].end() ? 1.0f : it->second;
+}
+
+int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err) {
+    if (!d) { err = "null descriptor"; return PF_EINVAL; }
+    if (d->n_users < 0 || d->n_cols < 0 || d->n_cols > kMaxCols) { err = "bad n_users/n_cols"; return PF_EINVAL; }
+    const int32_t n = d->n_users, T = d->n_cols;
+    if (n > 0 && (!d->user_id || !d->public_flag || !d->completion || !d->gender || !d->age || !d->region ||
+                  !d->club_off || !d->friend_off || !d->tok_off)) {
+        err = "missing profile arrays";
+        return PF_EINVAL;
+    }
+    hc.n = n;
+    hc.T = T;
+    // candidate index = rank of uid (ascending)
+    std::vector<int32_t> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return d->user_id[a] < d->user_id[b]; });
+    for (int i = 1; i < n; ++i)
+        if (d->user_id[order[i]] == d->user_id[order[i - 1]]) { err = "duplicate user id"; return PF_EINVAL; }
+    hc.uid.resize(n); hc.pub.resize(n); hc.comp.resize(n); hc.gen.resize(n); hc.age.resize(n);
+    hc.reg.resize(3 * (size_t)n);
+    hc.club_off.assign(n + 1, 0); hc.friend_off.assign(n + 1, 0); hc.tok_off.assign((size_t)n * T + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        int s = order[i];
+        hc.uid[i] = d->user_id[s]; hc.pub[i] = d->public_flag[s]; hc.comp[i] = d->completion[s];
+        hc.gen[i] = d->gender[s]; hc.age[i] = d->age[s];
+        for (int k = 0; k < 3; ++k) hc.reg[3 * (size_t)i + k] = d->region[3 * (size_t)s + k];
+        hc.club_off[i + 1] = hc.club_off[i] + (d->club_off[s + 1] - d->club_off[s]);
+        hc.friend_off[i + 1] = hc.friend_off[i] + (d->friend_off[s + 1] - d->friend_off[s]);
+        for (int t = 0; t < T; ++t) {
+            int64_t r = (int64_t)s * T + t;
+            hc.tok_off[(size_t)i * T + t + 1] = hc.tok_off[(size_t)i * T + t] + (d->tok_off[r + 1] - d->tok_off[r]);
+        }
+    }
+    hc.clubs.resize(hc.club_off[n]); hc.friends.resize(hc.friend_off[n]);
+    hc.tid.resize(hc.tok_off[(size_t)n * T]); hc.tf.resize(hc.tok_off[(size_t)n * T]);
+    par_for(n, [&](int64_t lo, int64_t hi) {
+        std::vector<std::pair<int32_t, int32_t>> row;
+        for (int64_t i = lo; i < hi; ++i) {
+            int s = order[i];
+            if (hc.club_off[i + 1] > hc.club_off[i])
+                std::memcpy(&hc.clubs[hc.club_off[i]], d->club_ids + d->club_off[s], sizeof(uint32_t) * (hc.club_off[i + 1] - hc.club_off[i]));
+            if (hc.friend_off[i + 1] > hc.friend_off[i])
+                std::memcpy(&hc.friends[hc.friend_off[i]], d->friend_ids + d->friend_off[s], sizeof(uint32_t) * (hc.friend_off[i + 1] - hc.friend_off[i]));
+            for (int t = 0; t < T; ++t) {
+                int64_t r = (int64_t)s * T + t;
+                row.clear();
+                for (int64_t k = d->tok_off[r]; k < d->tok_off[r + 1]; ++k) row.emplace_back(d->tok_tid[k], d->tok_tf[k]);
+                std::sort(row.begin(), row.end());
+                int64_t o = hc.tok_off[(size_t)i * T + t];
+                for (size_t k = 0; k < row.size(); ++k) { hc.tid[o + k] = row[k].first; hc.tf[o + k] = row[k].second; }
+            }
+        }
+    });
+    for (int64_t r = 0; r < (int64_t)n * T; ++r)
+        for (int64_t k = hc.tok_off[r] + 1; k < hc.tok_off[r + 1]; ++k)
+            if (hc.tid[k] == hc.tid[k - 1]) { err = "duplicate token id within a (user, column) row"; return PF_EINVAL; }
+
+    // ---- IDF ------------------------------------------------------------
+    hc.idf.assign(T, {});
+    hc.has_idf.assign(T, 1);
+    if (d->idf_mode == PF_IDF_EXPLICIT) {
+        for (int t = 0; t < T; ++t) {
+            hc.has_idf[t] = d->col_has_idf ? d->col_has_idf[t] : 1;
+            if (!hc.has_idf[t] || !d->idf_off) continue;
+            for (int64_t k = d->idf_off[t]; k < d->idf_off[t + 1]; ++k) hc.idf[t][d->idf_tid[k]] = d->idf_val[k];
+        }
+    } else {
+        // recommender.cpp:43-66: df = #profiles whose column map holds the token;
+        // idf = logf(1 + N/(1+df)) in float32, N = number of loaded profiles.
+        const float N = (float)n;
+        std::vector<std::thread> ts;
+        for (int t = 0; t < T; ++t) {
+            ts.emplace_back([&, t]() {
+                int32_t mx = -1, mn = 0;
+                for (int i = 0; i < n; ++i)
+                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) {
+                        mx = std::max(mx, hc.tid[k]);
+                        mn = std::min(mn, hc.tid[k]);
+                    }
+                auto& m = hc.idf[t];
+                if (mn >= 0 && mx < (1 << 22)) {
+                    std::vector<int32_t> df((size_t)mx + 1, 0);
+                    for (int i = 0; i < n; ++i)
+                        for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) ++df[hc.tid[k]];
+                    for (int32_t k = 0; k <= mx; ++k)
+                        if (df[k]) m[k] = logf(1.0f + N / (1.0f + (float)df[k]));
+                } else {
+                    std::unordered_map<int32_t, int32_t> df;
+                    for (int i = 0; i < n; ++i)
+                        for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) ++df[hc.tid[k]];
+                    for (auto& e : df) m[e.first] = logf(1.0f + N / (1.0f + (float)e.second));
+                }
+            });
+            if ((int)ts.size() >= 16) { for (auto& x : ts) x.join(); ts.clear(); }
+        }
+        for (auto& x : ts) x.join();
+    }
+    // ---- candidate norms sqrt(sum (tf*idf)^2) per (user, col) row --------
+    hc.sqrt_nb.assign((size_t)n * T, 0.0);
+    {
+        // dense idf lookup tables where possible (the norm pass touches every token)
+        std::vector<std::vector<float>> dense(T);
+        for (int t = 0; t < T; ++t) {
+            if (!hc.has_idf[t]) continue;
+            int32_t mx = -1;
+            bool ok = true;
+            for (auto& e : hc.idf[t]) { if (e.first < 0 || e.first >= (1 << 22)) { ok = false; break; } mx = std::max(mx, e.first); }
+            if (!ok) continue;
+            dense[t].assign((size_t)mx + 1, 1.0f);
+            for (auto& e : hc.idf[t]) dense[t][e.first] = e.second;
+        }
+        par_for(n, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; ++i)
+                for (int t = 0; t < T; ++t) {
+                    size_t r = (size_t)i * T + t;
+                    double nb = 0.0;
+                    for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
+                        double idf;
+                        if (!hc.has_idf[t]) idf = 1.0;
+                        else if (!dense[t].empty() || hc.idf[t].empty())
+                            idf = (hc.tid[k] >= 0 && hc.tid[k] < (int32_t)dense[t].size()) ? dense[t][hc.tid[k]] : 1.0f;
+                        else idf = hc.idf_of(t, hc.tid[k]);
+                        double w = (double)hc.tf[k] * idf;
+                        nb += w * w;
+                    }
+                    hc.sqrt_nb[r] = std::sqrt(nb);
+                }
+        });
+    }
+    // ---- normalisers -----------------------------------------------------
+    const int K = kNumFixed + T;
+    hc.npres.assign(K, 0); hc.nmean.assign(K, 0.f); hc.nsd.assign(K, 0.f);
+    if (d->norm_present)
+        for (int k = 0; k < K; ++k) { hc.npres[k] = d->norm_present[k]; hc.nmean[k] = d->norm_mean[k]; hc.nsd[k] = d->norm_sd[k]; }
+    // ---- equality codes for public / gender ------------------------------
+    auto codes = [&](const std::vector<int32_t>& v, std::unordered_map<int32_t, uint32_t>& m) -> bool {
+        std::vector<int32_t> vals;
+        for (int32_t x : v) if (x >= 0) vals.push_back(x);
+        std::sort(vals.begin(), vals.end());
+        vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+        if (vals.size() >= kCodeMissing) return false;
+        for (size_t k = 0; k < vals.size(); ++k) m[vals[k]] = (uint32_t)k;
+        return true;
+    };
+    if (!codes(hc.pub, hc.pub_code) || !codes(hc.gen, hc.gen_code)) {
+        err = "more than 254 distinct public/gender values";
+        return PF_EUNSUPP;
+    }
+    // ---- adjacency ---------------------------------------------------------
+    hc.adj.clear();
+    if (d->n_adj > 0 && (!d->adj_uid || !d->adj_off || !d->adj_nbr)) { err = "missing adjacency arrays"; return PF_EINVAL; }
+    for (int a = 0; a < d->n_adj; ++a) {
+        auto& row = hc.adj[d->adj_uid[a]];
+        row.insert(row.end(), d->adj_nbr + d->adj_off[a], d->adj_nbr + d->adj_off[a + 1]);
+    }
+    return PF_OK;
+}
+
+void build_store(const HostCorpus& hc, HostStore& hs) {
+    const int32_t n = hc.n, T = hc.T;
+    bool packed = true;
+    for (size_t k = 0; k < hc.tid.size() && packed; ++k)
+        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kPackedTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+    hs.packed = packed;
+    // record length in words
+    std::vector<uint32_t> len(n);
+    int64_t alg = 0;
+    for (int i = 0; i < n; ++i) {
+        int64_t l = 2 + (hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]);
+        int64_t ntok = 0;
+        for (int t = 0; t < T; ++t) {
+            int64_t c = hc.tok_off[(size_t)i * T + t + 1] - hc.tok_off[(size_t)i * T + t];
+            if (c) l += 3 + c * (packed ? 1 : 2);
+            ntok += c;
+        }
+        len[i] = (uint32_t)l;
+        alg += 32 + 4 * (hc.club_off[i + 1] - hc.club_off[i]) + 4 * (hc.friend_off[i + 1] - hc.friend_off[i]) + 8 * ntok;
+    }
+    hs.alg_bytes = alg;
+    // slots: longest records first (tiles of near-equal length, little padding)
+    hs.idx_of_slot.resize(n);
+    std::iota(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), 0);
+    std::stable_sort(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), [&](int a, int b) { return len[a] > len[b]; });
+    hs.slot_of_idx.resize(n);
+    for (int p = 0; p < n; ++p) hs.slot_of_idx[hs.idx_of_slot[p]] = p;
+    const int32_t ntiles = (n + kTileSlots - 1) / kTileSlots;
+    hs.tile_off.resize(ntiles);
+    hs.tile_steps.resize(ntiles);
+    uint64_t off = 0;
+    for (int t = 0; t < ntiles; ++t) {
+        uint32_t mx = 0;
+        for (int p = t * kTileSlots; p < std::min(n, (t + 1) * kTileSlots); ++p) mx = std::max(mx, len[hs.idx_of_slot[p]]);
+        hs.tile_off[t] = off;
+        hs.tile_steps[t] = (mx + 3) / 4;
+        off += (uint64_t)hs.tile_steps[t] * kTileSlots;
+    }
+    hs.stream.assign(off, make_uint4(0, 0, 0, 0));
+    hs.hdr0.resize(n); hs.hdr1.resize(n); hs.slot_uid.resize(n); hs.slot_len.resize(n);
+    par_for(n, [&](int64_t lo, int64_t hi) {
+        std::vector<uint32_t> w;
+        for (int64_t p = lo; p < hi; ++p) {
+            int i = hs.idx_of_slot[p];
+            w.clear();
+            uint64_t mask = 0;
+            w.push_back((uint32_t)(hc.club_off[i + 1] - hc.club_off[i]));
+            for (int64_t k = hc.club_off[i]; k < hc.club_off[i + 1]; ++k) w.push_back(hc.clubs[k]);
+            w.push_back((uint32_t)(hc.friend_off[i + 1] - hc.friend_off[i]));
+            for (int64_t k = hc.friend_off[i]; k < hc.friend_off[i + 1]; ++k) w.push_back(hc.friends[k]);
+            for (int t = 0; t < T; ++t) {
+                size_t r = (size_t)i * T + t;
+                int64_t c = hc.tok_off[r + 1] - hc.tok_off[r];
+                if (!c) continue;
+                mask |= 1ull << t;
+                w.push_back((uint32_t)t | ((uint32_t)c << 8));
+                uint64_t nb;
+                std::memcpy(&nb, &hc.sqrt_nb[r], 8);
+                w.push_back((uint32_t)nb);
+                w.push_back((uint32_t)(nb >> 32));
+                for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
+                    if (packed) w.push_back((uint32_t)hc.tid[k] | ((uint32_t)hc.tf[k] << 24));
+                    else { w.push_back((uint32_t)hc.tid[k]); w.push_back((uint32_t)hc.tf[k]); }
+                }
+            }
+            const int tile = (int)(p / kTileSlots), lane = (int)(p % kTileSlots);
+            uint32_t* base = reinterpret_cast<uint32_t*>(hs.stream.data() + hs.tile_off[tile]);
+            for (size_t q = 0; q < w.size(); ++q) {
+                size_t step = q / 4, part = q % 4;
+                base[(step * kTileSlots + lane) * 4 + part] = w[q];
+            }
+            auto code = [](const std::unordered_map<int32_t, uint32_t>& m, int32_t v) -> uint32_t {
+                if (v < 0) return kCodeMissing;
+                return m.at(v);
+            };
+            hs.hdr0[p] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)hc.comp[i], (uint32_t)hc.age[i]);
+            hs.hdr1[p] = make_uint4((uint32_t)hc.reg[3 * (size_t)i], (uint32_t)hc.reg[3 * (size_t)i + 1],
+                                    (uint32_t)hc.reg[3 * (size_t)i + 2],
+                                    code(hc.pub_code, hc.pub[i]) | (code(hc.gen_code, hc.gen[i]) << 8));
+            hs.slot_uid[p] = hc.uid[i];
+            hs.slot_len[p] = (uint32_t)w.size();
+        }
+    });
+}
+
+void build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
+    const int T = hc.T;
+    QConst& c = out.c;
+    std::memset(&c, 0, sizeof c);
+    c.n_cols = T;
+    // normaliser parameters: z = (s-mean)/sd when the key exists and sd > 0, else 6(s-0.5)
+    for (int k = 0; k < kNumFixed + T; ++k) {
+        bool use = hc.npres[k] && hc.nsd[k] > 0.0f;
+        c.zmean[k] = (double)hc.nmean[k];
+        c.zsd[k] = (double)hc.nsd[k];
+        if (use) {
+            if (k < kNumFixed) c.zmode_fx |= 1u << k;
+            else if (k - kNumFixed < 32) c.zmode_lo |= 1u << (k - kNumFixed);
+            else c.zmode_hi |= 1u << (k - kNumFixed - 32);
+        }
+    }
+    auto zval = [&](int slot, double s) -> double {
+        if (hc.npres[slot] && hc.nsd[slot] > 0.0f) return (s - (double)hc.nmean[slot]) / (double)hc.nsd[slot];
+        return 6.0 * (s - 0.5);
+    };
+    auto term = [&](int slot, double s) { return ref_sigmoid(zval(slot, s)); };
+
+    c.pubcode = hc.pub[i] < 0 ? kCodeMissing : hc.pub_code.at(hc.pub[i]);
+    c.gencode = hc.gen[i] < 0 ? kCodeMissing : hc.gen_code.at(hc.gen[i]);
+    c.comp = hc.comp[i];
+    c.age = hc.age[i];
+    for (int k = 0; k < 3; ++k) c.reg[k] = hc.reg[3 * (size_t)i + k];
+    c.a_regcnt = (c.reg[0] >= 0) + (c.reg[1] >= 0) + (c.reg[2] >= 0);
+    c.n_clubs = (int32_t)(hc.club_off[i + 1] - hc.club_off[i]);
+    c.n_friends = (int32_t)(hc.friend_off[i + 1] - hc.friend_off[i]);
+    c.sqrt_clubs = std::sqrt((double)c.n_clubs);
+    c.sqrt_friends = std::sqrt((double)c.n_friends);
+    for (int e = 0; e < 2; ++e) {
+        c.sig_pub[e] = term(PF_F_PUBLIC, e ? 1.0 : 0.0);
+        c.sig_gen[e] = term(PF_F_GENDER, e ? 1.0 : 0.0);
+    }
+    for (int b = 1; b <= 3; ++b)
+        for (int m = 0; m <= 3; ++m) {
+            int a = c.a_regcnt;
+            if (a == 0) continue;
+            double s = (double)(float)((double)m / (std::sqrt((double)a) * std::sqrt((double)b)));
+            c.sig_reg[b][m] = term(PF_F_REGION, s);
+        }
+    for (int v = 1; v <= kValTab; ++v) {
+        if (c.comp > 0) {
+            int lo = std::min(c.comp, v), hi = std::max(c.comp, v);
+            c.sig_comp[v] = term(PF_F_COMPLETION, (double)lo / (double)hi);
+        }
+        if (c.age > 0) {
+            int lo = std::min(c.age, v), hi = std::max(c.age, v);
+            c.sig_age[v] = term(PF_F_AGE, (double)lo / (double)hi);
+        }
+    }
+    c.sig0_clubs = term(PF_F_CLUBS, 0.0);
+    c.sig0_friends = term(PF_F_FRIENDS, 0.0);
+    // hash entries
+    struct Ent { uint32_t tag, id, val; };
+    std::vector<Ent> ents;
+    std::vector<uint32_t> tmp(hc.clubs.begin() + hc.club_off[i], hc.clubs.begin() + hc.club_off[i + 1]);
+    std::sort(tmp.begin(), tmp.end());
+    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+    for (uint32_t x : tmp) ents.push_back({kTagClubs, x, 0});
+    tmp.assign(hc.friends.begin() + hc.friend_off[i], hc.friends.begin() + hc.friend_off[i + 1]);
+    std::sort(tmp.begin(), tmp.end());
+    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+    for (uint32_t x : tmp) ents.push_back({kTagFriends, x, 0});
+    out.vals.clear();
+    c.colmask = 0;
+    for (int t = 0; t < T; ++t) {
+        size_t r = (size_t)i * T + t;
+        c.sig0_col[t] = term(kNumFixed + t, 0.0);
+        c.sqrt_na[t] = hc.sqrt_nb[r];
+        if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
+        c.colmask |= 1ull << t;
+        for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
+            double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;
+            QVal v;
+            v.wq = (double)hc.tf[k] * idf;
+            v.idf = idf;
+            ents.push_back({(uint32_t)t, (uint32_t)hc.tid[k], (uint32_t)out.vals.size()});
+            out.vals.push_back(v);
+        }
+    }
+    if (excl) {
+        tmp.assign(excl->begin(), excl->end());
+        std::sort(tmp.begin(), tmp.end());
+        tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+        for (uint32_t x : tmp) ents.push_back({kTagExcl, x, 0});
+    }
+    uint32_t cap = next_pow2(std::max<uint32_t>(16, 2 * (uint32_t)ents.size()));
+    int lg = 0;
+    while ((1u << lg) < cap) ++lg;
+    c.cap_log2 = lg;
+    c.n_vals = (int32_t)out.vals.size();
+    out.keys.assign(cap, kEmptyKey);
+    for (const Ent& e : ents) {
+        uint32_t s = hash_key(e.tag, e.id) & (cap - 1);
+        while (out.keys[s] != kEmptyKey) s = (s + 1) & (cap - 1);
+        out.keys[s] = make_key(e.tag, e.id) | ((uint64_t)e.val << 40);
+    }
+}
+
+}  // namespace pf

@@ -1,0 +1,63 @@
+// pf_store.h — host-side corpus model and device-layout builder.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pf_types.h"
+
+namespace pf {
+
+// Host copy of the corpus in candidate-index order (idx = rank of uid,
+// ascending, so idx order is the reference's tie-break order).
+struct HostCorpus {
+    int32_t n = 0, T = 0;
+    std::vector<int32_t> uid, pub, comp, gen, age, reg;  // reg: 3 per user
+    std::vector<int64_t> club_off, friend_off, tok_off;  // tok_off: n*T+1, rows sorted by tid
+    std::vector<uint32_t> clubs, friends;
+    std::vector<int32_t> tid, tf;
+    std::vector<double> sqrt_nb;                         // per (user, col) row
+    std::vector<uint8_t> has_idf;                        // per column
+    std::vector<std::unordered_map<int32_t, float>> idf; // per column
+    std::vector<uint8_t> npres;                          // 7 + T
+    std::vector<float> nmean, nsd;
+    std::unordered_map<int32_t, uint32_t> pub_code, gen_code;
+    // live adjacency (adj_list), mutable through pf_set_adj
+    std::unordered_map<int32_t, std::vector<int32_t>> adj;
+
+    int32_t idx_of(int32_t u) const;   // -1 when uid has no profile
+    float idf_of(int t, int32_t tid) const;  // 1.0 for absent token; NaN if no idf map
+};
+
+struct HostStore {
+    std::vector<uint4> stream;
+    std::vector<uint64_t> tile_off;
+    std::vector<uint32_t> tile_steps;
+    std::vector<uint4> hdr0, hdr1;
+    std::vector<int32_t> slot_uid;
+    std::vector<uint32_t> slot_len;
+    std::vector<int32_t> slot_of_idx;
+    std::vector<int32_t> idx_of_slot;
+    bool packed = true;
+    int64_t alg_bytes = 0;    // SURVEY 8(d) D3 accounting
+};
+
+// Query image (A side).  keys: 1 << cap_log2 slots; vals: token values.
+struct QImageHost {
+    QConst c;
+    std::vector<uint64_t> keys;
+    std::vector<QVal> vals;
+};
+
+int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err);
+void build_store(const HostCorpus& hc, HostStore& hs);
+// excl: uids to exclude (all-candidates mode), may be null
+void build_query(const HostCorpus& hc, int32_t idx, const std::vector<int32_t>* excl, QImageHost& out);
+
+// exact reference arithmetic on the host (glibc exp)
+double ref_sigmoid(double x);
+
+}  // namespace pf

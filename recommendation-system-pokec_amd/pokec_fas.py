@@ -1,0 +1,203 @@
+"""Python binding of the MI355X FAS engine (ctypes over libpokec_fas.so, the C ABI
+of include/pokec_fas.h).
+
+Mirrors the reference's `Recommender` operator surface (include/recommender.h:17-71)
+with the same names, argument meaning and error behaviour: an unknown user yields an
+empty list (recommender_graph.cpp:36-40), results are [(id, score)] sorted by
+(score desc, id asc).  The library is loaded from this directory (built in-tree by
+`make -C recommendation-system-pokec_amd`); if it or a gfx950 GPU is missing, opening
+an engine raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpokec_fas.so")
+
+PF_OK, PF_EINVAL, PF_ENODEV, PF_ENOMEM, PF_ENOTFOUND, PF_EUNSUPP = 0, -1, -2, -3, -4, -5
+PF_MODE_FOF, PF_MODE_ALL = 0, 1
+PF_FOF_GRAPH, PF_FOF_COLLAB = 0, 1
+MAX_TOPK_DEVICE = 64
+
+# every entry point of include/pokec_fas.h
+EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_users", "pf_idf", "pf_fas_pairs",
+           "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
+           "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
+           "pf_last_scan_ms"]
+
+
+class PfLayoutStats(ctypes.Structure):
+    _fields_ = [("n_slots", ctypes.c_int64), ("stream_bytes", ctypes.c_int64), ("header_bytes", ctypes.c_int64),
+                ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32)]
+
+
+class FasError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libpokec_fas.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FasError(f"{LIB_PATH} missing: build it with `make -C {HERE}` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        V, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.pf_abi_version.restype = ctypes.c_int
+        L.pf_open.argtypes = [V, ctypes.c_int, ctypes.POINTER(V)]
+        L.pf_close.argtypes = [V]
+        L.pf_last_error.argtypes = [V]
+        L.pf_last_error.restype = ctypes.c_char_p
+        L.pf_num_users.argtypes = [V]
+        L.pf_num_users.restype = I32
+        L.pf_idf.argtypes = [V, I32, I32]
+        L.pf_idf.restype = ctypes.c_float
+        L.pf_fas_pairs.argtypes = [V, V, V, I64, V]
+        L.pf_recommend_interest.argtypes = [V, V, I32, I32, I32, I32, V, V, V]
+        L.pf_recommend_collab.argtypes = [V, V, I32, I32, I32, V, V, V]
+        L.pf_recommend_clubs.argtypes = [V, V, I32, I32, I32, V, V, V]
+        L.pf_fof_candidates.argtypes = [V, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_set_adj.argtypes = [V, I32, V, I32]
+        L.pf_set_shard.argtypes = [V, I32, I32]
+        L.pf_scan_keys_async.argtypes = [V, V, I32, I32, V, V]
+        L.pf_merge_keys_async.argtypes = [V, V, I32, I32, I32, V, V]
+        L.pf_decode_keys.argtypes = [V, I32, V, V, V]
+        L.pf_decode_keys.restype = None
+        L.pf_layout.argtypes = [V, ctypes.POINTER(PfLayoutStats)]
+        L.pf_last_scan_ms.argtypes = [V]
+        L.pf_last_scan_ms.restype = ctypes.c_float
+        _lib = L
+    return _lib
+
+
+def _i32(a):
+    return np.ascontiguousarray(np.atleast_1d(np.asarray(a)), dtype=np.int32)
+
+
+class FasEngine:
+    """One device context (pf_ctx) over an in-memory corpus (a pf_corpus_desc pointer)."""
+
+    def __init__(self, desc_ptr, device=0):
+        L = lib()
+        self._L = L
+        self.h = ctypes.c_void_p()
+        rc = L.pf_open(desc_ptr, device, ctypes.byref(self.h))
+        if rc != PF_OK:
+            raise FasError(f"pf_open failed ({rc}): {L.pf_last_error(None).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.pf_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != PF_OK:
+            raise FasError(f"{what} failed ({rc}): {self._L.pf_last_error(self.h).decode()}")
+
+    @property
+    def num_users(self):
+        return self._L.pf_num_users(self.h)
+
+    def idf(self, col, tid):
+        return self._L.pf_idf(self.h, col, tid)
+
+    def layout(self):
+        s = PfLayoutStats()
+        self._check(self._L.pf_layout(self.h, ctypes.byref(s)), "pf_layout")
+        return s
+
+    # -- profile_similarity (recommender_similarity.cpp:10-124), batched
+    def fas_pairs(self, a_uid, b_uid):
+        a, b = _i32(a_uid), _i32(b_uid)
+        out = np.empty(len(a), np.float32)
+        self._check(self._L.pf_fas_pairs(self.h, a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data),
+                    "pf_fas_pairs")
+        return out
+
+    def _topk(self, fn, users, topk, *extra):
+        q = _i32(users)
+        k = max(int(topk), 0)
+        ou = np.zeros(max(len(q) * k, 1), np.int32)
+        os_ = np.zeros(max(len(q) * k, 1), np.float32)
+        oc = np.zeros(max(len(q), 1), np.int32)
+        self._check(getattr(self._L, fn)(self.h, q.ctypes.data, len(q), k, *extra, ou.ctypes.data,
+                                         os_.ctypes.data, oc.ctypes.data), fn)
+        return [(ou[i * k:i * k + oc[i]].copy(), os_[i * k:i * k + oc[i]].copy()) for i in range(len(q))]
+
+    # -- Recommender surface (include/recommender.h:24-35); batched over users
+    def recommend_interest(self, users, topk, mode=PF_MODE_FOF, candidate_limit=10000):
+        return self._topk("pf_recommend_interest", users, topk, mode, candidate_limit)
+
+    def recommend_collaborative(self, users, topk, candidate_limit=10000):
+        return self._topk("pf_recommend_collab", users, topk, candidate_limit)
+
+    def recommend_clubs_collab(self, users, topk, candidate_limit=10000):
+        return self._topk("pf_recommend_clubs", users, topk, candidate_limit)
+
+    def recommend_graph_registration(self, users, topk, candidate_limit=10000):
+        return self.recommend_interest(users, topk, PF_MODE_FOF, candidate_limit)
+
+    recommend_by_interest = recommend_graph_registration
+    recommend_friends_graph = recommend_graph_registration
+    recommend_friends_by_interest = recommend_graph_registration
+    recommend_friends_collab = recommend_collaborative
+
+    def recommend_interest_all(self, users, topk):
+        """All-candidates interest scan."""
+        return self.recommend_interest(users, topk, PF_MODE_ALL, 0)
+
+    def fof_candidates(self, uid, limit, flavour=PF_FOF_GRAPH):
+        cap = max(int(limit), 1) + 1
+        out = np.zeros(cap, np.int32)
+        n = ctypes.c_int32()
+        self._check(self._L.pf_fof_candidates(self.h, uid, limit, flavour, out.ctypes.data, cap, ctypes.byref(n)),
+                    "pf_fof_candidates")
+        return out[:min(n.value, cap)].copy()
+
+    def set_adj(self, uid, nbrs):
+        if nbrs is None:
+            self._check(self._L.pf_set_adj(self.h, uid, None, -1), "pf_set_adj")
+        else:
+            a = _i32(nbrs) if len(nbrs) else np.zeros(1, np.int32)
+            self._check(self._L.pf_set_adj(self.h, uid, a.ctypes.data, len(nbrs)), "pf_set_adj")
+
+    def set_shard(self, shard, nshards):
+        self._check(self._L.pf_set_shard(self.h, shard, nshards), "pf_set_shard")
+
+    # -- device-resident scan for multi-GPU benches (d_keys: device pointer, int)
+    def scan_keys_async(self, users, topk, d_keys_ptr, stream_ptr=None):
+        q = _i32(users)
+        self._check(self._L.pf_scan_keys_async(self.h, q.ctypes.data, len(q), topk, ctypes.c_void_p(d_keys_ptr),
+                                               ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+                    "pf_scan_keys_async")
+
+    def merge_keys_async(self, d_parts_ptr, nparts, nq, topk, d_out_ptr, stream_ptr=None):
+        self._check(self._L.pf_merge_keys_async(self.h, ctypes.c_void_p(d_parts_ptr), nparts, nq, topk,
+                                                ctypes.c_void_p(d_out_ptr),
+                                                ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+                    "pf_merge_keys_async")
+
+    @property
+    def last_scan_ms(self):
+        return self._L.pf_last_scan_ms(self.h)
+
+
+def decode_keys(keys):
+    """Packed 64-bit keys (numpy uint64, one query) -> (uids, scores)."""
+    keys = np.ascontiguousarray(keys, np.uint64)
+    ou = np.zeros(len(keys), np.int32)
+    os_ = np.zeros(len(keys), np.float32)
+    n = ctypes.c_int32()
+    lib().pf_decode_keys(keys.ctypes.data, len(keys), ou.ctypes.data, os_.ctypes.data, ctypes.byref(n))
+    return ou[:n.value], os_[:n.value]

@@ -437,3 +437,21 @@ class Oracle:
         m = np.zeros(5, np.float64)
         self.L.ro_recommendation_tests(self.h, sample, topk, m.ctypes.data)
         return m
+
+
+# ------------------------------------------------------------------ product
+PKG = os.path.join(ROOT, "recommendation-system-pokec_amd")
+
+
+def product():
+    """The product's Python binding (recommendation-system-pokec_amd/pokec_fas.py)."""
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    import pokec_fas  # noqa: E402
+    return pokec_fas
+
+
+def engine(corpus_or_ptr):
+    pf = product()
+    ptr = corpus_or_ptr if isinstance(corpus_or_ptr, int) else corpus_or_ptr.desc_ptr()
+    return pf.FasEngine(ptr, 0)

@@ -1,0 +1,121 @@
+"""GPU parity: the HIP FAS engine (through the C ABI) against golden vectors from the
+real reference and against the oracle on larger seeded corpora.
+
+Bar (BASELINE.json north_star): top-k ids and 2-hop lists bit-exact; FAS floats within
+1e-5 (we additionally require bit-exact floats on the golden fixtures, and report the
+mismatch count if any)."""
+import numpy as np
+import pytest
+
+import pokec_testlib as tl
+
+pytestmark = pytest.mark.gpu
+FAS_TOL = 1e-5
+
+
+@pytest.fixture(scope="module", params=["A", "B"])
+def gold(request):
+    name = request.param
+    corpus = tl.golden_corpus(name)
+    return name, corpus, tl.engine(corpus)
+
+
+def test_idf_matches_reference(gold):
+    name, corpus, eng = gold
+    N, rows = tl.golden_idf(name)
+    got = np.array([np.float32(eng.idf(t, k)).view(np.uint32) for t, k, _ in rows], np.uint32)
+    assert np.array_equal(got, np.array([h for _, _, h in rows], np.uint32))
+
+
+def test_fas_pairs_match_reference(gold):
+    name, corpus, eng = gold
+    a, b, s = tl.golden_pairs(name)
+    got = eng.fas_pairs(a, b)
+    ref = s.view(np.float32)
+    assert np.all(np.abs(got - ref) <= FAS_TOL)
+    nbad = int(np.count_nonzero(got.view(np.uint32) != s))
+    assert nbad == 0, f"{nbad}/{len(s)} FAS floats not bit-identical"
+
+
+def _check_lists(got, items, ctx):
+    ids, sc = got
+    assert list(ids) == [x for x, _ in items], ctx
+    assert list(sc.view(np.uint32)) == [h for _, h in items], ctx
+
+
+def test_recommenders_match_reference(gold):
+    name, corpus, eng = gold
+    g = tl.golden_lists(name, "recs.txt")
+    for (tag, uid, k, lim), items in g.items():
+        kk = min(k, 100000)
+        if tag in ("graph", "interest"):
+            got, = eng.recommend_interest([uid], kk, tl.PF_MODE_FOF, lim)
+        elif tag == "collab":
+            got, = eng.recommend_collaborative([uid], kk, lim)
+        else:
+            got, = eng.recommend_clubs_collab([uid], kk, lim)
+        _check_lists(got, items, (tag, uid, k, lim))
+
+
+def test_all_candidates_scan_matches_reference(gold):
+    name, corpus, eng = gold
+    g = tl.golden_lists(name, "all.txt")
+    keys = list(g.keys())
+    uids = [k[1] for k in keys]
+    got = eng.recommend_interest_all(uids, 50)
+    for key, res in zip(keys, got):
+        _check_lists(res, g[key], key)
+    # top-10 is the prefix of top-50 (same comparator)
+    got10 = eng.recommend_interest_all(uids, 10)
+    for key, res in zip(keys, got10):
+        _check_lists(res, g[key][:10], key)
+
+
+def test_fof_gathers_match_oracle(gold):
+    name, corpus, eng = gold
+    orc = tl.Oracle(corpus)
+    for uid in list(corpus.uid[::37]) + [-5]:
+        for lim in (0, 1, 5, 100, 5000):
+            for fl in (tl.PF_FOF_GRAPH, tl.PF_FOF_COLLAB):
+                assert list(eng.fof_candidates(int(uid), lim, fl)) == list(orc.fof(int(uid), lim, fl))
+
+
+@pytest.fixture(scope="module")
+def big():
+    """20k users, edge cases on, generated in memory (no reference files)."""
+    c = tl.synth.Corpus(n_users=20000, seed=77, edge_cases=1)
+    ptr = c.desc_ptr()
+    return c, tl.engine(ptr), tl.Oracle(None, desc_ptr=ptr)
+
+
+def test_big_all_candidates_vs_oracle(big):
+    c, eng, orc = big
+    rng = np.random.default_rng(5)
+    q = [int(x) for x in rng.integers(1, 20001, 12)] + [8, 1]
+    got = eng.recommend_interest_all(q, 10)
+    ref = orc.interest(q, 10, tl.PF_MODE_ALL, 0)
+    for u, g, r in zip(q, got, ref):
+        assert list(g[0]) == list(r[0]), u
+        assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def test_big_pairs_vs_oracle(big):
+    c, eng, orc = big
+    rng = np.random.default_rng(9)
+    a = rng.integers(1, 20001, 100000).astype(np.int32)
+    b = rng.integers(1, 20001, 100000).astype(np.int32)
+    g, r = eng.fas_pairs(a, b), orc.fas_pairs(a, b)
+    assert np.all(np.abs(g - r) <= FAS_TOL)
+    assert int(np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))) == 0
+
+
+def test_big_collab_and_clubs_vs_oracle(big):
+    c, eng, orc = big
+    q = [3, 8, 1000, 15000, 19999]
+    for u in q:
+        g, = eng.recommend_collaborative([u], 10, 1000)
+        r, = orc.collab([u], 10, 1000)
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+        g, = eng.recommend_clubs_collab([u], 20, 5000)
+        r, = orc.clubs([u], 20, 5000)
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u

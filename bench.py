@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""FAS all-candidates scan benchmark (BASELINE.json metric: "FAS candidates scored/sec
+over 1.6M users, top-k=10; 1/2/4/8 GPU + %HBM peak").
+
+Workload (BASELINE.json configs[1]): synthetic Pokec-shaped corpus of
+1,632,803 users (seeded generator tools/pokec_synth.cpp, resident in HBM), interest FAS
+top-10 over every candidate (A13).  One step = one all-candidates pass for a batch of
+queries: at N GPUs the batch holds N distinct query users (1 at N=1, i.e. exactly
+config 2), every rank scores its candidate shard (1/N of the corpus, split by stream
+bytes) for the whole batch, the per-shard top-10 keys are exchanged with one RCCL
+all-gather over xGMI and merged on device.  Per-GPU work is fixed (1.6M pairs/step):
+weak scaling.  value = candidates scored / s over the whole job.
+
+Also reports the roofline of the dominant kernel (fas_scan_kernel, HIP events around
+every launch) and the CPU baseline (oracle/refcpu.cpp, the reference algorithm with its
+unordered_map data structures, single thread, bounded sample of the same corpus).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "recommendation-system-pokec_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+N_USERS = 1632803
+TOPK = 10
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "FAS candidates scored/sec over 1.6M users, top-k=10; 1/2/4/8 GPU + %HBM peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(desc_ptr, seconds_budget=12.0):
+    """Oracle (reference algorithm, unordered_map per profile/column) on one core over a
+    bounded prefix of the same corpus: all-candidates interest top-10 per query."""
+    import pokec_testlib as tl
+    sample_users = 150000
+    t0 = time.time()
+    orc = tl.Oracle(None, max_users=sample_users, desc_ptr=desc_ptr)
+    build_s = time.time() - t0
+    rng = np.random.default_rng(123)
+    done, cands, el = 0, 0, 0.0
+    while el < seconds_budget and done < 64:
+        q = int(rng.integers(1, sample_users + 1))
+        t = time.perf_counter()
+        orc.interest([q], TOPK, tl.PF_MODE_ALL, 0)
+        el += time.perf_counter() - t
+        cands += orc.L.ro_num_users(orc.h) - 1
+        done += 1
+    orc.close()
+    return {"value": cands / el, "unit": "candidates/s", "cores": 1, "kind": "port",
+            "sample": f"{done} all-candidates interest top-10 queries over the first {sample_users} users of the "
+                      f"same synthetic corpus (oracle/refcpu.cpp, single thread, {el:.1f}s timed, "
+                      f"{build_s:.1f}s map build untimed)"}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC pass (profiles/pmc_*.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(workload)
+        return None if e is None else float(e["bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--users", type=int, default=N_USERS)
+    ap.add_argument("--queries-per-gpu", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import synth
+    import pokec_fas as pf
+
+    t0 = time.time()
+    corpus = synth.Corpus(n_users=args.users, seed=1, edge_cases=0, threads=16)
+    desc = corpus.desc_ptr()
+    t1 = time.time()
+    eng = pf.FasEngine(desc, local)
+    t2 = time.time()
+    eng.set_shard(rank, world)
+    lay = eng.layout()
+    log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t2 - t1:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
+        f"alg {lay.alg_bytes / 1e9:.3f} GB, packed={lay.packed_tokens}")
+
+    Q = world * args.queries_per_gpu
+    k = TOPK
+    steps, warm = args.steps, args.warmup
+    rng = np.random.default_rng(2)  # same query stream on every rank
+    qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    local_keys = torch.empty((Q, k), dtype=torch.int64, device="cuda")
+    gathered = torch.empty((world, Q, k), dtype=torch.int64, device="cuda") if world > 1 else None
+    final = torch.empty((Q, k), dtype=torch.int64, device="cuda")
+
+    def step(i):
+        eng.scan_keys_async(qstream[i], k, local_keys.data_ptr(), sptr)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_keys)
+            eng.merge_keys_async(gathered.data_ptr(), world, Q, k, final.data_ptr(), sptr)
+        else:
+            final.copy_(local_keys)
+
+    for i in range(warm):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.profile_reset()
+    t_start = time.perf_counter()
+    for i in range(warm, warm + steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    scan_ms, launches = eng.profile_read()
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: the merged top-k of the last step rescored by the pair kernel
+    last = final.cpu().numpy().view(np.uint64)
+    uids, scores = pf.decode_keys(last[0])
+    chk = eng.fas_pairs(np.full(len(uids), qstream[warm + steps - 1][0], np.int32), uids)
+    consistent = bool(len(uids) == k and np.array_equal(chk.view(np.uint32), scores.view(np.uint32)))
+
+    n_cand = eng.num_users - 1  # candidates per query: every profile but the query (minus adj[q])
+    value = Q * n_cand * steps / elapsed
+    avg_launch_ms = scan_ms / max(launches, 1)
+    # algorithmic bytes per launch: SURVEY 8(d) D3 b_c summed over this rank's shard, x queries per launch
+    shard_frac = 1.0 / world
+    alg_bytes = lay.alg_bytes * shard_frac * Q
+    achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
+    workload = f"cfg2_all_candidates_top{k}_{args.users}users_q{Q}_shard1of{world}"
+    traffic = pmc_traffic(workload)
+    rec = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": elapsed * 1e3 / steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
+        "config": {"workload": "cfg2: full 1.6M-user single-query interest FAS all-candidates top-10"
+                               + ("" if world == 1 else f"; {Q} queries/step, candidates sharded over {world} GPUs, "
+                                                        "RCCL all-gather of per-shard top-10"),
+                   "n_users": args.users, "queries_per_step": Q, "topk": k,
+                   "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "fas_scan_kernel", "avg_launch_ms": avg_launch_ms,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "stream_bytes_per_launch": (lay.stream_bytes + lay.header_bytes) * shard_frac * Q},
+        "topk_selfcheck": consistent,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(desc)
+        rec["cpu_baseline"] = base
+        rec["speedup_vs_cpu"] = value / base["value"]
+    elif rank == 0:
+        rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -208,9 +208,13 @@ typedef struct pf_layout_stats {
 } pf_layout_stats;
 int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
 
-/* Average device time (ms) of the last pf_scan_keys_async/_interest ALL call's
- * scan kernel, measured with HIP events on the context stream. */
+/* Device time (ms) of the last all-candidates scan kernel (HIP events on the
+ * stream it was launched on). */
 float pf_last_scan_ms(const pf_ctx* ctx);
+/* Per-launch timing of the scan kernel over a region: reset, run, then read the
+ * summed device time of every scan launch since the reset (synchronises). */
+int pf_profile_reset(pf_ctx* ctx);
+int pf_profile_read(pf_ctx* ctx, double* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

@@ -58,13 +58,13 @@ struct pf_ctx {
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, last_ev0 = nullptr, last_ev1 = nullptr;
     float last_scan_ms = 0.f;
     std::string err;
     pf::HostCorpus hc;
     pf::HostStore hs;       // metadata only after upload (stream freed)
-    int64_t stream_bytes = 0;
-    DBuf d_stream, d_tile_off, d_tile_steps, d_hdr0, d_hdr1, d_slot_uid, d_slot_len;
+    int64_t stream_bytes = 0, norm_bytes = 0;
+    DBuf d_stream, d_tile_off, d_tile_steps, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
     pf::DevStore ds{};
     // workspaces
     DBuf d_pool, d_refs, d_part, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum;
@@ -73,6 +73,10 @@ struct pf_ctx {
     std::vector<uint8_t> h_pool;
     std::vector<pf::QImageRef> h_refs;
     std::vector<int32_t> h_rows;
+    // scan-kernel timing pool (pf_profile_*)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+    size_t prof_used = 0;
+    bool prof_on = false;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -104,8 +108,12 @@ hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 struct Images {
     std::vector<uint8_t> pool;
     std::vector<pf::QImageRef> refs;
-    uint32_t max_lds = sizeof(pf::QConst) + 2048;
+    uint32_t max_lds = 0;  // dynamic LDS a 256-thread block needs for the largest image
+    bool gtab = false;     // some image probes its table in global memory
 };
+
+constexpr uint32_t kStageLimit = 48 * 1024;   // keys+vals above this are probed in global memory
+constexpr uint32_t kBlockThreads = 256;
 
 void add_image(Images& im, const pf::QImageHost& q) {
     auto align = [&](size_t a) { while (im.pool.size() % a) im.pool.push_back(0); };
@@ -121,9 +129,11 @@ void add_image(Images& im, const pf::QImageHost& q) {
     r.vals_off = (uint32_t)im.pool.size();
     const uint8_t* vp = reinterpret_cast<const uint8_t*>(q.vals.data());
     im.pool.insert(im.pool.end(), vp, vp + q.vals.size() * sizeof(pf::QVal));
-    size_t lds = sizeof(pf::QConst) + q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal) + 2048;
-    r.lds_bytes = lds <= kLdsLimit ? (uint32_t)lds : 0u;
-    im.max_lds = std::max<uint32_t>(im.max_lds, r.lds_bytes);
+    const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
+    r.lds_bytes = kv <= kStageLimit ? (uint32_t)kv : 0u;
+    im.gtab = im.gtab || r.lds_bytes == 0;
+    const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads * 8u + 2048u;
+    im.max_lds = std::max(im.max_lds, need);
     im.refs.push_back(r);
 }
 
@@ -178,7 +188,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
     for (size_t g = 0; g < qidx.size(); ++g) {
         out[g].assign(slots[g].size(), 0.f);
         if (slots[g].empty()) continue;
-        pf::build_query(c->hc, qidx[g], nullptr, qi);
+        if (!pf::build_query(c->hc, qidx[g], nullptr, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
         const int32_t img = (int32_t)im.refs.size();
         add_image(im, qi);
         for (size_t b = 0; b < slots[g].size(); b += 256) {
@@ -193,7 +203,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
     HIPCHK(c, upload(c, c->d_blocks, blocks));
     HIPCHK(c, upload(c, c->d_slots, flat));
     HIPCHK(c, c->d_scores.ensure(flat.size() * sizeof(float)));
-    HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds,
+    HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
                                c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
                                c->d_scores.as<float>(), c->stream));
     std::vector<float> res(flat.size());
@@ -227,7 +237,7 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         auto it = c->hc.adj.find(u);
         if (it != c->hc.adj.end()) excl = it->second;
         excl.push_back(u);
-        pf::build_query(c->hc, i, &excl, qi);
+        if (!pf::build_query(c->hc, i, &excl, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
         add_image(im, qi);
     }
     const int nq = (int)idx.size();
@@ -244,10 +254,32 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     HIPCHK(c, c->d_rows.ensure(c->h_rows.size() * sizeof(int32_t)));
     HIPCHK(c, hipMemcpyAsync(c->d_rows.p, c->h_rows.data(), c->h_rows.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
     HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
-    if (timed) HIPCHK(c, hipEventRecord(c->ev0, s));
-    HIPCHK(c, pf::launch_scan(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), c->h_refs.data(), nq,
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (c->prof_on) {
+        if (c->prof_used == c->prof_ev.size()) {
+            hipEvent_t a, b;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b));
+            c->prof_ev.emplace_back(a, b);
+        }
+        e0 = c->prof_ev[c->prof_used].first;
+        e1 = c->prof_ev[c->prof_used].second;
+        ++c->prof_used;
+        timed = true;
+    }
+    if (timed) HIPCHK(c, hipEventRecord(e0, s));
+    const uint32_t lds = im.max_lds;
+    const bool gtab = im.gtab;
+    HIPCHK(c, pf::launch_scan(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), lds, gtab, nq,
                               c->tile_begin, c->tile_end, k, blocks, c->d_part.as<uint64_t>(), s));
-    if (timed) HIPCHK(c, hipEventRecord(c->ev1, s));
+    if (timed) HIPCHK(c, hipEventRecord(e1, s));
+    if (timed && e0 != c->ev0) {  // keep pf_last_scan_ms meaningful in profiling mode
+        c->last_ev0 = e0;
+        c->last_ev1 = e1;
+    } else if (timed) {
+        c->last_ev0 = c->ev0;
+        c->last_ev1 = c->ev1;
+    }
     HIPCHK(c, pf::launch_merge(c->d_part.as<uint64_t>(), blocks, k, (int64_t)blocks * k, nq, k, d_keys,
                                c->d_rows.as<int32_t>(), s));
     return PF_OK;
@@ -286,7 +318,8 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     }
     int rc = pf::build_host_corpus(desc, c->hc, c->err);
     if (rc != PF_OK) return bail(rc);
-    pf::build_store(c->hc, c->hs);
+    rc = pf::build_store(c->hc, c->hs, c->err);
+    if (rc != PF_OK) return bail(rc);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         c->err = "stream/event creation failed";
@@ -297,24 +330,28 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     if (e == hipSuccess) e = upload(c, c->d_stream, hs.stream);
     if (e == hipSuccess) e = upload(c, c->d_tile_off, hs.tile_off);
     if (e == hipSuccess) e = upload(c, c->d_tile_steps, hs.tile_steps);
+    if (e == hipSuccess) e = upload(c, c->d_norms, hs.norms);
+    if (e == hipSuccess) e = upload(c, c->d_norm_off, hs.norm_off);
     if (e == hipSuccess) e = upload(c, c->d_hdr0, hs.hdr0);
     if (e == hipSuccess) e = upload(c, c->d_hdr1, hs.hdr1);
-    if (e == hipSuccess) e = upload(c, c->d_slot_uid, hs.slot_uid);
-    if (e == hipSuccess) e = upload(c, c->d_slot_len, hs.slot_len);
+    if (e == hipSuccess) e = upload(c, c->d_hdr2, hs.hdr2);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         c->hip_fail(e, "corpus upload");
         return bail(e == hipErrorOutOfMemory ? PF_ENOMEM : PF_ENODEV);
     }
     c->stream_bytes = (int64_t)hs.stream.size() * 16;
+    c->norm_bytes = (int64_t)hs.norms.size() * 8;
     std::vector<uint4>().swap(hs.stream);
+    std::vector<double>().swap(hs.norms);
     c->ds.stream = c->d_stream.as<uint4>();
     c->ds.tile_off = c->d_tile_off.as<uint64_t>();
     c->ds.tile_steps = c->d_tile_steps.as<uint32_t>();
+    c->ds.norms = c->d_norms.as<double>();
+    c->ds.norm_off = c->d_norm_off.as<uint64_t>();
     c->ds.hdr0 = c->d_hdr0.as<uint4>();
     c->ds.hdr1 = c->d_hdr1.as<uint4>();
-    c->ds.slot_uid = c->d_slot_uid.as<int32_t>();
-    c->ds.slot_len = c->d_slot_len.as<uint32_t>();
+    c->ds.hdr2 = c->d_hdr2.as<uint4>();
     c->ds.n_slots = c->hc.n;
     c->ds.n_tiles = (int32_t)hs.tile_steps.size();
     c->ds.packed = hs.packed ? 1 : 0;
@@ -329,6 +366,7 @@ void pf_close(pf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -394,7 +432,7 @@ int pf_recommend_interest(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk,
         std::vector<uint64_t> keys((size_t)nq * topk);
         HIPCHK(c, hipMemcpyAsync(keys.data(), c->d_out.p, keys.size() * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (!idx.empty()) HIPCHK(c, hipEventElapsedTime(&c->last_scan_ms, c->ev0, c->ev1));
+        if (!idx.empty() && c->last_ev0) HIPCHK(c, hipEventElapsedTime(&c->last_scan_ms, c->last_ev0, c->last_ev1));
         for (int i = 0; i < nq; ++i) pf_decode_keys(&keys[(size_t)i * topk], topk, ou + (size_t)i * topk, os + (size_t)i * topk, &oc[i]);
         return PF_OK;
     }
@@ -673,13 +711,40 @@ int pf_layout(const pf_ctx* c, pf_layout_stats* o) {
     if (!c || !o) return PF_EINVAL;
     o->n_slots = c->hc.n;
     o->stream_bytes = c->stream_bytes;
-    o->header_bytes = (int64_t)c->hc.n * 32;
+    o->header_bytes = (int64_t)c->hc.n * 48;
     o->alg_bytes = c->hs.alg_bytes;
     o->packed_tokens = c->hs.packed ? 1 : 0;
     o->n_tiles = (int32_t)c->hs.tile_steps.size();
     return PF_OK;
 }
 
-float pf_last_scan_ms(const pf_ctx* c) { return c ? c->last_scan_ms : 0.f; }
+float pf_last_scan_ms(const pf_ctx* c) {
+    if (!c) return 0.f;
+    float ms = c->last_scan_ms;
+    if (c->last_ev1 && hipEventSynchronize(c->last_ev1) == hipSuccess)
+        (void)hipEventElapsedTime(&ms, c->last_ev0, c->last_ev1);
+    return ms;
+}
+
+int pf_profile_reset(pf_ctx* c) {
+    if (!c) return PF_EINVAL;
+    c->prof_on = true;
+    c->prof_used = 0;
+    return PF_OK;
+}
+
+int pf_profile_read(pf_ctx* c, double* total_ms, int64_t* launches) {
+    if (!c || !total_ms || !launches) return PF_EINVAL;
+    double tot = 0.0;
+    for (size_t i = 0; i < c->prof_used; ++i) {
+        HIPCHK(c, hipEventSynchronize(c->prof_ev[i].second));
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->prof_ev[i].first, c->prof_ev[i].second));
+        tot += ms;
+    }
+    *total_ms = tot;
+    *launches = (int64_t)c->prof_used;
+    return PF_OK;
+}
 
 }  // extern "C"

@@ -28,11 +28,6 @@ void par_for(int64_t n, F f) {
     for (auto& t : ts) t.join();
 }
 
-uint32_t next_pow2(uint32_t v) {
-    uint32_t p = 1;
-    while (p < v) p <<= 1;
-    return p;
-}
 
 }  // namespace
 
@@ -215,28 +210,29 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
     return PF_OK;
 }
 
-void build_store(const HostCorpus& hc, HostStore& hs) {
+int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     const int32_t n = hc.n, T = hc.T;
     bool packed = true;
     for (size_t k = 0; k < hc.tid.size() && packed; ++k)
-        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kPackedTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+    if (!packed)
+        for (size_t k = 0; k < hc.tf.size(); ++k)
+            if (hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23)) { err = "token count outside [-2^23, 2^23)"; return PF_EUNSUPP; }
     hs.packed = packed;
-    // record length in words
-    std::vector<uint32_t> len(n);
+    // record length in words: clubs, friends, tokens
+    std::vector<uint32_t> len(n), ncols(n);
     int64_t alg = 0;
     for (int i = 0; i < n; ++i) {
-        int64_t l = 2 + (hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]);
-        int64_t ntok = 0;
-        for (int t = 0; t < T; ++t) {
-            int64_t c = hc.tok_off[(size_t)i * T + t + 1] - hc.tok_off[(size_t)i * T + t];
-            if (c) l += 3 + c * (packed ? 1 : 2);
-            ntok += c;
-        }
-        len[i] = (uint32_t)l;
-        alg += 32 + 4 * (hc.club_off[i + 1] - hc.club_off[i]) + 4 * (hc.friend_off[i + 1] - hc.friend_off[i]) + 8 * ntok;
+        const int64_t nc = hc.club_off[i + 1] - hc.club_off[i], nf = hc.friend_off[i + 1] - hc.friend_off[i];
+        const int64_t nt = hc.tok_off[(size_t)(i + 1) * T] - hc.tok_off[(size_t)i * T];
+        uint32_t nz = 0;
+        for (int t = 0; t < T; ++t) nz += hc.tok_off[(size_t)i * T + t + 1] > hc.tok_off[(size_t)i * T + t];
+        len[i] = (uint32_t)(nc + nf + nt * (packed ? 1 : 2));
+        ncols[i] = nz;
+        alg += 32 + 4 * nc + 4 * nf + 8 * nt;
     }
     hs.alg_bytes = alg;
-    // slots: longest records first (tiles of near-equal length, little padding)
+    // slots: longest records first, so the 64 records of a tile have near-equal length
     hs.idx_of_slot.resize(n);
     std::iota(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), 0);
     std::stable_sort(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), [&](int a, int b) { return len[a] > len[b]; });
@@ -245,62 +241,90 @@ void build_store(const HostCorpus& hc, HostStore& hs) {
     const int32_t ntiles = (n + kTileSlots - 1) / kTileSlots;
     hs.tile_off.resize(ntiles);
     hs.tile_steps.resize(ntiles);
-    uint64_t off = 0;
+    hs.norm_off.resize(ntiles);
+    uint64_t off = 0, noff = 0;
     for (int t = 0; t < ntiles; ++t) {
-        uint32_t mx = 0;
-        for (int p = t * kTileSlots; p < std::min(n, (t + 1) * kTileSlots); ++p) mx = std::max(mx, len[hs.idx_of_slot[p]]);
+        uint32_t mx = 0, mr = 0;
+        for (int p = t * kTileSlots; p < std::min(n, (t + 1) * kTileSlots); ++p) {
+            mx = std::max(mx, len[hs.idx_of_slot[p]]);
+            mr = std::max(mr, ncols[hs.idx_of_slot[p]]);
+        }
         hs.tile_off[t] = off;
         hs.tile_steps[t] = (mx + 3) / 4;
         off += (uint64_t)hs.tile_steps[t] * kTileSlots;
+        hs.norm_off[t] = noff;
+        noff += (uint64_t)mr * kTileSlots;
     }
     hs.stream.assign(off, make_uint4(0, 0, 0, 0));
-    hs.hdr0.resize(n); hs.hdr1.resize(n); hs.slot_uid.resize(n); hs.slot_len.resize(n);
+    hs.norms.assign(noff, 0.0);
+    hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
     par_for(n, [&](int64_t lo, int64_t hi) {
         std::vector<uint32_t> w;
         for (int64_t p = lo; p < hi; ++p) {
-            int i = hs.idx_of_slot[p];
+            const int i = hs.idx_of_slot[p];
+            const int tile = (int)(p / kTileSlots), lane = (int)(p % kTileSlots);
             w.clear();
             uint64_t mask = 0;
-            w.push_back((uint32_t)(hc.club_off[i + 1] - hc.club_off[i]));
             for (int64_t k = hc.club_off[i]; k < hc.club_off[i + 1]; ++k) w.push_back(hc.clubs[k]);
-            w.push_back((uint32_t)(hc.friend_off[i + 1] - hc.friend_off[i]));
             for (int64_t k = hc.friend_off[i]; k < hc.friend_off[i + 1]; ++k) w.push_back(hc.friends[k]);
+            uint32_t rank = 0;
             for (int t = 0; t < T; ++t) {
-                size_t r = (size_t)i * T + t;
-                int64_t c = hc.tok_off[r + 1] - hc.tok_off[r];
-                if (!c) continue;
+                const size_t r = (size_t)i * T + t;
+                if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
                 mask |= 1ull << t;
-                w.push_back((uint32_t)t | ((uint32_t)c << 8));
-                uint64_t nb;
-                std::memcpy(&nb, &hc.sqrt_nb[r], 8);
-                w.push_back((uint32_t)nb);
-                w.push_back((uint32_t)(nb >> 32));
+                hs.norms[hs.norm_off[tile] + (uint64_t)rank * kTileSlots + lane] = hc.sqrt_nb[r];
+                ++rank;
                 for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
-                    if (packed) w.push_back((uint32_t)hc.tid[k] | ((uint32_t)hc.tf[k] << 24));
-                    else { w.push_back((uint32_t)hc.tid[k]); w.push_back((uint32_t)hc.tf[k]); }
+                    if (packed) {
+                        w.push_back(((uint32_t)t << 26) | ((uint32_t)hc.tf[k] << kTidBits) | (uint32_t)hc.tid[k]);
+                    } else {
+                        w.push_back((uint32_t)hc.tid[k]);
+                        w.push_back(((uint32_t)hc.tf[k] << 8) | (uint32_t)t);
+                    }
                 }
             }
-            const int tile = (int)(p / kTileSlots), lane = (int)(p % kTileSlots);
             uint32_t* base = reinterpret_cast<uint32_t*>(hs.stream.data() + hs.tile_off[tile]);
-            for (size_t q = 0; q < w.size(); ++q) {
-                size_t step = q / 4, part = q % 4;
-                base[(step * kTileSlots + lane) * 4 + part] = w[q];
-            }
+            for (size_t q = 0; q < w.size(); ++q) base[((q / 4) * kTileSlots + lane) * 4 + (q % 4)] = w[q];
             auto code = [](const std::unordered_map<int32_t, uint32_t>& m, int32_t v) -> uint32_t {
-                if (v < 0) return kCodeMissing;
-                return m.at(v);
+                return v < 0 ? kCodeMissing : m.at(v);
             };
+            const int64_t nc = hc.club_off[i + 1] - hc.club_off[i], nf = hc.friend_off[i + 1] - hc.friend_off[i];
+            const int64_t nt = hc.tok_off[(size_t)(i + 1) * T] - hc.tok_off[(size_t)i * T];
             hs.hdr0[p] = make_uint4((uint32_t)mask, (uint32_t)(mask >> 32), (uint32_t)hc.comp[i], (uint32_t)hc.age[i]);
             hs.hdr1[p] = make_uint4((uint32_t)hc.reg[3 * (size_t)i], (uint32_t)hc.reg[3 * (size_t)i + 1],
-                                    (uint32_t)hc.reg[3 * (size_t)i + 2],
-                                    code(hc.pub_code, hc.pub[i]) | (code(hc.gen_code, hc.gen[i]) << 8));
-            hs.slot_uid[p] = hc.uid[i];
-            hs.slot_len[p] = (uint32_t)w.size();
+                                    (uint32_t)hc.reg[3 * (size_t)i + 2], (uint32_t)hc.uid[i]);
+            hs.hdr2[p] = make_uint4(code(hc.pub_code, hc.pub[i]) | (code(hc.gen_code, hc.gen[i]) << 8),
+                                    (uint32_t)nc, (uint32_t)nf, (uint32_t)nt);
         }
     });
+    return PF_OK;
 }
 
-void build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
+namespace {
+
+// 2-choice cuckoo insertion (host); false if it does not converge
+bool cuckoo_fill(std::vector<uint64_t>& keys, int lg, uint32_t seed, const std::vector<uint64_t>& items) {
+    keys.assign((size_t)1 << lg, kEmptyKey);
+    for (uint64_t it : items) {
+        uint64_t cur = it;
+        uint32_t slot = cuckoo_h1(cuckoo_mix((uint32_t)(cur >> 32) & 0xFF, (uint32_t)cur, seed), lg);
+        bool placed = false;
+        for (int kick = 0; kick < 256; ++kick) {
+            const uint32_t mx = cuckoo_mix((uint32_t)(cur >> 32) & 0xFF, (uint32_t)cur, seed);
+            const uint32_t a = cuckoo_h1(mx, lg), b = cuckoo_h2(mx, lg);
+            if (keys[a] == kEmptyKey) { keys[a] = cur; placed = true; break; }
+            if (keys[b] == kEmptyKey) { keys[b] = cur; placed = true; break; }
+            slot = (slot == a) ? b : a;  // evict from the slot we did not come from
+            std::swap(cur, keys[slot]);
+        }
+        if (!placed) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+bool build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
     const int T = hc.T;
     QConst& c = out.c;
     std::memset(&c, 0, sizeof c);
@@ -336,70 +360,64 @@ void build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* ex
         c.sig_pub[e] = term(PF_F_PUBLIC, e ? 1.0 : 0.0);
         c.sig_gen[e] = term(PF_F_GENDER, e ? 1.0 : 0.0);
     }
-    for (int b = 1; b <= 3; ++b)
-        for (int m = 0; m <= 3; ++m) {
-            int a = c.a_regcnt;
-            if (a == 0) continue;
-            double s = (double)(float)((double)m / (std::sqrt((double)a) * std::sqrt((double)b)));
-            c.sig_reg[b][m] = term(PF_F_REGION, s);
-        }
+    if (c.a_regcnt > 0)
+        for (int b = 1; b <= 3; ++b)
+            for (int m = 0; m <= 3; ++m) {
+                // recommender.cpp:130-139, cast to float then back to double
+                double s = (double)(float)((double)m / (std::sqrt((double)c.a_regcnt) * std::sqrt((double)b)));
+                c.sig_reg[b][m] = term(PF_F_REGION, s);
+            }
     for (int v = 1; v <= kValTab; ++v) {
-        if (c.comp > 0) {
-            int lo = std::min(c.comp, v), hi = std::max(c.comp, v);
-            c.sig_comp[v] = term(PF_F_COMPLETION, (double)lo / (double)hi);
-        }
-        if (c.age > 0) {
-            int lo = std::min(c.age, v), hi = std::max(c.age, v);
-            c.sig_age[v] = term(PF_F_AGE, (double)lo / (double)hi);
-        }
+        if (c.comp > 0) c.sig_comp[v] = term(PF_F_COMPLETION, (double)std::min(c.comp, v) / (double)std::max(c.comp, v));
+        if (c.age > 0) c.sig_age[v] = term(PF_F_AGE, (double)std::min(c.age, v) / (double)std::max(c.age, v));
     }
     c.sig0_clubs = term(PF_F_CLUBS, 0.0);
     c.sig0_friends = term(PF_F_FRIENDS, 0.0);
-    // hash entries
-    struct Ent { uint32_t tag, id, val; };
-    std::vector<Ent> ents;
+    // hash items: distinct clubs, distinct friends, (column, token) weights, exclusions
+    std::vector<uint64_t> items;
     std::vector<uint32_t> tmp(hc.clubs.begin() + hc.club_off[i], hc.clubs.begin() + hc.club_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) ents.push_back({kTagClubs, x, 0});
+    for (uint32_t x : tmp) items.push_back(make_key(kTagClubs, x));
     tmp.assign(hc.friends.begin() + hc.friend_off[i], hc.friends.begin() + hc.friend_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) ents.push_back({kTagFriends, x, 0});
+    for (uint32_t x : tmp) items.push_back(make_key(kTagFriends, x));
     out.vals.clear();
     c.colmask = 0;
     for (int t = 0; t < T; ++t) {
-        size_t r = (size_t)i * T + t;
+        const size_t r = (size_t)i * T + t;
         c.sig0_col[t] = term(kNumFixed + t, 0.0);
         c.sqrt_na[t] = hc.sqrt_nb[r];
         if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
         c.colmask |= 1ull << t;
         for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
-            double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;
+            const double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;  // recommender.cpp:78
             QVal v;
             v.wq = (double)hc.tf[k] * idf;
             v.idf = idf;
-            ents.push_back({(uint32_t)t, (uint32_t)hc.tid[k], (uint32_t)out.vals.size()});
+            items.push_back(make_key((uint32_t)t, (uint32_t)hc.tid[k]) | ((uint64_t)out.vals.size() << 40));
             out.vals.push_back(v);
         }
     }
+    c.n_hits_max = (uint32_t)__builtin_popcountll(c.colmask);
     if (excl) {
         tmp.assign(excl->begin(), excl->end());
         std::sort(tmp.begin(), tmp.end());
         tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-        for (uint32_t x : tmp) ents.push_back({kTagExcl, x, 0});
+        for (uint32_t x : tmp) items.push_back(make_key(kTagExcl, x));
     }
-    uint32_t cap = next_pow2(std::max<uint32_t>(16, 2 * (uint32_t)ents.size()));
-    int lg = 0;
-    while ((1u << lg) < cap) ++lg;
-    c.cap_log2 = lg;
     c.n_vals = (int32_t)out.vals.size();
-    out.keys.assign(cap, kEmptyKey);
-    for (const Ent& e : ents) {
-        uint32_t s = hash_key(e.tag, e.id) & (cap - 1);
-        while (out.keys[s] != kEmptyKey) s = (s + 1) & (cap - 1);
-        out.keys[s] = make_key(e.tag, e.id) | ((uint64_t)e.val << 40);
-    }
+    int lg = 5;
+    while ((1u << lg) < items.size() * 5 / 2 + 1) ++lg;
+    for (; lg <= kMaxHashLog2; ++lg)
+        for (uint32_t seed = 0; seed < 16; ++seed)
+            if (cuckoo_fill(out.keys, lg, seed * 0x6A09E667u, items)) {
+                c.cap_log2 = lg;
+                c.seed = seed * 0x6A09E667u;
+                return true;
+            }
+    return false;
 }
 
 }  // namespace pf

@@ -36,9 +36,9 @@ struct HostStore {
     std::vector<uint4> stream;
     std::vector<uint64_t> tile_off;
     std::vector<uint32_t> tile_steps;
-    std::vector<uint4> hdr0, hdr1;
-    std::vector<int32_t> slot_uid;
-    std::vector<uint32_t> slot_len;
+    std::vector<double> norms;
+    std::vector<uint64_t> norm_off;
+    std::vector<uint4> hdr0, hdr1, hdr2;
     std::vector<int32_t> slot_of_idx;
     std::vector<int32_t> idx_of_slot;
     bool packed = true;
@@ -53,9 +53,10 @@ struct QImageHost {
 };
 
 int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err);
-void build_store(const HostCorpus& hc, HostStore& hs);
+int build_store(const HostCorpus& hc, HostStore& hs, std::string& err);
 // excl: uids to exclude (all-candidates mode), may be null
-void build_query(const HostCorpus& hc, int32_t idx, const std::vector<int32_t>* excl, QImageHost& out);
+// returns false when the cuckoo table cannot be built within kMaxHashLog2
+bool build_query(const HostCorpus& hc, int32_t idx, const std::vector<int32_t>* excl, QImageHost& out);
 
 // exact reference arithmetic on the host (glibc exp)
 double ref_sigmoid(double x);

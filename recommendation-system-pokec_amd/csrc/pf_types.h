@@ -15,33 +15,43 @@ constexpr int kNumFixed = PF_NUM_FIXED;
 constexpr int kNormSlots = kNumFixed + kMaxCols;
 constexpr int kValTab = 128;        // completion/age sigmoid tables cover values 1..128
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
+constexpr int kScanThreads = 256;   // 4 waves per scan block
+constexpr int kMaxHashLog2 = 16;    // cuckoo table <= 65536 slots (h1/h2 from one 32-bit mix)
 
-// hash-table key tags (bits 32..39 of a key)
+// hash-table key tags (bits 32..39 of a key); text columns use tag = column index
 constexpr uint32_t kTagClubs = 64;
 constexpr uint32_t kTagFriends = 65;
 constexpr uint32_t kTagExcl = 66;   // all-candidates exclusion set adj[q] + {q}, keyed by uid
 constexpr uint64_t kEmptyKey = ~0ull;
-constexpr uint64_t kKeyMask = 0xFFFFFFFFFFull;  // low 40 bits: tag:id
+constexpr uint64_t kKeyMask = 0xFFFFFFFFFFull;  // low 40 bits: tag:id; bits 40..63: value index
 
-// Record stream words (per candidate, in this order), see DESIGN.md:
-//   n_clubs, clubs[n_clubs], n_friends, friends[n_friends],
-//   per non-empty text column t (ascending):
-//     (t | count << 8), sqrt(nb) lo, sqrt(nb) hi, count token words
-//   token word (packed): tid | tf << 24      (needs 0 <= tid < 2^24, 0 <= tf < 256)
-//   token words (wide):  tid, tf
-constexpr uint32_t kPackedTidMask = 0xFFFFFFu;
+// Record stream (per candidate, tile-interleaved in 16-B steps):
+//   clubs[n_clubs] | friends[n_friends] | tokens[n_tok]
+// packed token word = col << 26 | tf << 18 | tid      (tid < 2^18, 0 <= tf < 256, col < 64)
+// wide token = 2 words: tid, (tf << 8) | col          (tf in [-2^23, 2^23))
+// Tokens are grouped by column (ascending), ascending tid within a column.
+constexpr uint32_t kTidBits = 18;
+constexpr uint32_t kTidMask = (1u << kTidBits) - 1;
 
-// per-slot fixed header, 2 x uint4 (32 B):
+// Per-slot header, 3 x uint4 (48 B), SoA:
 //   h0 = {colmask lo, colmask hi, completion, age}
-//   h1 = {region0, region1, region2, codes} codes = pub | gen << 8 | (nclubs>0)<<16 ...
+//   h1 = {region0, region1, region2, uid}
+//   h2 = {codes (pub | gen << 8), n_clubs, n_friends, n_tok}
 constexpr uint32_t kCodeMissing = 0xFFu;
 
-__host__ __device__ inline uint32_t hash_key(uint32_t tag, uint32_t id) {
-    uint32_t h = id * 0x9E3779B1u ^ (tag * 0x85EBCA77u);
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    h ^= h >> 12;
-    return h;
+// 2-choice cuckoo hash over (tag, id): one 32-bit mix, two slots from its top bits
+__host__ __device__ inline uint32_t cuckoo_mix(uint32_t tag, uint32_t id, uint32_t seed) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t x = id ^ __umul24(tag + 1u, 0x9E3779u) ^ seed;
+#else
+    uint32_t x = id ^ ((tag + 1u) * 0x9E3779u) ^ seed;
+#endif
+    x *= 0x9E3779B1u;
+    return x ^ (x >> 16);
+}
+__host__ __device__ inline uint32_t cuckoo_h1(uint32_t mix, int lg) { return mix >> (32 - lg); }
+__host__ __device__ inline uint32_t cuckoo_h2(uint32_t mix, int lg) {
+    return ((mix * 0x85EBCA6Bu) >> (32 - lg)) ^ 1u;
 }
 
 __host__ __device__ inline uint64_t make_key(uint32_t tag, uint32_t id) {
@@ -49,7 +59,7 @@ __host__ __device__ inline uint64_t make_key(uint32_t tag, uint32_t id) {
 }
 
 // Per-query constants (A side of profile_similarity).  Built on the host with
-// glibc exp/logf so every table entry is bit-identical to the reference.
+// glibc exp so every table entry is bit-identical to the reference.
 struct QConst {
     uint64_t colmask;          // non-empty text columns of A
     int32_t comp, age;         // > 0 when present
@@ -57,10 +67,10 @@ struct QConst {
     uint32_t pubcode, gencode; // kCodeMissing when < 0
     int32_t a_regcnt;          // parts >= 0 (0 -> region term never used)
     int32_t n_clubs, n_friends;// |A.clubs|, |A.friends| with duplicates
-    int32_t cap_log2;          // hash table capacity
+    int32_t cap_log2;          // cuckoo table capacity (log2)
+    uint32_t seed;             // cuckoo hash seed
     int32_t n_vals;            // token value entries
     int32_t n_cols;            // T
-    int32_t pad0;
     double sqrt_clubs, sqrt_friends;     // sqrt((double)|A|)
     double sig_pub[2], sig_gen[2];       // [eq]
     double sig_reg[4][4];                // [b_cnt][matches]
@@ -72,7 +82,7 @@ struct QConst {
     // normaliser z = zmode ? (s - zmean)/zsd : 6(s - 0.5)   (slots 0..6 fixed, 7+t text)
     double zmean[kNormSlots];
     double zsd[kNormSlots];
-    uint32_t zmode_lo, zmode_hi, zmode_fx, pad1;  // bitmask per text column / fixed slot
+    uint32_t zmode_lo, zmode_hi, zmode_fx, n_hits_max;  // n_hits_max = popcount(colmask)
 };
 
 // token value of a query hash entry: dot += wq * (tf * idf)
@@ -86,7 +96,7 @@ struct QImageRef {
     uint32_t const_off;   // byte offset of QConst in the image pool
     uint32_t keys_off;    // byte offset of the key table
     uint32_t vals_off;    // byte offset of the value table
-    uint32_t lds_bytes;   // bytes needed to stage this query in LDS (0 = too big -> global)
+    uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 
 // top-k key: ascending key == (score desc, uid asc), recommender_graph.cpp:97-101
@@ -111,13 +121,14 @@ __host__ __device__ inline int32_t key_uid(uint64_t k) {
 
 // Device-side corpus (the "tile store").
 struct DevStore {
-    const uint4* stream;       // [sum tile_steps * 64] interleaved record stream
+    const uint4* stream;       // interleaved record stream, [tile][step][lane] uint4
     const uint64_t* tile_off;  // [n_tiles] uint4 offset of each tile
     const uint32_t* tile_steps;// [n_tiles] 16-B steps of the longest record in the tile
+    const double* norms;       // [tile][rank][lane] sqrt(sum (tf*idf)^2) per non-empty column
+    const uint64_t* norm_off;  // [n_tiles] double offset of each tile's norms
     const uint4* hdr0;         // [n_slots]
-    const uint4* hdr1;         // [n_slots]
-    const int32_t* slot_uid;   // [n_slots]
-    const uint32_t* slot_len;  // [n_slots] record length in words
+    const uint4* hdr1;
+    const uint4* hdr2;
     int32_t n_slots;
     int32_t n_tiles;
     int32_t packed;

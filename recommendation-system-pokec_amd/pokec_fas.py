@@ -25,7 +25,7 @@ MAX_TOPK_DEVICE = 64
 EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_users", "pf_idf", "pf_fas_pairs",
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
-           "pf_last_scan_ms"]
+           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read"]
 
 
 class PfLayoutStats(ctypes.Structure):
@@ -71,6 +71,8 @@ def lib():
         L.pf_layout.argtypes = [V, ctypes.POINTER(PfLayoutStats)]
         L.pf_last_scan_ms.argtypes = [V]
         L.pf_last_scan_ms.restype = ctypes.c_float
+        L.pf_profile_reset.argtypes = [V]
+        L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
         _lib = L
     return _lib
 
@@ -191,6 +193,15 @@ class FasEngine:
     @property
     def last_scan_ms(self):
         return self._L.pf_last_scan_ms(self.h)
+
+    def profile_reset(self):
+        self._check(self._L.pf_profile_reset(self.h), "pf_profile_reset")
+
+    def profile_read(self):
+        """(summed scan-kernel device ms, launches) since profile_reset()."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._check(self._L.pf_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)), "pf_profile_read")
+        return ms.value, n.value
 
 
 def decode_keys(keys):

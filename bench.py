@@ -121,7 +121,9 @@ def main():
     steps, warm = args.steps, args.warmup
     rng = np.random.default_rng(2)  # same query stream on every rank
     qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
-    stream = torch.cuda.current_stream()
+    # a dedicated stream: the engine, the all-gather and the copies are all ordered on it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     local_keys = torch.empty((Q, k), dtype=torch.int64, device="cuda")
     gathered = torch.empty((world, Q, k), dtype=torch.int64, device="cuda") if world > 1 else None

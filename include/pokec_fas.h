@@ -186,11 +186,14 @@ int pf_set_shard(pf_ctx* ctx, int32_t shard, int32_t nshards);
  * 64-bit keys to DEVICE memory d_keys[nq*topk] on `stream` (a hipStream_t;
  * NULL = the context's stream).  Key = (~orderable(score) << 32) | (uid ^
  * 0x80000000): ascending key = (score desc, uid asc); unused slots are
- * UINT64_MAX.  No host synchronisation.
+ * UINT64_MAX.  `stream` is used as given (NULL = the HIP null stream), so the
+ * caller's collectives on that stream are ordered after the scan.  No host
+ * synchronisation.
  */
 int pf_scan_keys_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq,
                        int32_t topk, uint64_t* d_keys, void* stream);
-/* Merge nparts key lists laid out [part][nq][topk] (device) into d_out[nq][topk]. */
+/* Merge nparts key lists laid out [part][nq][topk] (device) into d_out[nq][topk]
+ * on `stream` (as given, NULL = null stream). */
 int pf_merge_keys_async(pf_ctx* ctx, const uint64_t* d_parts, int32_t nparts,
                         int32_t nq, int32_t topk, uint64_t* d_out, void* stream);
 /* Host-side decode of packed keys; count = number of non-empty keys. */

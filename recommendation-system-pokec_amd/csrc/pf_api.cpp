@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -113,6 +114,16 @@ struct Images {
 };
 
 constexpr uint32_t kStageLimit = 48 * 1024;   // keys+vals above this are probed in global memory
+
+// PF_STAGE_LIMIT (bytes) lowers the LDS staging limit; tests use it to force the
+// global-memory table variant on small corpora.
+uint32_t stage_limit() {
+    static const uint32_t lim = [] {
+        const char* e = getenv("PF_STAGE_LIMIT");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : kStageLimit;
+    }();
+    return lim;
+}
 constexpr uint32_t kBlockThreads = 256;
 
 void add_image(Images& im, const pf::QImageHost& q) {
@@ -130,9 +141,9 @@ void add_image(Images& im, const pf::QImageHost& q) {
     const uint8_t* vp = reinterpret_cast<const uint8_t*>(q.vals.data());
     im.pool.insert(im.pool.end(), vp, vp + q.vals.size() * sizeof(pf::QVal));
     const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
-    r.lds_bytes = kv <= kStageLimit ? (uint32_t)kv : 0u;
+    r.lds_bytes = kv <= stage_limit() ? (uint32_t)kv : 0u;
     im.gtab = im.gtab || r.lds_bytes == 0;
-    const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads * 8u + 2048u;
+    const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads + 2048u;
     im.max_lds = std::max(im.max_lds, need);
     im.refs.push_back(r);
 }
@@ -188,7 +199,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
     for (size_t g = 0; g < qidx.size(); ++g) {
         out[g].assign(slots[g].size(), 0.f);
         if (slots[g].empty()) continue;
-        if (!pf::build_query(c->hc, qidx[g], nullptr, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
+        if (!pf::build_query(c->hc, c->hs.packed, qidx[g], nullptr, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
         const int32_t img = (int32_t)im.refs.size();
         add_image(im, qi);
         for (size_t b = 0; b < slots[g].size(); b += 256) {
@@ -237,7 +248,7 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         auto it = c->hc.adj.find(u);
         if (it != c->hc.adj.end()) excl = it->second;
         excl.push_back(u);
-        if (!pf::build_query(c->hc, i, &excl, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
+        if (!pf::build_query(c->hc, c->hs.packed, i, &excl, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
         add_image(im, qi);
     }
     const int nq = (int)idx.size();
@@ -677,7 +688,7 @@ int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {
 int pf_scan_keys_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, uint64_t* d_keys, void* stream) {
     if (!c || nq < 0 || topk <= 0 || topk > pf::kMaxTopK || (nq && (!q || !d_keys))) return PF_EINVAL;
     (void)hipSetDevice(c->device);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;  // as given: NULL is the null stream
     HIPCHK(c, hipMemsetAsync(d_keys, 0xFF, (size_t)nq * topk * sizeof(uint64_t), s));
     std::vector<int32_t> idx, rows;
     for (int i = 0; i < nq; ++i) {
@@ -691,7 +702,7 @@ int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int3
                         void* stream) {
     if (!c || nparts < 1 || nq < 0 || topk <= 0 || topk > pf::kMaxTopK) return PF_EINVAL;
     (void)hipSetDevice(c->device);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;
     HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, nullptr, s));
     return PF_OK;
 }

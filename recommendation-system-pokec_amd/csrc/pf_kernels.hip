@@ -69,22 +69,27 @@ __device__ __forceinline__ double ratio_term(const QConst& q, int slot, int a, i
 // ---------------------------------------------------------------- query hash (cuckoo)
 struct QView {
     const QConst* q;
-    const uint64_t* keys;
+    const uint2* tab;  // T0 clubs | T1 friends | T2 tokens (2^lg each) | T3 excl (2^lg_excl)
     const QVal* vals;
-    double* hits;      // LDS [H][blockDim.x] per-lane column dot products
-    int lg;
+    void* hits;        // LDS [kHitCap][blockDim.x] per-lane token-hit list
+    int lg, lge;
     uint32_t seed;
 };
 
-__device__ __forceinline__ int lookup(const QView& v, uint32_t tag, uint32_t id) {
-    const uint32_t mx = cuckoo_mix(tag, id, v.seed);
-    const uint64_t want = make_key(tag, id);
-    const uint64_t k1 = v.keys[cuckoo_h1(mx, v.lg)];
-    const uint64_t k2 = v.keys[cuckoo_h2(mx, v.lg)];
-    int r = -1;
-    if ((k1 & kKeyMask) == want) r = (int)(k1 >> 40);
-    if ((k2 & kKeyMask) == want) r = (int)(k2 >> 40);
-    return r;
+// 2-choice probe of table `off` (entries) with capacity 2^lg; returns the entry's val or kEmptyVal
+__device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, uint32_t key) {
+    const uint32_t x = cuckoo_x(key, v.seed);
+    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
+    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
+    // a key sits in at most one of its two slots: AND-combining keeps both reads
+    // unconditional (a ?: chain lets the compiler sink the second read into a branch)
+    const uint32_t r1 = e1.x == key ? e1.y : kEmptyVal;
+    const uint32_t r2 = e2.x == key ? e2.y : kEmptyVal;
+    return r1 & r2;
+}
+
+__device__ __forceinline__ bool excluded(const QView& v, uint32_t uid) {
+    return probe(v, 3u << v.lg, v.lge, uid) != kEmptyVal;
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -97,56 +102,123 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Per-lane record walk state
 struct Walk {
-    int ic, ifr;         // clubs / friends intersections
-    uint32_t nh;         // hit columns recorded
-    uint32_t last_col;   // column of the last hit
-    uint64_t hitmask;
+    uint32_t cnt;        // clubs intersections (low 16 bits) + friends intersections << 16
+    uint32_t nh;         // token hits seen (entries beyond kHitCap are not stored)
     uint32_t pend;       // wide tokens: tid word waiting for its (tf, col) word
+};
+
+// A token hit is stored as its T2 val plus the candidate's tf:
+//   packed: one word  vi | col << 18 | tf << 24        (the walk's only LDS write)
+//   wide:   two words {col | vi << 8, tf << 8 | col}
+template <bool PACKED>
+struct HitT;
+template <>
+struct HitT<true> {
+    using type = uint32_t;
+    __device__ static uint32_t col(type e) { return (e >> kTidBits) & 63u; }
+    __device__ static uint32_t vi(type e) { return e & kTidMask; }
+    __device__ static int32_t tf(type e) { return (int32_t)(e >> 24); }
+};
+template <>
+struct HitT<false> {
+    using type = uint2;
+    __device__ static uint32_t col(type e) { return e.x & 0xFFu; }
+    __device__ static uint32_t vi(type e) { return e.x >> 8; }
+    __device__ static int32_t tf(type e) { return (int32_t)e.y >> 8; }
 };
 
 template <bool PACKED>
 __device__ __forceinline__ void walk_word(Walk& W, uint32_t w, uint32_t j, uint32_t nc, uint32_t nset, uint32_t len,
                                           const QView& v, uint32_t hstride) {
+    using H = HitT<PACKED>;
     const bool ok = j < len;
     const bool tok = j >= nset;
     const bool fr = j >= nc;
-    uint32_t tag, id, tfw;
-    bool probe;
+    const uint32_t cap = 1u << v.lg;
+    typename H::type* hits = reinterpret_cast<typename H::type*>(v.hits);
     if (PACKED) {
-        tag = tok ? (w >> 26) : (fr ? kTagFriends : kTagClubs);
-        id = tok ? (w & kTidMask) : w;
-        tfw = (w >> kTidBits) & 0xFFu;
-        probe = ok;
-    } else {
-        const bool second = tok && ((j - nset) & 1u);
-        tag = second ? (w & 0xFFu) : (fr ? kTagFriends : kTagClubs);
-        id = second ? W.pend : w;
-        tfw = (uint32_t)((int32_t)w >> 8);
-        if (tok && !second) W.pend = w;
-        probe = ok && (!tok || second);
-    }
-    int vi = lookup(v, tag, id);
-    vi = probe ? vi : -1;
-    const bool hit = vi >= 0;
-    W.ic += (!fr && hit) ? 1 : 0;
-    W.ifr += (fr && !tok && hit) ? 1 : 0;
-    if (tok && hit) {  // rare: accumulate this token's product into its column's dot
-        const QVal qv = v.vals[vi];
-        const double prod = qv.wq * ((double)(int32_t)tfw * qv.idf);
-        if (tag != W.last_col) {
-            v.hits[W.nh * hstride + threadIdx.x] = prod;
+        // sets: T0/T1 keyed by the id; tokens: T2 keyed by the word's low 24 bits (col:tid)
+        const uint32_t key = tok ? (w & 0xFFFFFFu) : w;
+        const uint32_t val = probe(v, tok ? 2u * cap : (fr ? cap : 0u), v.lg, key);
+        const bool hit = ok && val != kEmptyVal;
+        W.cnt += (hit && !tok) ? (fr ? 0x10000u : 1u) : 0u;
+        if (tok && hit) {  // rare
+            if (W.nh < kHitCap) reinterpret_cast<uint32_t*>(hits)[W.nh * hstride + threadIdx.x] = val | (w & 0xFF000000u);
             W.nh += 1;
-            W.last_col = tag;
-            W.hitmask |= 1ull << tag;
-        } else {
-            v.hits[(W.nh - 1) * hstride + threadIdx.x] += prod;
+        }
+    } else {
+        // wide tokens: (tid, tf << 8 | col) word pairs, probed at the second word
+        const bool second = tok && ((j - nset) & 1u);
+        const uint32_t key = second ? W.pend : w;
+        if (tok && !second) W.pend = w;
+        const uint32_t val = probe(v, tok ? 2u * cap : (fr ? cap : 0u), v.lg, key);
+        const bool hit = ok && (!tok || second) && val != kEmptyVal && (!tok || (val & 0xFFu) == (w & 0xFFu));
+        W.cnt += (hit && !tok) ? (fr ? 0x10000u : 1u) : 0u;
+        if (tok && hit) {
+            if (W.nh < kHitCap) reinterpret_cast<uint2*>(hits)[W.nh * hstride + threadIdx.x] = make_uint2(val, w);
+            W.nh += 1;
         }
     }
+}
+
+// product of one shared token, recommender.cpp:74-85 (wA * wB, wB = tf * idf)
+__device__ __forceinline__ double hit_product(const QView& v, uint32_t vi, int32_t tf) {
+    const QVal qv = v.vals[vi];
+    return qv.wq * ((double)tf * qv.idf);
+}
+
+__device__ __forceinline__ double col_norm(const DevStore& st, int p, uint64_t cmask, int t) {
+    const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
+    return st.norms[st.norm_off[p >> 6] + (uint64_t)r * kTileSlots + (p & 63)];
+}
+
+// Text terms of a lane whose hit list overflowed: re-walk its token words from global
+// memory, accumulating each column's dot in stream order (rare path).
+template <bool PACKED>
+__device__ __forceinline__ double text_terms_slow(const DevStore& st, const QView& v, int p, uint32_t nset,
+                                                  uint32_t len, uint64_t cmask, double sum) {
+    const QConst& q = *v.q;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(st.stream + st.tile_off[p >> 6] + (p & 63));
+    auto word = [&](uint32_t j) { return base[(size_t)(j >> 2) * (kTileSlots * 4) + (j & 3)]; };
+    const uint32_t cap = 1u << v.lg;
+    int cur = -1;
+    double dot = 0.0;
+    auto close = [&]() {
+        if (cur >= 0 && ((q.colmask >> cur) & 1ull))
+            sum += dot == 0.0 ? q.sig0_col[cur] : text_term(q, cur, dot, col_norm(st, p, cmask, cur));
+    };
+    for (uint32_t j = nset; j < len; j += PACKED ? 1 : 2) {
+        uint32_t key, col, val;
+        int32_t tf;
+        if (PACKED) {
+            const uint32_t w = word(j);
+            key = w & 0xFFFFFFu;
+            col = (w >> kTidBits) & 63u;
+            tf = (int32_t)(w >> 24);
+            val = probe(v, 2u * cap, v.lg, key);
+        } else {
+            const uint32_t w = word(j + 1);
+            key = word(j);
+            col = w & 0xFFu;
+            tf = (int32_t)w >> 8;
+            val = probe(v, 2u * cap, v.lg, key);
+            if (val != kEmptyVal && (val & 0xFFu) != col) val = kEmptyVal;
+        }
+        if ((int)col != cur) {
+            close();
+            cur = (int)col;
+            dot = 0.0;
+        }
+        if (val != kEmptyVal) dot += hit_product(v, PACKED ? (val & kTidMask) : (val >> 8), tf);
+    }
+    close();
+    return sum;
 }
 
 // FAS(A = staged query, B = candidate slot p).  Every lane of the wave calls it.
 template <bool PACKED>
 __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
+    using H = HitT<PACKED>;
     const QConst& q = *v.q;
     const uint32_t hstride = blockDim.x;
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
@@ -162,15 +234,15 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     const uint4* base = st.stream + (active ? st.tile_off[p >> 6] + (p & 63) : 0);
 
     Walk W;
-    W.ic = 0; W.ifr = 0; W.nh = 0; W.last_col = 0xFFFFFFFFu; W.hitmask = 0; W.pend = 0;
+    W.cnt = 0; W.nh = 0; W.pend = 0;
     const uint32_t smax = wave_max_u32(steps);
-    // 4-deep software prefetch of the 16-B steps.  Loads past a lane's record re-read its
-    // last step (always a valid address); those words are masked by j < len.
+    // Loads past a lane's record re-read its last step (always a valid address); those
+    // words are masked by j < len.
     const uint32_t last = steps ? steps - 1 : 0;
     auto ld = [&](uint32_t s) { return base[(size_t)(s < last ? s : last) * kTileSlots]; };
-    // Unrolled by 4 so every buffer is consumed and refilled in place: a register
-    // rotation (b0 = b1 ...) would make the compiler wait for the newest load.
-    uint4 b0 = ld(0), b1 = ld(1), b2 = ld(2), b3 = ld(3);
+    // Double buffer of 4 steps: the next group's 4 loads are issued before the current
+    // group is walked, so every wait is covered by a whole group of work.  (Loads kept in
+    // flight across the loop back-edge make the waitcnt pass drain them at the loop head.)
     auto step = [&](const uint4& cur, uint32_t s) {
         const uint32_t j = s * 4;
         walk_word<PACKED>(W, cur.x, j + 0, nc, nset, len, v, hstride);
@@ -178,17 +250,14 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
         walk_word<PACKED>(W, cur.z, j + 2, nc, nset, len, v, hstride);
         walk_word<PACKED>(W, cur.w, j + 3, nc, nset, len, v, hstride);
     };
-    // straight-line body (no early exit): the waitcnt pass then keeps 3 loads in flight
-    // across the back-edge; steps past smax only see words with j >= len (masked).
+    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
     for (uint32_t s = 0; s < smax; s += 4) {
-        step(b0, s);
-        b0 = ld(s + 4);
-        step(b1, s + 1);
-        b1 = ld(s + 5);
-        step(b2, s + 2);
-        b2 = ld(s + 6);
-        step(b3, s + 3);
-        b3 = ld(s + 7);
+        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
+        step(c0, s);
+        step(c1, s + 1);
+        step(c2, s + 2);
+        step(c3, s + 3);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
     }
     if (!active) return 0.0f;
 
@@ -208,32 +277,35 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
         sum += q.sig_reg[bcnt][m];
         ++used;
     }
+    const int ic = (int)(W.cnt & 0xFFFFu), ifr = (int)(W.cnt >> 16);
     if (q.n_clubs > 0 && nc > 0) {
-        sum += W.ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, W.ic, (int)nc, q.sqrt_clubs);
+        sum += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs);
         ++used;
     }
     if (q.n_friends > 0 && nf > 0) {
-        sum += W.ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, W.ifr, (int)nf, q.sqrt_friends);
+        sum += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends);
         ++used;
     }
     const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
     uint64_t common = q.colmask & cmask;
     used += __popcll(common);
-    uint32_t h = 0;
-    while (common) {
-        const int t = __ffsll((unsigned long long)common) - 1;
-        common &= common - 1;
-        double term = q.sig0_col[t];
-        if ((W.hitmask >> t) & 1ull) {
-            const double dot = v.hits[h * hstride + threadIdx.x];
-            ++h;
-            if (dot != 0.0) {
-                const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
-                const double nb = st.norms[st.norm_off[p >> 6] + (uint64_t)r * kTileSlots + (p & 63)];
-                term = text_term(q, t, dot, nb);
+    if (W.nh <= kHitCap) {
+        const typename H::type* hits = reinterpret_cast<const typename H::type*>(v.hits);
+        uint32_t h = 0;
+        while (common) {
+            const int t = __ffsll((unsigned long long)common) - 1;
+            common &= common - 1;
+            double dot = 0.0;
+            while (h < W.nh) {  // this column's hits, in stream (ascending tid) order
+                const typename H::type e = hits[h * hstride + threadIdx.x];
+                if ((int)H::col(e) != t) break;
+                dot += hit_product(v, H::vi(e), H::tf(e));
+                ++h;
             }
+            sum += dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, col_norm(st, p, cmask, t));
         }
-        sum += term;
+    } else {
+        sum = text_terms_slow<PACKED>(st, v, p, nset, len, cmask, sum);
     }
     if (used == 0) return 0.0f;
     // recommender_similarity.cpp:114-123
@@ -250,18 +322,55 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// lane i < k holds the i-th smallest key seen so far (ascending key = best first)
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ascending bitonic sort of one key per lane across the wave
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t x, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t y = shfl_xor64(x, j);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+        }
+    }
+    return x;
+}
+
+// The wave keeps the 64 smallest keys seen so far, sorted ascending across lanes
+// (lane i = i-th best); a top-k caller reads lanes < k.  Few qualifying keys are
+// inserted one by one; many are merged with a bitonic sort + merge (O(log^2 64)).
 __device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int lane) {
     uint64_t thr = rdlane64(list, k - 1);
     uint64_t m = __ballot(x < thr);
+    if (!m) return;
+    if (__popcll(m) > 3) {
+        uint64_t xs = wave_sort64(x < thr ? x : ~0ull, lane);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)xs, 63 - lane);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(xs >> 32), 63 - lane);
+        const uint64_t rev = ((uint64_t)hi << 32) | lo;
+        uint64_t y = list < rev ? list : rev;  // bitonic: the 64 smallest of both lists
+#pragma unroll
+        for (int j = 32; j > 0; j >>= 1) {
+            const uint64_t z = shfl_xor64(y, j);
+            y = (lane & j) ? (y < z ? z : y) : (y < z ? y : z);
+        }
+        list = y;
+        return;
+    }
     while (m) {
         const int src = __ffsll((unsigned long long)m) - 1;
         m &= m - 1;
         const uint64_t y = rdlane64(x, src);
         if (y < thr) {
-            const int pos = __popcll(__ballot(lane < k && list < y));
+            const int pos = __popcll(__ballot(list < y));
             const uint64_t up = __shfl_up(list, 1);
-            if (lane > pos && lane < k) list = up;
+            if (lane > pos) list = up;
             if (lane == pos) list = y;
             thr = rdlane64(list, k - 1);
         }
@@ -275,7 +384,7 @@ __device__ __forceinline__ void stage(void* dst, const void* src, uint32_t bytes
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
 }
 
-// LDS carve: [QConst][keys][vals][hits H x blockDim doubles][merge scratch 2 KiB].
+// LDS carve: [QConst][tables][vals][hit lists kHitCap x blockDim][merge scratch 2 KiB].
 // GTAB = false: the cuckoo table and the token values are staged in LDS, so every probe
 // is a ds_read (pointer provenance is the LDS symbol only, never merged with a global
 // pointer: a merged pointer would compile to flat loads, whose waits also drain the
@@ -287,22 +396,23 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     const QConst* q = reinterpret_cast<const QConst*>(smem);
     QView v;
     v.q = q;
-    v.lg = q->cap_log2;
+    v.lg = q->lg;
+    v.lge = q->lg_excl;
     v.seed = q->seed;
-    const uint32_t kb = 8u << q->cap_log2, vb = (uint32_t)q->n_vals * 16u;
+    const uint32_t kb = 8u * ((3u << q->lg) + (1u << q->lg_excl)), vb = (uint32_t)q->n_vals * 16u;
     char* p = smem + sizeof(QConst);
     if constexpr (!GTAB) {
         stage(p, pool + r.keys_off, kb);
         stage(p + kb, pool + r.vals_off, vb);
-        v.keys = reinterpret_cast<const uint64_t*>(p);
+        v.tab = reinterpret_cast<const uint2*>(p);
         v.vals = reinterpret_cast<const QVal*>(p + kb);
         p += kb + vb;
     } else {
-        v.keys = reinterpret_cast<const uint64_t*>(pool + r.keys_off);
+        v.tab = reinterpret_cast<const uint2*>(pool + r.keys_off);
         v.vals = reinterpret_cast<const QVal*>(pool + r.vals_off);
     }
-    v.hits = reinterpret_cast<double*>(p);
-    p += (size_t)q->n_hits_max * blockDim.x * 8;
+    v.hits = p;
+    p += (size_t)q->n_hits_max * blockDim.x;  // n_hits_max = bytes per lane of the hit list
     *scratch = p;
     __syncthreads();
     return v;
@@ -327,17 +437,21 @@ __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, con
         uint64_t key = ~0ull;
         if (active) {
             const int32_t uid = (int32_t)st.hdr1[p].w;
-            if (lookup(v, kTagExcl, (uint32_t)uid) < 0) key = score_key(f, uid);
+            if (!excluded(v, (uint32_t)uid)) key = score_key(f, uid);
         }
         topk_push(list, key, k, lane);
     }
+    // block merge: the 4 wave lists are packed densely (k keys each) and wave 0 takes
+    // them 64 at a time, so 4*k <= 64 keys cost a single push
     uint64_t* sc = reinterpret_cast<uint64_t*>(scratch);
     __syncthreads();
-    if (wave) sc[(wave - 1) * 64 + lane] = lane < k ? list : ~0ull;
+    if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
     if (wave == 0) {
-        for (int w = 0; w < kScanThreads / 64 - 1; ++w) topk_push(list, sc[w * 64 + lane], k, lane);
-        if (lane < k) out_keys[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * k + lane] = list;
+        uint64_t acc = ~0ull;
+        const int n = (kScanThreads / 64) * k;
+        for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
+        if (lane < k) out_keys[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * k + lane] = acc;
     }
 }
 
@@ -359,17 +473,22 @@ __global__ __launch_bounds__(1024) void topk_merge_kernel(const uint64_t* __rest
         for (int u = 0; u < 8; ++u) {
             const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
             x[u] = ~0ull;
-            if (i < total) x[u] = in[(i / k) * part_stride + q * query_stride + (i % k)];
+            if (i < total) {
+                const int32_t part = (int32_t)i / k, j = (int32_t)i - part * k;
+                x[u] = in[(int64_t)part * part_stride + q * query_stride + j];
+            }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) topk_push(list, x[u], k, lane);
     }
-    sc[wave * 64 + lane] = lane < k ? list : ~0ull;
+    if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
     if (wave == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) topk_push(list, sc[w * 64 + lane], k, lane);
+        uint64_t acc = ~0ull;
+        const int n = (int)(blockDim.x >> 6) * k;
+        for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         const int row = out_rows ? out_rows[q] : q;
-        if (lane < k) out[(size_t)row * k + lane] = list;
+        if (lane < k) out[(size_t)row * k + lane] = acc;
     }
 }
 

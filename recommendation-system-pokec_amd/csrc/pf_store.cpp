@@ -276,7 +276,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                 ++rank;
                 for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
                     if (packed) {
-                        w.push_back(((uint32_t)t << 26) | ((uint32_t)hc.tf[k] << kTidBits) | (uint32_t)hc.tid[k]);
+                        w.push_back(((uint32_t)hc.tf[k] << 24) | ((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k]);
                     } else {
                         w.push_back((uint32_t)hc.tid[k]);
                         w.push_back(((uint32_t)hc.tf[k] << 8) | (uint32_t)t);
@@ -302,29 +302,36 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
 
 namespace {
 
-// 2-choice cuckoo insertion (host); false if it does not converge
-bool cuckoo_fill(std::vector<uint64_t>& keys, int lg, uint32_t seed, const std::vector<uint64_t>& items) {
-    keys.assign((size_t)1 << lg, kEmptyKey);
+// 2-choice cuckoo insertion of (key, val) items into a 2^lg table; false if it does not converge
+bool cuckoo_fill(uint64_t* tab, int lg, uint32_t seed, const std::vector<uint64_t>& items) {
+    const size_t cap = (size_t)1 << lg;
+    for (size_t i = 0; i < cap; ++i) tab[i] = kEmptyEntry;
     for (uint64_t it : items) {
         uint64_t cur = it;
-        uint32_t slot = cuckoo_h1(cuckoo_mix((uint32_t)(cur >> 32) & 0xFF, (uint32_t)cur, seed), lg);
+        uint32_t from = cuckoo_h1(cuckoo_x((uint32_t)cur, seed), lg);
         bool placed = false;
-        for (int kick = 0; kick < 256; ++kick) {
-            const uint32_t mx = cuckoo_mix((uint32_t)(cur >> 32) & 0xFF, (uint32_t)cur, seed);
-            const uint32_t a = cuckoo_h1(mx, lg), b = cuckoo_h2(mx, lg);
-            if (keys[a] == kEmptyKey) { keys[a] = cur; placed = true; break; }
-            if (keys[b] == kEmptyKey) { keys[b] = cur; placed = true; break; }
-            slot = (slot == a) ? b : a;  // evict from the slot we did not come from
-            std::swap(cur, keys[slot]);
+        for (int kick = 0; kick < 500; ++kick) {
+            const uint32_t x = cuckoo_x((uint32_t)cur, seed);
+            const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
+            if (tab[a] == kEmptyEntry) { tab[a] = cur; placed = true; break; }
+            if (tab[b] == kEmptyEntry) { tab[b] = cur; placed = true; break; }
+            from = (from == a) ? b : a;  // evict from the slot we did not come from
+            std::swap(cur, tab[from]);
         }
         if (!placed) return false;
     }
     return true;
 }
 
+int lg_for(size_t n) {
+    int lg = 4;
+    while (((size_t)1 << lg) * 2 < n * 5) ++lg;  // load factor <= 0.4
+    return lg;
+}
+
 }  // namespace
 
-bool build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
+bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
     const int T = hc.T;
     QConst& c = out.c;
     std::memset(&c, 0, sizeof c);
@@ -373,16 +380,17 @@ bool build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* ex
     }
     c.sig0_clubs = term(PF_F_CLUBS, 0.0);
     c.sig0_friends = term(PF_F_FRIENDS, 0.0);
-    // hash items: distinct clubs, distinct friends, (column, token) weights, exclusions
-    std::vector<uint64_t> items;
+    // hash items: distinct clubs (T0), distinct friends (T1), (column, token) weights (T2),
+    // exclusions (T3)
+    std::vector<uint64_t> items[4];
     std::vector<uint32_t> tmp(hc.clubs.begin() + hc.club_off[i], hc.clubs.begin() + hc.club_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) items.push_back(make_key(kTagClubs, x));
+    for (uint32_t x : tmp) items[0].push_back(make_entry(x, 0));
     tmp.assign(hc.friends.begin() + hc.friend_off[i], hc.friends.begin() + hc.friend_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) items.push_back(make_key(kTagFriends, x));
+    for (uint32_t x : tmp) items[1].push_back(make_entry(x, 0));
     out.vals.clear();
     c.colmask = 0;
     for (int t = 0; t < T; ++t) {
@@ -396,27 +404,39 @@ bool build_query(const HostCorpus& hc, int32_t i, const std::vector<int32_t>* ex
             QVal v;
             v.wq = (double)hc.tf[k] * idf;
             v.idf = idf;
-            items.push_back(make_key((uint32_t)t, (uint32_t)hc.tid[k]) | ((uint64_t)out.vals.size() << 40));
+            const uint32_t vi = (uint32_t)out.vals.size();
+            if (packed) items[2].push_back(make_entry(((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k], vi | ((uint32_t)t << kTidBits)));
+            else items[2].push_back(make_entry((uint32_t)hc.tid[k], (uint32_t)t | (vi << 8)));
             out.vals.push_back(v);
         }
     }
-    c.n_hits_max = (uint32_t)__builtin_popcountll(c.colmask);
+    c.n_hits_max = kHitCap * (packed ? 4u : 8u);
     if (excl) {
         tmp.assign(excl->begin(), excl->end());
         std::sort(tmp.begin(), tmp.end());
         tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-        for (uint32_t x : tmp) items.push_back(make_key(kTagExcl, x));
+        for (uint32_t x : tmp) items[3].push_back(make_entry(x, 0));
     }
     c.n_vals = (int32_t)out.vals.size();
-    int lg = 5;
-    while ((1u << lg) < items.size() * 5 / 2 + 1) ++lg;
-    for (; lg <= kMaxHashLog2; ++lg)
-        for (uint32_t seed = 0; seed < 16; ++seed)
-            if (cuckoo_fill(out.keys, lg, seed * 0x6A09E667u, items)) {
-                c.cap_log2 = lg;
-                c.seed = seed * 0x6A09E667u;
+    if (out.vals.size() >= (packed ? (1u << kTidBits) : (1u << 24))) return false;
+    int lg = std::max({lg_for(items[0].size()), lg_for(items[1].size()), lg_for(items[2].size())});
+    int lge = lg_for(items[3].size());
+    for (; lg <= kMaxHashLog2; ++lg, ++lge) {
+        lge = std::min(lge, kMaxHashLog2);
+        out.keys.assign(((size_t)3 << lg) + ((size_t)1 << lge), kEmptyEntry);
+        for (uint32_t s = 0; s < 16; ++s) {
+            const uint32_t seed = s * 0x6A09E667u;
+            bool ok = true;
+            for (int k = 0; k < 3 && ok; ++k) ok = cuckoo_fill(out.keys.data() + ((size_t)k << lg), lg, seed, items[k]);
+            if (ok) ok = cuckoo_fill(out.keys.data() + ((size_t)3 << lg), lge, seed, items[3]);
+            if (ok) {
+                c.lg = lg;
+                c.lg_excl = lge;
+                c.seed = seed;
                 return true;
             }
+        }
+    }
     return false;
 }
 

@@ -45,7 +45,7 @@ struct HostStore {
     int64_t alg_bytes = 0;    // SURVEY 8(d) D3 accounting
 };
 
-// Query image (A side).  keys: 1 << cap_log2 slots; vals: token values.
+// Query image (A side).  keys: tables T0..T3 (see pf_types.h); vals: token values.
 struct QImageHost {
     QConst c;
     std::vector<uint64_t> keys;
@@ -56,7 +56,7 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
 int build_store(const HostCorpus& hc, HostStore& hs, std::string& err);
 // excl: uids to exclude (all-candidates mode), may be null
 // returns false when the cuckoo table cannot be built within kMaxHashLog2
-bool build_query(const HostCorpus& hc, int32_t idx, const std::vector<int32_t>* excl, QImageHost& out);
+bool build_query(const HostCorpus& hc, bool packed, int32_t idx, const std::vector<int32_t>* excl, QImageHost& out);
 
 // exact reference arithmetic on the host (glibc exp)
 double ref_sigmoid(double x);

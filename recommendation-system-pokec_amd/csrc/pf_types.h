@@ -16,18 +16,25 @@ constexpr int kNormSlots = kNumFixed + kMaxCols;
 constexpr int kValTab = 128;        // completion/age sigmoid tables cover values 1..128
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
-constexpr int kMaxHashLog2 = 16;    // cuckoo table <= 65536 slots (h1/h2 from one 32-bit mix)
+constexpr uint32_t kHitCap = 24;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
+constexpr int kMaxHashLog2 = 16;    // cuckoo tables <= 65536 slots (h1/h2 from one 32-bit product)
 
-// hash-table key tags (bits 32..39 of a key); text columns use tag = column index
-constexpr uint32_t kTagClubs = 64;
-constexpr uint32_t kTagFriends = 65;
-constexpr uint32_t kTagExcl = 66;   // all-candidates exclusion set adj[q] + {q}, keyed by uid
-constexpr uint64_t kEmptyKey = ~0ull;
-constexpr uint64_t kKeyMask = 0xFFFFFFFFFFull;  // low 40 bits: tag:id; bits 40..63: value index
+// Query hash: four 2-choice cuckoo tables of 8-byte entries {key, val} (uint2).
+//   T0 clubs    key = club id                      val = 0
+//   T1 friends  key = friend id                    val = 0
+//   T2 tokens   packed: key = col << 18 | tid      val = value index | col << 18
+//               wide:   key = tid                  val = col | value index << 8
+//   T3 excl     key = uid (adj[q] + {q})            val = 0
+// T0..T2 share one capacity 2^lg (so a word's table is base + kind * 2^lg); T3 has its own.
+// Empty slot = {~0, ~0}; a hit needs val != ~0, so an id equal to ~0 cannot fake a match.
+constexpr uint32_t kEmptyVal = 0xFFFFFFFFu;
+constexpr uint64_t kEmptyEntry = ~0ull;
+constexpr uint32_t kHashMul = 0x9E3779B1u;
 
 // Record stream (per candidate, tile-interleaved in 16-B steps):
 //   clubs[n_clubs] | friends[n_friends] | tokens[n_tok]
-// packed token word = col << 26 | tf << 18 | tid      (tid < 2^18, 0 <= tf < 256, col < 64)
+// packed token word = tf << 24 | col << 18 | tid      (tid < 2^18, 0 <= tf < 256, col < 64);
+//   its low 24 bits are exactly the T2 key (col << 18 | tid)
 // wide token = 2 words: tid, (tf << 8) | col          (tf in [-2^23, 2^23))
 // Tokens are grouped by column (ascending), ascending tid within a column.
 constexpr uint32_t kTidBits = 18;
@@ -39,24 +46,11 @@ constexpr uint32_t kTidMask = (1u << kTidBits) - 1;
 //   h2 = {codes (pub | gen << 8), n_clubs, n_friends, n_tok}
 constexpr uint32_t kCodeMissing = 0xFFu;
 
-// 2-choice cuckoo hash over (tag, id): one 32-bit mix, two slots from its top bits
-__host__ __device__ inline uint32_t cuckoo_mix(uint32_t tag, uint32_t id, uint32_t seed) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t x = id ^ __umul24(tag + 1u, 0x9E3779u) ^ seed;
-#else
-    uint32_t x = id ^ ((tag + 1u) * 0x9E3779u) ^ seed;
-#endif
-    x *= 0x9E3779B1u;
-    return x ^ (x >> 16);
-}
-__host__ __device__ inline uint32_t cuckoo_h1(uint32_t mix, int lg) { return mix >> (32 - lg); }
-__host__ __device__ inline uint32_t cuckoo_h2(uint32_t mix, int lg) {
-    return ((mix * 0x85EBCA6Bu) >> (32 - lg)) ^ 1u;
-}
-
-__host__ __device__ inline uint64_t make_key(uint32_t tag, uint32_t id) {
-    return ((uint64_t)tag << 32) | id;
-}
+// 2-choice cuckoo slots of a 32-bit key: one multiply, two bit fields of the product
+__host__ __device__ inline uint32_t cuckoo_x(uint32_t key, uint32_t seed) { return (key ^ seed) * kHashMul; }
+__host__ __device__ inline uint32_t cuckoo_h1(uint32_t x, int lg) { return x >> (32 - lg); }
+__host__ __device__ inline uint32_t cuckoo_h2(uint32_t x, int lg) { return (x >> (32 - 2 * lg)) & ((1u << lg) - 1u); }
+__host__ __device__ inline uint64_t make_entry(uint32_t key, uint32_t val) { return ((uint64_t)val << 32) | key; }
 
 // Per-query constants (A side of profile_similarity).  Built on the host with
 // glibc exp so every table entry is bit-identical to the reference.
@@ -67,8 +61,9 @@ struct QConst {
     uint32_t pubcode, gencode; // kCodeMissing when < 0
     int32_t a_regcnt;          // parts >= 0 (0 -> region term never used)
     int32_t n_clubs, n_friends;// |A.clubs|, |A.friends| with duplicates
-    int32_t cap_log2;          // cuckoo table capacity (log2)
-    uint32_t seed;             // cuckoo hash seed
+    int32_t lg;                // capacity log2 of each of T0..T2
+    int32_t lg_excl;           // capacity log2 of T3
+    uint32_t seed;             // cuckoo hash seed (all tables)
     int32_t n_vals;            // token value entries
     int32_t n_cols;            // T
     double sqrt_clubs, sqrt_friends;     // sqrt((double)|A|)
@@ -82,7 +77,8 @@ struct QConst {
     // normaliser z = zmode ? (s - zmean)/zsd : 6(s - 0.5)   (slots 0..6 fixed, 7+t text)
     double zmean[kNormSlots];
     double zsd[kNormSlots];
-    uint32_t zmode_lo, zmode_hi, zmode_fx, n_hits_max;  // n_hits_max = popcount(colmask)
+    uint32_t zmode_lo, zmode_hi, zmode_fx, n_hits_max;  // n_hits_max: hit-list bytes per lane
+    uint32_t pad2;
 };
 
 // token value of a query hash entry: dot += wq * (tf * idf)
@@ -91,7 +87,7 @@ struct QVal {
     double idf;
 };
 
-// One query image in device memory: QConst + keys[1<<cap_log2] + vals[n_vals].
+// One query image in device memory: QConst + tables[3 * 2^lg + 2^lg_excl] + vals[n_vals].
 struct QImageRef {
     uint32_t const_off;   // byte offset of QConst in the image pool
     uint32_t keys_off;    // byte offset of the key table

@@ -177,17 +177,16 @@ class FasEngine:
     def set_shard(self, shard, nshards):
         self._check(self._L.pf_set_shard(self.h, shard, nshards), "pf_set_shard")
 
-    # -- device-resident scan for multi-GPU benches (d_keys: device pointer, int)
-    def scan_keys_async(self, users, topk, d_keys_ptr, stream_ptr=None):
+    # -- device-resident scan for multi-GPU benches (device pointers and a hipStream_t
+    #    handle as ints; stream 0 is the HIP null stream, exactly as given)
+    def scan_keys_async(self, users, topk, d_keys_ptr, stream_ptr):
         q = _i32(users)
         self._check(self._L.pf_scan_keys_async(self.h, q.ctypes.data, len(q), topk, ctypes.c_void_p(d_keys_ptr),
-                                               ctypes.c_void_p(stream_ptr) if stream_ptr else None),
-                    "pf_scan_keys_async")
+                                               ctypes.c_void_p(stream_ptr)), "pf_scan_keys_async")
 
-    def merge_keys_async(self, d_parts_ptr, nparts, nq, topk, d_out_ptr, stream_ptr=None):
+    def merge_keys_async(self, d_parts_ptr, nparts, nq, topk, d_out_ptr, stream_ptr):
         self._check(self._L.pf_merge_keys_async(self.h, ctypes.c_void_p(d_parts_ptr), nparts, nq, topk,
-                                                ctypes.c_void_p(d_out_ptr),
-                                                ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+                                                ctypes.c_void_p(d_out_ptr), ctypes.c_void_p(stream_ptr)),
                     "pf_merge_keys_async")
 
     @property

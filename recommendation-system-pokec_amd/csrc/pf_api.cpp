@@ -68,12 +68,40 @@ struct pf_ctx {
     DBuf d_stream, d_tile_off, d_tile_steps, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
     pf::DevStore ds{};
     // workspaces
-    DBuf d_pool, d_refs, d_part, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum;
+    DBuf d_pool, d_refs, d_part, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_bound;
+    size_t bound_cap = 0;
     int32_t tile_begin = 0, tile_end = 0;
-    // host sources of in-flight async uploads (kept alive until the next call)
-    std::vector<uint8_t> h_pool;
-    std::vector<pf::QImageRef> h_refs;
-    std::vector<int32_t> h_rows;
+    // pinned staging ring for the per-call query upload (a slot is reused only after
+    // the copy that read it has completed)
+    struct Stage {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    };
+    Stage stage[4];
+    int stage_cur = 0;
+    uint8_t* stage_acquire(size_t bytes) {
+        Stage& st = stage[stage_cur];
+        if (st.done) (void)hipEventSynchronize(st.done);
+        if (st.cap < bytes) {
+            if (st.p) (void)hipHostFree(st.p);
+            st.p = nullptr;
+            st.cap = 0;
+            size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 16);
+            if (hipHostMalloc((void**)&st.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+            st.cap = want;
+        }
+        return st.p;
+    }
+    hipError_t stage_release(hipStream_t s) {
+        Stage& st = stage[stage_cur];
+        stage_cur = (stage_cur + 1) % 4;
+        if (!st.done) {
+            hipError_t e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(st.done, s);
+    }
     // scan-kernel timing pool (pf_profile_*)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
     size_t prof_used = 0;
@@ -236,6 +264,7 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 }
 
 // All-candidates scan for `idx` (valid query indices) into d_keys rows `rows`.
+// One pinned staging buffer [refs | rows | image pool] goes up in a single async copy.
 int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
              hipStream_t s, bool timed) {
     if (idx.empty()) return PF_OK;
@@ -253,17 +282,23 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     }
     const int nq = (int)idx.size();
     const int tiles = c->tile_end - c->tile_begin;
-    int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(8, c->num_cus * 8 / nq)));
-    c->h_pool.swap(im.pool);
-    c->h_refs.swap(im.refs);
-    c->h_rows = rows;
-    HIPCHK(c, c->d_pool.ensure(c->h_pool.size()));
-    HIPCHK(c, hipMemcpyAsync(c->d_pool.p, c->h_pool.data(), c->h_pool.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(c, c->d_refs.ensure(c->h_refs.size() * sizeof(pf::QImageRef)));
-    HIPCHK(c, hipMemcpyAsync(c->d_refs.p, c->h_refs.data(), c->h_refs.size() * sizeof(pf::QImageRef),
-                             hipMemcpyHostToDevice, s));
-    HIPCHK(c, c->d_rows.ensure(c->h_rows.size() * sizeof(int32_t)));
-    HIPCHK(c, hipMemcpyAsync(c->d_rows.p, c->h_rows.data(), c->h_rows.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    // oversubscribed grid (~8 blocks per CU over the batch): blocks that draw short tiles
+    // finish early and new ones fill in, which balances better than one resident round
+    const int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(8, c->num_cus * 8 / nq)));
+    const size_t refs_b = (size_t)nq * sizeof(pf::QImageRef);
+    const size_t rows_b = ((size_t)nq * sizeof(int32_t) + 15) & ~(size_t)15;
+    const size_t total = refs_b + rows_b + im.pool.size();
+    uint8_t* h = c->stage_acquire(total);
+    if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
+    std::memcpy(h, im.refs.data(), refs_b);
+    std::memcpy(h + refs_b, rows.data(), (size_t)nq * sizeof(int32_t));
+    std::memcpy(h + refs_b + rows_b, im.pool.data(), im.pool.size());
+    HIPCHK(c, c->d_pool.ensure(total));
+    HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
+    HIPCHK(c, c->stage_release(s));
+    const pf::QImageRef* d_refs = reinterpret_cast<const pf::QImageRef*>(c->d_pool.as<uint8_t>());
+    const int32_t* d_rows = reinterpret_cast<const int32_t*>(c->d_pool.as<uint8_t>() + refs_b);
+    const uint8_t* d_images = c->d_pool.as<uint8_t>() + refs_b + rows_b;
     HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (c->prof_on) {
@@ -279,20 +314,20 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         timed = true;
     }
     if (timed) HIPCHK(c, hipEventRecord(e0, s));
-    const uint32_t lds = im.max_lds;
-    const bool gtab = im.gtab;
-    HIPCHK(c, pf::launch_scan(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), lds, gtab, nq,
-                              c->tile_begin, c->tile_end, k, blocks, c->d_part.as<uint64_t>(), s));
-    if (timed) HIPCHK(c, hipEventRecord(e1, s));
-    if (timed && e0 != c->ev0) {  // keep pf_last_scan_ms meaningful in profiling mode
+    if (c->bound_cap < (size_t)nq) {  // per-query k-th-key bounds, kept at ~0 between calls
+        HIPCHK(c, c->d_bound.ensure((size_t)nq * 8));
+        HIPCHK(c, hipMemsetAsync(c->d_bound.p, 0xFF, c->d_bound.cap, s));
+        c->bound_cap = c->d_bound.cap / 8;
+    }
+    HIPCHK(c, pf::launch_scan(c->ds, d_images, d_refs, im.max_lds, im.gtab, nq, c->tile_begin, c->tile_end, k, blocks,
+                              c->d_part.as<uint64_t>(), c->d_bound.as<uint64_t>(), s));
+    if (timed) {
+        HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;
         c->last_ev1 = e1;
-    } else if (timed) {
-        c->last_ev0 = c->ev0;
-        c->last_ev1 = c->ev1;
     }
-    HIPCHK(c, pf::launch_merge(c->d_part.as<uint64_t>(), blocks, k, (int64_t)blocks * k, nq, k, d_keys,
-                               c->d_rows.as<int32_t>(), s));
+    HIPCHK(c, pf::launch_merge(c->d_part.as<uint64_t>(), blocks, k, (int64_t)blocks * k, nq, k, d_keys, d_rows,
+                               c->d_bound.as<uint64_t>(), s));
     return PF_OK;
 }
 
@@ -378,6 +413,10 @@ void pf_close(pf_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    for (auto& st : c->stage) {
+        if (st.done) (void)hipEventDestroy(st.done);
+        if (st.p) (void)hipHostFree(st.p);
+    }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -432,7 +471,8 @@ int pf_recommend_interest(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk,
             if (x >= 0) { idx.push_back(x); rows.push_back(i); }
         }
         HIPCHK(c, c->d_out.ensure((size_t)nq * topk * sizeof(uint64_t)));
-        HIPCHK(c, hipMemsetAsync(c->d_out.p, 0xFF, (size_t)nq * topk * sizeof(uint64_t), c->stream));
+        if ((int)idx.size() < nq)  // rows of unknown users stay empty
+            HIPCHK(c, hipMemsetAsync(c->d_out.p, 0xFF, (size_t)nq * topk * sizeof(uint64_t), c->stream));
         const int chunk = 256;
         for (size_t b = 0; b < idx.size(); b += chunk) {
             std::vector<int32_t> ii(idx.begin() + b, idx.begin() + std::min(idx.size(), b + chunk));
@@ -689,12 +729,13 @@ int pf_scan_keys_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, ui
     if (!c || nq < 0 || topk <= 0 || topk > pf::kMaxTopK || (nq && (!q || !d_keys))) return PF_EINVAL;
     (void)hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream;  // as given: NULL is the null stream
-    HIPCHK(c, hipMemsetAsync(d_keys, 0xFF, (size_t)nq * topk * sizeof(uint64_t), s));
     std::vector<int32_t> idx, rows;
     for (int i = 0; i < nq; ++i) {
         int32_t x = c->hc.idx_of(q[i]);
         if (x >= 0) { idx.push_back(x); rows.push_back(i); }
     }
+    if ((int)idx.size() < nq)  // rows of unknown users stay empty
+        HIPCHK(c, hipMemsetAsync(d_keys, 0xFF, (size_t)nq * topk * sizeof(uint64_t), s));
     return scan_all(c, idx, rows, topk, d_keys, s, true);
 }
 
@@ -703,7 +744,7 @@ int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int3
     if (!c || nparts < 1 || nq < 0 || topk <= 0 || topk > pf::kMaxTopK) return PF_EINVAL;
     (void)hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, nullptr, s));
+    HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, nullptr, nullptr, s));
     return PF_OK;
 }
 

@@ -423,7 +423,8 @@ template <bool PACKED, bool GTAB>
 __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                                 const QImageRef* __restrict__ refs, int32_t tile_begin,
                                                                 int32_t tile_end, int32_t k,
-                                                                uint64_t* __restrict__ out_keys) {
+                                                                uint64_t* __restrict__ out_keys,
+                                                                unsigned long long* __restrict__ bound) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const QImageRef r = refs[blockIdx.y];
     char* scratch;
@@ -452,21 +453,66 @@ __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, con
         const int n = (kScanThreads / 64) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         if (lane < k) out_keys[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * k + lane] = acc;
+        // this block holds k keys <= its k-th key, so the global k-th key is <= the minimum
+        // of the blocks' k-th keys: the merge only has to look at keys below that bound
+        const uint64_t kth = rdlane64(acc, k - 1);
+        if (lane == 0) atomicMin(&bound[blockIdx.y], (unsigned long long)kth);
     }
 }
 
 // ---------------------------------------------------------------- K2: merge
 // Key lists in[part * part_stride + q * query_stride + j] (j < k) -> out[row(q) * k + j].
-// 1024 threads per query; every lane keeps 8 loads in flight, then the 16 wave
-// lists meet in LDS.
-__global__ __launch_bounds__(1024) void topk_merge_kernel(const uint64_t* __restrict__ in, int32_t nparts,
-                                                          int64_t part_stride, int64_t query_stride, int32_t k,
-                                                          uint64_t* __restrict__ out,
-                                                          const int32_t* __restrict__ out_rows) {
+// With a bound (from the scan), only keys <= bound[q] can be in the top-k: they are
+// compacted into LDS and one wave merges them; the bound is then reset for the next call.
+// Without a bound (or on compaction overflow) every wave pushes its share of all keys.
+constexpr int kMergeThreads = 1024;
+constexpr int kSurvivorCap = 2048;
+__global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_t* __restrict__ in, int32_t nparts,
+                                                                   int64_t part_stride, int64_t query_stride, int32_t k,
+                                                                   uint64_t* __restrict__ out,
+                                                                   const int32_t* __restrict__ out_rows,
+                                                                   unsigned long long* __restrict__ bound) {
+    __shared__ uint64_t surv[kSurvivorCap];
     __shared__ uint64_t sc[16 * 64];
+    __shared__ int nsurv;
     const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t list = ~0ull;
     const int64_t total = (int64_t)nparts * k;
+    const uint64_t thr = bound ? (uint64_t)bound[q] : ~0ull;
+    if (threadIdx.x == 0) nsurv = 0;
+    __syncthreads();
+    if (bound) {
+        for (int64_t base = 0; base < total; base += (int64_t)blockDim.x * 8) {
+            uint64_t x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
+                x[u] = ~0ull;
+                if (i < total) {
+                    const int32_t part = (int32_t)i / k, j = (int32_t)i - part * k;
+                    x[u] = in[(int64_t)part * part_stride + q * query_stride + j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (x[u] <= thr && x[u] != ~0ull) {
+                    const int pos = atomicAdd(&nsurv, 1);
+                    if (pos < kSurvivorCap) surv[pos] = x[u];
+                }
+        }
+    }
+    __syncthreads();
+    const int ns = nsurv;
+    if (bound && ns <= kSurvivorCap) {
+        if (wave == 0) {
+            uint64_t acc = ~0ull;
+            for (int b = 0; b < ns; b += 64) topk_push(acc, b + lane < ns ? surv[b + lane] : ~0ull, k, lane);
+            const int row = out_rows ? out_rows[q] : q;
+            if (lane < k) out[(size_t)row * k + lane] = acc;
+            if (lane == 0) bound[q] = ~0ull;
+        }
+        return;
+    }
+    uint64_t list = ~0ull;
     for (int64_t base = 0; base < total; base += (int64_t)blockDim.x * 8) {
         uint64_t x[8];
 #pragma unroll
@@ -489,6 +535,7 @@ __global__ __launch_bounds__(1024) void topk_merge_kernel(const uint64_t* __rest
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         const int row = out_rows ? out_rows[q] : q;
         if (lane < k) out[(size_t)row * k + lane] = acc;
+        if (bound && lane == 0) bound[q] = ~0ull;
     }
 }
 
@@ -528,11 +575,12 @@ __global__ __launch_bounds__(256) void collab_sum_kernel(const float* __restrict
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t lds, bool gtab,
-                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* out_keys, hipStream_t s) {
+                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* out_keys, uint64_t* bound,
+                       hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     dim3 grid(blocks, nq), block(kScanThreads);
 #define PF_SCAN(P, G) hipLaunchKernelGGL((fas_scan_kernel<P, G>), grid, block, lds, s, st, pool, refs_dev, tile_begin, \
-                                         tile_end, k, out_keys)
+                                         tile_end, k, out_keys, (unsigned long long*)bound)
     if (st.packed) { if (gtab) PF_SCAN(true, true); else PF_SCAN(true, false); }
     else { if (gtab) PF_SCAN(false, true); else PF_SCAN(false, false); }
 #undef PF_SCAN
@@ -540,10 +588,10 @@ hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef*
 }
 
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
-                        uint64_t* out, const int32_t* out_rows, hipStream_t s) {
+                        uint64_t* out, const int32_t* out_rows, uint64_t* bound, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(topk_merge_kernel, dim3(nq), dim3(1024), 0, s, in, nparts, part_stride, query_stride, k, out,
-                       out_rows);
+    hipLaunchKernelGGL(topk_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, s, in, nparts, part_stride, query_stride,
+                       k, out, out_rows, (unsigned long long*)bound);
     return hipGetLastError();
 }
 

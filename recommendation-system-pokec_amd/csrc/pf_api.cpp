@@ -68,8 +68,7 @@ struct pf_ctx {
     DBuf d_stream, d_tile_off, d_tile_steps, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
     pf::DevStore ds{};
     // workspaces
-    DBuf d_pool, d_refs, d_part, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_bound;
-    size_t bound_cap = 0;
+    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part;
     int32_t tile_begin = 0, tile_end = 0;
     // pinned staging ring for the per-call query upload (a slot is reused only after
     // the copy that read it has completed)
@@ -287,18 +286,22 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     const int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(8, c->num_cus * 8 / nq)));
     const size_t refs_b = (size_t)nq * sizeof(pf::QImageRef);
     const size_t rows_b = ((size_t)nq * sizeof(int32_t) + 15) & ~(size_t)15;
-    const size_t total = refs_b + rows_b + im.pool.size();
+    const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);  // zeros: the per-launch rendezvous
+    const size_t total = refs_b + rows_b + sync_b + im.pool.size();
     uint8_t* h = c->stage_acquire(total);
     if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
     std::memcpy(h, im.refs.data(), refs_b);
     std::memcpy(h + refs_b, rows.data(), (size_t)nq * sizeof(int32_t));
-    std::memcpy(h + refs_b + rows_b, im.pool.data(), im.pool.size());
+    std::memset(h + refs_b + rows_b, 0, sync_b);
+    std::memcpy(h + refs_b + rows_b + sync_b, im.pool.data(), im.pool.size());
     HIPCHK(c, c->d_pool.ensure(total));
     HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
     HIPCHK(c, c->stage_release(s));
-    const pf::QImageRef* d_refs = reinterpret_cast<const pf::QImageRef*>(c->d_pool.as<uint8_t>());
-    const int32_t* d_rows = reinterpret_cast<const int32_t*>(c->d_pool.as<uint8_t>() + refs_b);
-    const uint8_t* d_images = c->d_pool.as<uint8_t>() + refs_b + rows_b;
+    uint8_t* base = c->d_pool.as<uint8_t>();
+    const pf::QImageRef* d_refs = reinterpret_cast<const pf::QImageRef*>(base);
+    const int32_t* d_rows = reinterpret_cast<const int32_t*>(base + refs_b);
+    pf::ScanSync* d_sync = reinterpret_cast<pf::ScanSync*>(base + refs_b + rows_b);
+    const uint8_t* d_images = base + refs_b + rows_b + sync_b;
     HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (c->prof_on) {
@@ -314,20 +317,13 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         timed = true;
     }
     if (timed) HIPCHK(c, hipEventRecord(e0, s));
-    if (c->bound_cap < (size_t)nq) {  // per-query k-th-key bounds, kept at ~0 between calls
-        HIPCHK(c, c->d_bound.ensure((size_t)nq * 8));
-        HIPCHK(c, hipMemsetAsync(c->d_bound.p, 0xFF, c->d_bound.cap, s));
-        c->bound_cap = c->d_bound.cap / 8;
-    }
     HIPCHK(c, pf::launch_scan(c->ds, d_images, d_refs, im.max_lds, im.gtab, nq, c->tile_begin, c->tile_end, k, blocks,
-                              c->d_part.as<uint64_t>(), c->d_bound.as<uint64_t>(), s));
+                              c->d_part.as<uint64_t>(), d_sync, d_keys, d_rows, s));
     if (timed) {
         HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;
         c->last_ev1 = e1;
     }
-    HIPCHK(c, pf::launch_merge(c->d_part.as<uint64_t>(), blocks, k, (int64_t)blocks * k, nq, k, d_keys, d_rows,
-                               c->d_bound.as<uint64_t>(), s));
     return PF_OK;
 }
 
@@ -744,7 +740,7 @@ int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int3
     if (!c || nparts < 1 || nq < 0 || topk <= 0 || topk > pf::kMaxTopK) return PF_EINVAL;
     (void)hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, nullptr, nullptr, s));
+    HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, s));
     return PF_OK;
 }
 

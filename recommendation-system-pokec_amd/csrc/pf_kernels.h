@@ -12,16 +12,15 @@ struct PairBlock {
 };
 
 // lds: dynamic LDS bytes per block = max over the batch of
-//   sizeof(QConst) + staged keys/vals + n_hits_max * threads * 8 + 2048
+//   sizeof(QConst) + staged keys/vals + n_hits_max * threads + 2048
 // gtab: at least one image of the batch probes its table in global memory (lds_bytes == 0);
 // the whole launch then uses the global-table variant.
 hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t lds, bool gtab,
-                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* out_keys, uint64_t* bound,
-                       hipStream_t s);
-// bound: per-query upper bound on the k-th key written by launch_scan (reset to ~0 here),
-// or null for a plain merge of key lists
+                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* parts, ScanSync* sync,
+                       uint64_t* out, const int32_t* out_rows, hipStream_t s);
+// plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
-                        uint64_t* out, const int32_t* out_rows, uint64_t* bound, hipStream_t s);
+                        uint64_t* out, hipStream_t s);
 hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
                         bool gtab, const PairBlock* blocks, int nblocks, const int32_t* slots, float* out,
                         hipStream_t s);

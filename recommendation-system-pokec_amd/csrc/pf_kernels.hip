@@ -419,12 +419,22 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
 }
 
 // ---------------------------------------------------------------- K1: scan
+// write-through store / L1-bypassing load of a word handed between workgroups of a launch
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool PACKED, bool GTAB>
 __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                                 const QImageRef* __restrict__ refs, int32_t tile_begin,
                                                                 int32_t tile_end, int32_t k,
-                                                                uint64_t* __restrict__ out_keys,
-                                                                unsigned long long* __restrict__ bound) {
+                                                                uint64_t* __restrict__ parts,
+                                                                ScanSync* __restrict__ sync,
+                                                                uint64_t* __restrict__ out,
+                                                                const int32_t* __restrict__ out_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const QImageRef r = refs[blockIdx.y];
     char* scratch;
@@ -448,70 +458,131 @@ __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, con
     __syncthreads();
     if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
+    // Fused cross-block merge (no second launch).  Each block publishes its sorted k-list
+    // with write-through (sc1) stores, drains them and takes a ticket; the last block of
+    // the query merges, reading the lists with sc1 loads (cdna_hip_programming.md
+    // Guideline 16, R1: no L2 write-back or acquire fence needed).
+    ScanSync* sy = sync + blockIdx.y;
+    uint64_t* qparts = parts + (size_t)blockIdx.y * gridDim.x * k;
+    // tail scratch in the (now idle) hit lists: flag, threshold, block count, block ids
+    int* s_flag = reinterpret_cast<int*>(v.hits);
+    int* s_cnt = s_flag + 1;
+    uint64_t* s_T = reinterpret_cast<uint64_t*>(s_flag + 2);
+    int* s_blk = s_flag + 4;
     if (wave == 0) {
         uint64_t acc = ~0ull;
         const int n = (kScanThreads / 64) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        if (lane < k) out_keys[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * k + lane] = acc;
-        // this block holds k keys <= its k-th key, so the global k-th key is <= the minimum
-        // of the blocks' k-th keys: the merge only has to look at keys below that bound
-        const uint64_t kth = rdlane64(acc, k - 1);
-        if (lane == 0) atomicMin(&bound[blockIdx.y], (unsigned long long)kth);
+        if (lane < k) st_agent(qparts + (size_t)blockIdx.x * k + lane, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(&sy->done, 1u);
+        if (lane == 0) {
+            *s_flag = t == gridDim.x - 1;
+            *s_cnt = 0;
+        }
+    }
+    __syncthreads();
+    if (!*s_flag) return;
+    const int nb = (int)gridDim.x;
+    const int row = out_rows ? out_rows[blockIdx.y] : (int)blockIdx.y;
+    // Pass 1: the k smallest of every block's first j keys (j * nb >= 2k).  Its k-th key T
+    // bounds the final k-th key from above, and a block can hold further keys <= T only
+    // if its j-th key is <= T, which at most k blocks satisfy (keys are distinct).
+    const int j = min(k, max(1, (2 * k + nb - 1) / nb));
+    const int n1 = nb * j;
+    list = ~0ull;
+    for (int base = wave * 512; base < n1; base += kScanThreads * 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 64 + lane;
+            x[u] = ~0ull;
+            if (i < n1) {
+                const int blk = i / j;
+                x[u] = ld_agent(qparts + (size_t)blk * k + (i - blk * j));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) topk_push(list, x[u], k, lane);
+    }
+    if (lane < k) sc[wave * k + lane] = list;
+    __syncthreads();
+    uint64_t acc = ~0ull;
+    if (wave == 0) {
+        const int n = (kScanThreads / 64) * k;
+        for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
+        if (lane == 0) *s_T = rdlane64(acc, k - 1);
+    }
+    __syncthreads();
+    const uint64_t T = *s_T;
+    if (T == ~0ull) {
+        // fewer than k keys among the first j of every block: merge every list in full
+        list = ~0ull;
+        const int total = nb * k;
+        for (int base = wave * 512; base < total; base += kScanThreads * 8) {
+            uint64_t x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = base + u * 64 + lane;
+                x[u] = i < total ? ld_agent(qparts + i) : ~0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) topk_push(list, x[u], k, lane);
+        }
+        __syncthreads();
+        if (lane < k) sc[wave * k + lane] = list;
+        __syncthreads();
+        if (wave == 0) {
+            acc = ~0ull;
+            const int n = (kScanThreads / 64) * k;
+            for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
+            if (lane < k) out[(size_t)row * k + lane] = acc;
+        }
+        return;
+    }
+    // Pass 2: the remaining keys of the blocks whose j-th key is <= T
+    if (j < k) {
+        for (int b = (int)threadIdx.x; b < nb; b += kScanThreads) {
+            const uint64_t y = ld_agent(qparts + (size_t)b * k + (j - 1));
+            if (y <= T) {
+                const int p = atomicAdd(s_cnt, 1);
+                if (p < kMaxTopK) s_blk[p] = b;
+            }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int nblk = min(*s_cnt, kMaxTopK), rest = k - j, n2 = nblk * rest;
+        for (int base = 0; base < n2; base += 512) {
+            uint64_t x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = base + u * 64 + lane;
+                x[u] = ~0ull;
+                if (i < n2) {
+                    const int bi = i / rest;
+                    x[u] = ld_agent(qparts + (size_t)s_blk[bi] * k + j + (i - bi * rest));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) topk_push(acc, x[u] <= T ? x[u] : ~0ull, k, lane);
+        }
+        if (lane < k) out[(size_t)row * k + lane] = acc;
     }
 }
 
 // ---------------------------------------------------------------- K2: merge
-// Key lists in[part * part_stride + q * query_stride + j] (j < k) -> out[row(q) * k + j].
-// With a bound (from the scan), only keys <= bound[q] can be in the top-k: they are
-// compacted into LDS and one wave merges them; the bound is then reset for the next call.
-// Without a bound (or on compaction overflow) every wave pushes its share of all keys.
+// Key lists in[part * part_stride + q * query_stride + j] (j < k) -> out[q * k + j]
+// (the cross-shard merge after the all-gather; one block per query, every wave pushes
+// its share of the keys, then wave 0 merges the wave lists).
 constexpr int kMergeThreads = 1024;
-constexpr int kSurvivorCap = 2048;
 __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_t* __restrict__ in, int32_t nparts,
                                                                    int64_t part_stride, int64_t query_stride, int32_t k,
-                                                                   uint64_t* __restrict__ out,
-                                                                   const int32_t* __restrict__ out_rows,
-                                                                   unsigned long long* __restrict__ bound) {
-    __shared__ uint64_t surv[kSurvivorCap];
+                                                                   uint64_t* __restrict__ out) {
     __shared__ uint64_t sc[16 * 64];
-    __shared__ int nsurv;
     const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t total = (int64_t)nparts * k;
-    const uint64_t thr = bound ? (uint64_t)bound[q] : ~0ull;
-    if (threadIdx.x == 0) nsurv = 0;
-    __syncthreads();
-    if (bound) {
-        for (int64_t base = 0; base < total; base += (int64_t)blockDim.x * 8) {
-            uint64_t x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
-                x[u] = ~0ull;
-                if (i < total) {
-                    const int32_t part = (int32_t)i / k, j = (int32_t)i - part * k;
-                    x[u] = in[(int64_t)part * part_stride + q * query_stride + j];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (x[u] <= thr && x[u] != ~0ull) {
-                    const int pos = atomicAdd(&nsurv, 1);
-                    if (pos < kSurvivorCap) surv[pos] = x[u];
-                }
-        }
-    }
-    __syncthreads();
-    const int ns = nsurv;
-    if (bound && ns <= kSurvivorCap) {
-        if (wave == 0) {
-            uint64_t acc = ~0ull;
-            for (int b = 0; b < ns; b += 64) topk_push(acc, b + lane < ns ? surv[b + lane] : ~0ull, k, lane);
-            const int row = out_rows ? out_rows[q] : q;
-            if (lane < k) out[(size_t)row * k + lane] = acc;
-            if (lane == 0) bound[q] = ~0ull;
-        }
-        return;
-    }
     uint64_t list = ~0ull;
     for (int64_t base = 0; base < total; base += (int64_t)blockDim.x * 8) {
         uint64_t x[8];
@@ -520,7 +591,7 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
             const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
             x[u] = ~0ull;
             if (i < total) {
-                const int32_t part = (int32_t)i / k, j = (int32_t)i - part * k;
+                const int32_t part = (int32_t)(i / k), j = (int32_t)(i - (int64_t)part * k);
                 x[u] = in[(int64_t)part * part_stride + q * query_stride + j];
             }
         }
@@ -533,9 +604,7 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
         uint64_t acc = ~0ull;
         const int n = (int)(blockDim.x >> 6) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        const int row = out_rows ? out_rows[q] : q;
-        if (lane < k) out[(size_t)row * k + lane] = acc;
-        if (bound && lane == 0) bound[q] = ~0ull;
+        if (lane < k) out[(size_t)q * k + lane] = acc;
     }
 }
 
@@ -575,12 +644,12 @@ __global__ __launch_bounds__(256) void collab_sum_kernel(const float* __restrict
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t lds, bool gtab,
-                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* out_keys, uint64_t* bound,
-                       hipStream_t s) {
+                       int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* parts, ScanSync* sync,
+                       uint64_t* out, const int32_t* out_rows, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     dim3 grid(blocks, nq), block(kScanThreads);
 #define PF_SCAN(P, G) hipLaunchKernelGGL((fas_scan_kernel<P, G>), grid, block, lds, s, st, pool, refs_dev, tile_begin, \
-                                         tile_end, k, out_keys, (unsigned long long*)bound)
+                                         tile_end, k, parts, sync, out, out_rows)
     if (st.packed) { if (gtab) PF_SCAN(true, true); else PF_SCAN(true, false); }
     else { if (gtab) PF_SCAN(false, true); else PF_SCAN(false, false); }
 #undef PF_SCAN
@@ -588,10 +657,10 @@ hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef*
 }
 
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
-                        uint64_t* out, const int32_t* out_rows, uint64_t* bound, hipStream_t s) {
+                        uint64_t* out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     hipLaunchKernelGGL(topk_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, s, in, nparts, part_stride, query_stride,
-                       k, out, out_rows, (unsigned long long*)bound);
+                       k, out);
     return hipGetLastError();
 }
 

@@ -95,6 +95,13 @@ struct QImageRef {
     uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 
+// Per-query rendezvous of one scan launch: blocks finished.  Zeroed by the host before
+// every launch (it rides in the query upload).  Padded to 16 B.
+struct ScanSync {
+    unsigned int done;
+    unsigned int pad[3];
+};
+
 // top-k key: ascending key == (score desc, uid asc), recommender_graph.cpp:97-101
 __host__ __device__ inline uint64_t score_key(float s, int32_t uid) {
     union { float f; uint32_t u; } v;

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpokec_fas.so")
+LIB_PATH = os.environ.get("PF_LIB_PATH") or os.path.join(HERE, "libpokec_fas.so")
 
 PF_OK, PF_EINVAL, PF_ENODEV, PF_ENOMEM, PF_ENOTFOUND, PF_EUNSUPP = 0, -1, -2, -3, -4, -5
 PF_MODE_FOF, PF_MODE_ALL = 0, 1

@@ -119,3 +119,25 @@ def test_big_collab_and_clubs_vs_oracle(big):
         g, = eng.recommend_clubs_collab([u], 20, 5000)
         r, = orc.clubs([u], 20, 5000)
         assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def test_big_top64_vs_oracle(big):
+    c, eng, orc = big
+    q = [2, 777, 12345, 19999]
+    for u, g, r in zip(q, eng.recommend_interest_all(q, 64), orc.interest(q, 64, tl.PF_MODE_ALL, 0)):
+        assert list(g[0]) == list(r[0]), u
+        assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+@pytest.mark.parametrize("env", [{"PF_STAGE_LIMIT": "0"}, {"PF_STAGE_LIMIT": "1024"}],
+                         ids=["global-tables", "threshold-1k"])
+def test_kernel_variants(env):
+    """Forced variants: query tables probed in global memory, always, or whenever one
+    query of the batch has tables above 1 KiB (the whole launch then probes global)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_variant_check.py")], env={**os.environ, **env},
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr

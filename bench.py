@@ -130,12 +130,12 @@ def main():
     final = torch.empty((Q, k), dtype=torch.int64, device="cuda")
 
     def step(i):
+        if world == 1:  # the scan's fused merge already yields the final top-k
+            eng.scan_keys_async(qstream[i], k, final.data_ptr(), sptr)
+            return
         eng.scan_keys_async(qstream[i], k, local_keys.data_ptr(), sptr)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, local_keys)
-            eng.merge_keys_async(gathered.data_ptr(), world, Q, k, final.data_ptr(), sptr)
-        else:
-            final.copy_(local_keys)
+        dist.all_gather_into_tensor(gathered, local_keys)
+        eng.merge_keys_async(gathered.data_ptr(), world, Q, k, final.data_ptr(), sptr)
 
     for i in range(warm):
         step(i)
@@ -189,7 +189,7 @@ def main():
         "config": {"workload": "cfg2: full 1.6M-user single-query interest FAS all-candidates top-10"
                                + ("" if world == 1 else f"; {Q} queries/step, candidates sharded over {world} GPUs, "
                                                         "RCCL all-gather of per-shard top-10"),
-                   "n_users": args.users, "queries_per_step": Q, "topk": k,
+                   "workload_key": workload, "n_users": args.users, "queries_per_step": Q, "topk": k,
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -1,0 +1,93 @@
+/*
+ * pokec_io.h — C ABI of the host-side data path around the FAS engine: the
+ * reference's start-up loaders and its hold-out drivers, in front of
+ * pokec_fas.h.
+ *
+ *   pf_dataset_load      api_cli.cpp:86-167 start-up, from a directory holding
+ *                        config/text_columns.txt and data/:
+ *                          load_text_columns_from_file   src/utils.cpp:13-24
+ *                          GraphBuilder::load_serialized src/graph_builder.cpp:39-59   (A17)
+ *                          build_adj_list                src/utils.cpp:26-34           (A17)
+ *                          load_users_encoded            src/user_loader.cpp:10-96     (A2)
+ *                          split_csv_line / parse_tok_field src/utils.cpp:36-68        (A2)
+ *                          load_median_age / compute_median_age_from_profiles /
+ *                          fill_missing_ages             src/user_loader.cpp:98-140    (A3)
+ *                          load_column_normalizers       src/utils.cpp:123-142         (A18)
+ *                          VocabBuilder::load_vocab (club names only)
+ *                                                        src/vocab_builder.cpp:133-197
+ *   pf_dataset_profile_json  write_profile_json          src/api_cli.cpp:49-84
+ *   pf_holdout_friends       run_friends_holdout_test    src/test.cpp:13-105           (A19)
+ *   pf_recommendation_tests  run_recommendation_tests_sample
+ *                                                        src/recommendation_tests.cpp:68-169 (A19)
+ *
+ * The loaders keep the reference's hash containers (same key types, same
+ * insertion sequence), so every order the reference derives from
+ * unordered_map iteration is reproduced: the profile order the drivers
+ * shuffle, the adjacency order, and the token order in profile JSON.
+ * The loaders run on the host only and need no GPU. The drivers call the engine.
+ * Status codes and pf_last_error(NULL) are shared with pokec_fas.h.
+ */
+#ifndef POKEC_IO_H
+#define POKEC_IO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pokec_fas.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* load_users_encoded reads at most this many data lines (user_loader.cpp:34) */
+#define PF_LOAD_REFERENCE_CAP 100000
+
+typedef struct pf_dataset pf_dataset;
+
+typedef struct pf_dataset_info {
+    int64_t lines_read;      /* data lines consumed by the user loader (its counter c)  */
+    int32_t n_profiles;      /* profiles after de-duplication by uid                    */
+    int32_t n_cols;          /* text columns                                            */
+    int32_t n_adj;           /* adjacency rows                                          */
+    int32_t median_age;      /* loaded or computed median                               */
+    int32_t median_loaded;   /* 1: from data/median_age.txt                             */
+    int32_t ages_replaced;   /* zero ages filled with the median                        */
+    int32_t n_normalizers;   /* entries of column_normalizers.csv (0 = absent/empty)    */
+    int32_t vocab_loaded;    /* 1: data/tokens.csv exists (VocabBuilder::load_vocab)    */
+    int32_t n_club_names;
+} pf_dataset_info;
+
+/* Load `root`/config + `root`/data like api_cli's start-up.  max_lines caps
+ * the user loader's data lines (PF_LOAD_REFERENCE_CAP reproduces the
+ * reference; 0 = no cap, for the full 1.6M-user configurations).  Fails with
+ * PF_EINVAL when config/text_columns.txt, data/users_encoded.csv or
+ * data/adjacency.csv cannot be read. */
+int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out);
+void pf_dataset_free(pf_dataset* ds);
+/* Engine input view (valid while ds lives): IDF from profiles, normalisers as loaded. */
+const pf_corpus_desc* pf_dataset_desc(const pf_dataset* ds);
+int pf_dataset_info_get(const pf_dataset* ds, pf_dataset_info* out);
+/* Text column name t (NULL if out of range). */
+const char* pf_dataset_column(const pf_dataset* ds, int32_t t);
+/* uids in the iteration order of the reference's profiles map / adj_list map;
+ * *n gets the full count, at most cap ids are written. */
+int pf_dataset_profile_order(const pf_dataset* ds, int32_t* out, int32_t cap, int32_t* n);
+int pf_dataset_adj_order(const pf_dataset* ds, int32_t* out, int32_t cap, int32_t* n);
+/* write_profile_json for uid into buf (NUL-terminated when it fits); *len gets the
+ * length without the NUL.  PF_ENOTFOUND for an unknown uid. */
+int pf_dataset_profile_json(const pf_dataset* ds, int32_t uid, char* buf, int64_t cap, int64_t* len);
+/* Club slug for a club id from data/clubs_map.csv (NULL if none). */
+const char* pf_dataset_club_name(const pf_dataset* ds, int32_t club_id);
+
+/* run_friends_holdout_test: per tested user, hits/hold_k in file order.
+ * ctx must have been opened on pf_dataset_desc(ds); its adjacency is restored on return. */
+int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, double* out_ratios, int32_t cap,
+                       int32_t* n_out);
+/* run_recommendation_tests_sample: out[5] = {graph_hit_rate, collab_hit_rate,
+ * interest_hit_rate, avg_club_prec_at_k, avg_club_recall_at_k}. */
+int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POKEC_IO_H */

@@ -21,6 +21,7 @@
 namespace {
 
 thread_local std::string g_open_error;
+
 constexpr uint32_t kLdsLimit = 64 * 1024;  // query images above this probe from global memory
 
 struct DBuf {
@@ -54,6 +55,10 @@ void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
 }
 
 }  // namespace
+
+namespace pf {
+void set_open_error(const std::string& m) { g_open_error = m; }
+}  // namespace pf
 
 struct pf_ctx {
     int device = 0;

@@ -1,0 +1,622 @@
+// pf_dataset.cpp — the reference's start-up loaders (include/pokec_io.h), restated
+// for the product: api_cli.cpp:86-167 reads text columns, adjacency, encoded users,
+// the median age and the normalisers, then hands the maps to Recommender.  Here the
+// result is a pf_corpus_desc for pf_open plus the reference's own hash containers
+// (same key types, same insertion sequence), which fix every iteration order the
+// reference exposes: the profiles map (hold-out drivers), adj_list, and each
+// token_cols map (profile JSON).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "pokec_io.h"
+
+namespace pf {
+void set_open_error(const std::string& m);
+}
+
+namespace {
+
+constexpr int kFixed = PF_NUM_FIXED;
+const char* const kFixedKeys[kFixed] = {"public", "gender", "completion", "age", "region", "clubs", "friends"};
+
+// split_csv_line (utils.cpp:36-50): '"' toggles quoting and is dropped, no escapes.
+// Reuses the strings of `out` (assign keeps their capacity).
+void split_csv(const std::string& line, std::vector<std::string>& out, size_t& n) {
+    n = 0;
+    auto next = [&]() -> std::string& {
+        if (n == out.size()) out.emplace_back();
+        std::string& s = out[n++];
+        s.clear();
+        return s;
+    };
+    std::string* cur = &next();
+    bool q = false;
+    for (char c : line) {
+        if (c == '"') { q = !q; continue; }
+        if (c == ',' && !q) cur = &next();
+        else cur->push_back(c);
+    }
+}
+
+// split_csv_line_local (vocab_builder.cpp:123-131): as above, plus "" inside quotes = '"'
+std::vector<std::string> split_csv_local(const std::string& line) {
+    std::vector<std::string> out;
+    std::string cur;
+    bool q = false;
+    for (size_t i = 0; i < line.size(); ++i) {
+        const char c = line[i];
+        if (c == '"') {
+            if (q && i + 1 < line.size() && line[i + 1] == '"') { cur.push_back('"'); ++i; continue; }
+            q = !q;
+            continue;
+        }
+        if (c == ',' && !q) { out.push_back(cur); cur.clear(); }
+        else cur.push_back(c);
+    }
+    out.push_back(cur);
+    return out;
+}
+
+// std::getline(stringstream(s), tok, sep) tokens: [b, e) ranges of s; no trailing empty token
+template <class F>
+void for_each_token(const std::string& s, char sep, F&& f) {
+    size_t b = 0;
+    const size_t n = s.size();
+    while (b < n) {
+        size_t e = s.find(sep, b);
+        if (e == std::string::npos) e = n;
+        f(b, e);
+        b = e + 1;
+    }
+}
+
+// C atoi of s[b..): stops at the first non-digit, which the separators (';' ':' ',') are
+int atoi_at(const std::string& s, size_t b) { return atoi(s.c_str() + b); }
+
+bool is_space(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+
+// One parsed users_encoded row (UserProfile, include/user_profile.h:10-20)
+struct Row {
+    int32_t uid, pub, comp, gen, age;
+    int32_t reg[3];
+    std::vector<uint32_t> clubs, friends;
+    std::vector<int32_t> col_off;                 // T+1 offsets into tok
+    std::vector<std::pair<int32_t, int32_t>> tok; // per column: first-insertion order, last value
+};
+
+}  // namespace
+
+struct pf_dataset {
+    std::vector<std::string> cols;
+    std::vector<Row> rows;                             // slot = first appearance of the uid
+    std::unordered_map<int, int32_t> profiles;         // uid -> slot, built like out_profiles
+    std::unordered_map<int, std::vector<int>> adj_list;// built like build_adj_list(gb.adjacency)
+    std::unordered_map<std::string, std::pair<float, float>> norms;
+    std::unordered_map<int, std::string> club_names;
+    pf_dataset_info info{};
+    // pf_corpus_desc storage
+    std::vector<int32_t> uid, pub, comp, gen, age, reg, tok_tid, tok_tf, adj_uid, adj_nbr;
+    std::vector<int64_t> club_off, friend_off, tok_off, adj_off;
+    std::vector<uint32_t> club_ids, friend_ids;
+    std::vector<uint8_t> npres;
+    std::vector<float> nmean, nsd;
+    pf_corpus_desc desc{};
+};
+
+namespace {
+
+int fail(const std::string& m) {
+    pf::set_open_error(m);
+    return PF_EINVAL;
+}
+
+// load_text_columns_from_file (utils.cpp:13-24)
+bool load_columns(const std::string& path, std::vector<std::string>& out) {
+    std::ifstream in(path);
+    if (!in.is_open()) return false;
+    std::string line;
+    while (std::getline(in, line))
+        if (!line.empty()) out.push_back(line);
+    return true;
+}
+
+// GraphBuilder::load_serialized (graph_builder.cpp:39-59) + build_adj_list (utils.cpp:26-34)
+bool load_adjacency(const std::string& path, std::unordered_map<int, std::vector<int>>& adj_list) {
+    std::ifstream in(path);
+    if (!in.is_open()) return false;
+    std::unordered_map<int, std::vector<int>> adjacency;  // GraphBuilder::adjacency
+    std::string line;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        bool first = true;
+        int uid = -1;
+        for_each_token(line, ',', [&](size_t b, size_t e) {
+            while (b < e && is_space((unsigned char)line[b])) ++b;  // trim_copy_g
+            if (b == e) return;
+            if (first) { uid = atoi_at(line, b); first = false; return; }
+            adjacency[uid].push_back(atoi_at(line, b));
+        });
+    }
+    for (auto& kv : adjacency) {  // build_adj_list: out[u].push_back in adjacency order
+        std::vector<int>& o = adj_list[kv.first];
+        o.insert(o.end(), kv.second.begin(), kv.second.end());
+    }
+    return true;
+}
+
+// load_users_encoded (user_loader.cpp:10-96)
+bool load_users(const std::string& path, int64_t max_lines, pf_dataset& d) {
+    std::ifstream in(path);
+    if (!in.is_open()) return false;
+    std::string line;
+    if (!std::getline(in, line)) return false;  // header
+    const size_t T = d.cols.size();
+    std::vector<std::string> parts;
+    size_t np = 0;
+    int64_t c = 0;
+    while (std::getline(in, line) && (max_lines <= 0 || c < max_lines)) {
+        ++c;
+        if (line.empty()) continue;
+        split_csv(line, parts, np);
+        const int uid = atoi(parts[0].c_str());
+        if (uid == 0) continue;
+        auto has = [&](size_t i) { return i < np && !parts[i].empty(); };
+        Row r;
+        r.uid = uid;
+        r.pub = has(1) ? atoi(parts[1].c_str()) : -1;
+        r.comp = has(2) ? atoi(parts[2].c_str()) : -1;
+        r.gen = has(3) ? atoi(parts[3].c_str()) : -1;
+        r.age = has(5) ? atoi(parts[5].c_str()) : 0;
+        if (has(6))
+            for_each_token(parts[6], ';', [&](size_t b, size_t e) {
+                if (b < e) r.clubs.push_back((uint32_t)atoi_at(parts[6], b));
+            });
+        if (has(7))
+            for_each_token(parts[7], ';', [&](size_t b, size_t e) {
+                if (b < e) r.friends.push_back((uint32_t)atoi_at(parts[7], b));
+            });
+        r.reg[0] = r.reg[1] = r.reg[2] = -1;
+        if (has(4)) {
+            std::string rf = parts[4];
+            if (rf.size() >= 2 && rf.front() == '"' && rf.back() == '"') rf = rf.substr(1, rf.size() - 2);
+            int pi = 0;
+            for_each_token(rf, ';', [&](size_t b, size_t e) {
+                if (pi >= 3) return;
+                if (b < e) r.reg[pi] = atoi_at(rf, b);
+                ++pi;
+            });
+        }
+        r.col_off.resize(T + 1);
+        for (size_t t = 0; t < T; ++t) {
+            r.col_off[t] = (int32_t)r.tok.size();
+            const size_t idx = 8 + t;
+            if (!has(idx)) continue;
+            std::string s = parts[idx];  // parse_tok_field (utils.cpp:52-68)
+            if (s.size() >= 2 && s.front() == '"' && s.back() == '"') s = s.substr(1, s.size() - 2);
+            const size_t base = r.tok.size();
+            for_each_token(s, ';', [&](size_t b, size_t e) {
+                if (b == e) return;
+                const size_t p = s.find(':', b);
+                if (p == std::string::npos || p >= e) return;
+                const int tid = atoi_at(s, b), cnt = atoi_at(s, p + 1);
+                // token_cols[t][tid] = cnt: a repeated tid keeps its first position, takes the last count
+                for (size_t k = base; k < r.tok.size(); ++k)
+                    if (r.tok[k].first == tid) { r.tok[k].second = cnt; return; }
+                r.tok.emplace_back(tid, cnt);
+            });
+        }
+        r.col_off[T] = (int32_t)r.tok.size();
+        // out_profiles[p.user_id] = std::move(p): a repeated uid replaces the profile in place
+        auto ins = d.profiles.emplace(uid, (int32_t)d.rows.size());
+        if (ins.second) d.rows.push_back(std::move(r));
+        else d.rows[ins.first->second] = std::move(r);
+    }
+    d.info.lines_read = c;
+    return true;
+}
+
+// load_column_normalizers (utils.cpp:123-142)
+bool load_norms(const std::string& path, std::unordered_map<std::string, std::pair<float, float>>& out) {
+    std::ifstream in(path);
+    if (!in.is_open()) return false;
+    std::string line;
+    if (!std::getline(in, line)) return false;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        const size_t p1 = line.find(',');
+        if (p1 == std::string::npos) continue;
+        const size_t p2 = line.find(',', p1 + 1);
+        const std::string col = line.substr(0, p1);
+        if (p2 == std::string::npos) continue;
+        const float mean = (float)atof(line.substr(p1 + 1, p2 - (p1 + 1)).c_str());
+        const float sd = (float)atof(line.substr(p2 + 1).c_str());
+        out[col] = std::make_pair(mean, sd);
+    }
+    return !out.empty();
+}
+
+// VocabBuilder::load_vocab (vocab_builder.cpp:133-197): only the club map is used by the
+// path (api_cli.cpp:169-170); tokens.csv must exist and have a header for it to load.
+bool load_club_names(const std::string& dir, std::unordered_map<int, std::string>& names) {
+    {
+        std::ifstream tok(dir + "/tokens.csv");
+        std::string header;
+        if (!tok.is_open() || !std::getline(tok, header)) return false;
+    }
+    std::unordered_map<std::string, int> club_to_id;
+    std::ifstream in(dir + "/clubs_map.csv");
+    if (in.is_open()) {
+        std::string line;
+        if (std::getline(in, line)) {
+            while (std::getline(in, line)) {
+                if (line.empty()) continue;
+                std::vector<std::string> cols = split_csv_local(line);
+                if (cols.size() < 3) continue;
+                club_to_id[cols[1]] = atoi(cols[0].c_str());
+            }
+        }
+    }
+    for (auto& kv : club_to_id) names[kv.second] = kv.first;  // api_cli.cpp:169-170
+    return true;
+}
+
+void build_desc(pf_dataset& d) {
+    const int32_t n = (int32_t)d.rows.size(), T = (int32_t)d.cols.size();
+    d.uid.resize(n); d.pub.resize(n); d.comp.resize(n); d.gen.resize(n); d.age.resize(n);
+    d.reg.resize((size_t)3 * n);
+    d.club_off.assign(1, 0); d.friend_off.assign(1, 0); d.tok_off.assign(1, 0);
+    d.club_off.reserve(n + 1); d.friend_off.reserve(n + 1); d.tok_off.reserve((size_t)n * T + 1);
+    size_t nc = 0, nf = 0, nt = 0;
+    for (const Row& r : d.rows) { nc += r.clubs.size(); nf += r.friends.size(); nt += r.tok.size(); }
+    d.club_ids.reserve(nc); d.friend_ids.reserve(nf); d.tok_tid.reserve(nt); d.tok_tf.reserve(nt);
+    for (int32_t i = 0; i < n; ++i) {
+        const Row& r = d.rows[i];
+        d.uid[i] = r.uid; d.pub[i] = r.pub; d.comp[i] = r.comp; d.gen[i] = r.gen; d.age[i] = r.age;
+        for (int k = 0; k < 3; ++k) d.reg[(size_t)3 * i + k] = r.reg[k];
+        d.club_ids.insert(d.club_ids.end(), r.clubs.begin(), r.clubs.end());
+        d.club_off.push_back((int64_t)d.club_ids.size());
+        d.friend_ids.insert(d.friend_ids.end(), r.friends.begin(), r.friends.end());
+        d.friend_off.push_back((int64_t)d.friend_ids.size());
+        for (int32_t t = 0; t < T; ++t) {
+            for (int32_t k = r.col_off[t]; k < r.col_off[t + 1]; ++k) {
+                d.tok_tid.push_back(r.tok[k].first);
+                d.tok_tf.push_back(r.tok[k].second);
+            }
+            d.tok_off.push_back((int64_t)d.tok_tid.size());
+        }
+    }
+    d.adj_uid.clear(); d.adj_off.assign(1, 0); d.adj_nbr.clear();
+    for (auto& kv : d.adj_list) {
+        d.adj_uid.push_back(kv.first);
+        d.adj_nbr.insert(d.adj_nbr.end(), kv.second.begin(), kv.second.end());
+        d.adj_off.push_back((int64_t)d.adj_nbr.size());
+    }
+    // one map feeds both normaliser sets (api_cli.cpp:163-165)
+    const int K = kFixed + T;
+    d.npres.assign(K, 0); d.nmean.assign(K, 0.f); d.nsd.assign(K, 0.f);
+    for (int k = 0; k < K; ++k) {
+        auto it = d.norms.find(k < kFixed ? std::string(kFixedKeys[k]) : d.cols[k - kFixed]);
+        if (it == d.norms.end()) continue;
+        d.npres[k] = 1;
+        d.nmean[k] = it->second.first;
+        d.nsd[k] = it->second.second;
+    }
+    pf_corpus_desc& c = d.desc;
+    c = pf_corpus_desc{};
+    c.n_users = n;
+    c.n_cols = T;
+    c.user_id = d.uid.data(); c.public_flag = d.pub.data(); c.completion = d.comp.data();
+    c.gender = d.gen.data(); c.age = d.age.data(); c.region = d.reg.data();
+    c.club_off = d.club_off.data(); c.club_ids = d.club_ids.data();
+    c.friend_off = d.friend_off.data(); c.friend_ids = d.friend_ids.data();
+    c.tok_off = d.tok_off.data(); c.tok_tid = d.tok_tid.data(); c.tok_tf = d.tok_tf.data();
+    c.n_adj = (int32_t)d.adj_uid.size();
+    c.adj_uid = d.adj_uid.data(); c.adj_off = d.adj_off.data(); c.adj_nbr = d.adj_nbr.data();
+    c.idf_mode = PF_IDF_FROM_PROFILES;  // rec.compute_idf_from_profiles(textCols), api_cli.cpp:162
+    c.norm_present = d.npres.data(); c.norm_mean = d.nmean.data(); c.norm_sd = d.nsd.data();
+}
+
+void write_int_list(std::string& o, const std::vector<uint32_t>& v) {
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (i) o += ',';
+        o += std::to_string(v[i]);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out) {
+    if (!root || !out) return fail("null argument");
+    *out = nullptr;
+    auto d = new pf_dataset();
+    const std::string r(root), data = r + "/data";
+    auto bail = [&](const std::string& m) { delete d; return fail(m); };
+    if (!load_columns(r + "/config/text_columns.txt", d->cols)) return bail("cannot read config/text_columns.txt");
+    if (d->cols.size() > PF_MAX_COLS) return bail("more than PF_MAX_COLS text columns");
+    if (!load_adjacency(data + "/adjacency.csv", d->adj_list)) return bail("cannot read data/adjacency.csv");
+    if (!load_users(data + "/users_encoded.csv", max_lines, *d)) return bail("cannot load users_encoded.csv");
+    // median age (api_cli.cpp:139-153, user_loader.cpp:98-140)
+    int median = 0;
+    bool loaded = false;
+    {
+        std::ifstream in(data + "/median_age.txt");
+        std::string s;
+        if (in.is_open() && std::getline(in, s)) { median = atoi(s.c_str()); loaded = true; }
+    }
+    if (!loaded) {
+        std::vector<int> ages;
+        for (const Row& row : d->rows)
+            if (row.age > 0) ages.push_back(row.age);
+        if (!ages.empty()) {
+            std::sort(ages.begin(), ages.end());
+            const size_t n = ages.size();
+            median = n % 2 ? ages[n / 2] : (ages[n / 2 - 1] + ages[n / 2]) / 2;
+        }
+    }
+    int replaced = 0;
+    for (Row& row : d->rows)
+        if (row.age == 0) { row.age = median; ++replaced; }
+    load_norms(data + "/column_normalizers.csv", d->norms);
+    d->info.vocab_loaded = load_club_names(data, d->club_names) ? 1 : 0;
+    build_desc(*d);
+    d->info.n_profiles = (int32_t)d->rows.size();
+    d->info.n_cols = (int32_t)d->cols.size();
+    d->info.n_adj = (int32_t)d->adj_list.size();
+    d->info.median_age = median;
+    d->info.median_loaded = loaded ? 1 : 0;
+    d->info.ages_replaced = replaced;
+    d->info.n_normalizers = (int32_t)d->norms.size();
+    d->info.n_club_names = (int32_t)d->club_names.size();
+    *out = d;
+    return PF_OK;
+}
+
+void pf_dataset_free(pf_dataset* ds) { delete ds; }
+
+const pf_corpus_desc* pf_dataset_desc(const pf_dataset* ds) { return ds ? &ds->desc : nullptr; }
+
+int pf_dataset_info_get(const pf_dataset* ds, pf_dataset_info* out) {
+    if (!ds || !out) return PF_EINVAL;
+    *out = ds->info;
+    return PF_OK;
+}
+
+const char* pf_dataset_column(const pf_dataset* ds, int32_t t) {
+    if (!ds || t < 0 || t >= (int32_t)ds->cols.size()) return nullptr;
+    return ds->cols[t].c_str();
+}
+
+int pf_dataset_profile_order(const pf_dataset* ds, int32_t* out, int32_t cap, int32_t* n) {
+    if (!ds || !n || (cap > 0 && !out)) return PF_EINVAL;
+    int32_t i = 0;
+    for (auto& kv : ds->profiles) {
+        if (i < cap) out[i] = kv.first;
+        ++i;
+    }
+    *n = i;
+    return PF_OK;
+}
+
+int pf_dataset_adj_order(const pf_dataset* ds, int32_t* out, int32_t cap, int32_t* n) {
+    if (!ds || !n || (cap > 0 && !out)) return PF_EINVAL;
+    int32_t i = 0;
+    for (auto& kv : ds->adj_list) {
+        if (i < cap) out[i] = kv.first;
+        ++i;
+    }
+    *n = i;
+    return PF_OK;
+}
+
+// write_profile_json (api_cli.cpp:49-84)
+int pf_dataset_profile_json(const pf_dataset* ds, int32_t uid, char* buf, int64_t cap, int64_t* len) {
+    if (!ds || !len || (cap > 0 && !buf)) return PF_EINVAL;
+    auto it = ds->profiles.find(uid);
+    if (it == ds->profiles.end()) { *len = 0; return PF_ENOTFOUND; }
+    const Row& p = ds->rows[it->second];
+    std::string o;
+    o.reserve(1024);
+    o += "{\"user_id\":" + std::to_string(p.uid) + ",";
+    o += "\"public_flag\":" + std::to_string(p.pub) + ",";
+    o += "\"completion_percentage\":" + std::to_string(p.comp) + ",";
+    o += "\"gender\":" + std::to_string(p.gen) + ",";
+    o += "\"age\":" + std::to_string(p.age) + ",";
+    o += "\"region_parts\":[" + std::to_string(p.reg[0]) + "," + std::to_string(p.reg[1]) + "," +
+         std::to_string(p.reg[2]) + "],";
+    o += "\"clubs\":[";
+    write_int_list(o, p.clubs);
+    o += "],\"friends\":[";
+    write_int_list(o, p.friends);
+    o += "],\"token_cols\":[";
+    const size_t T = ds->cols.size();
+    for (size_t t = 0; t < T; ++t) {
+        if (t) o += ',';
+        o += '{';
+        // the reference iterates its unordered_map<int,int>: rebuild it with the same
+        // insertion sequence (first occurrences in field order) to get the same order
+        std::unordered_map<int, int> m;
+        for (int32_t k = p.col_off[t]; k < p.col_off[t + 1]; ++k) m[p.tok[k].first] = p.tok[k].second;
+        bool first = true;
+        for (auto& pr : m) {
+            if (!first) o += ',';
+            first = false;
+            o += "\"" + std::to_string(pr.first) + "\":" + std::to_string(pr.second);
+        }
+        o += '}';
+    }
+    o += "]}";
+    *len = (int64_t)o.size();
+    if (cap > 0) {
+        const size_t k = std::min<size_t>(o.size(), (size_t)cap - 1);
+        std::memcpy(buf, o.data(), k);
+        buf[k] = 0;
+    }
+    return PF_OK;
+}
+
+const char* pf_dataset_club_name(const pf_dataset* ds, int32_t club_id) {
+    if (!ds) return nullptr;
+    auto it = ds->club_names.find(club_id);
+    return it == ds->club_names.end() ? nullptr : it->second.c_str();
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- hold-out drivers (A19)
+#include <random>
+#include <unordered_set>
+
+namespace {
+
+struct Topk {
+    std::vector<int32_t> uid;
+    std::vector<float> score;
+    int32_t n = 0;
+    explicit Topk(int k) : uid(std::max(k, 1)), score(std::max(k, 1)) {}
+};
+
+}  // namespace
+
+extern "C" {
+
+// run_friends_holdout_test (test.cpp:13-105); adj_mod accumulates over users
+int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, double* out_ratios, int32_t cap,
+                       int32_t* n_out) {
+    if (!ctx || !ds || !n_out || (cap > 0 && !out_ratios)) return PF_EINVAL;
+    *n_out = 0;
+    std::vector<int> candidates;
+    for (auto& kv : ds->profiles) {
+        auto it = ds->adj_list.find(kv.first);
+        if (it == ds->adj_list.end()) continue;
+        if ((int)it->second.size() >= 20) candidates.push_back(kv.first);
+    }
+    if (candidates.empty()) return PF_OK;
+    std::mt19937 rng(1234567);
+    std::shuffle(candidates.begin(), candidates.end(), rng);
+    std::vector<int> touched;
+    std::vector<double> results;
+    int taken = 0, rc = PF_OK;
+    for (int uid : candidates) {
+        if (taken >= sample_size) break;
+        const std::vector<int>& friends = ds->adj_list.find(uid)->second;
+        const int F = (int)friends.size();
+        if (F < 2) continue;
+        const int hold_k = F / 5;
+        if (hold_k <= 0) continue;
+        std::vector<int> idx(F);
+        for (int i = 0; i < F; ++i) idx[i] = i;
+        std::shuffle(idx.begin(), idx.end(), rng);
+        std::unordered_set<int> held;
+        for (int i = 0; i < hold_k; ++i) held.insert(friends[idx[i]]);
+        std::vector<int32_t> newf;
+        newf.reserve(F - hold_k);
+        for (int f : friends)
+            if (held.find(f) == held.end()) newf.push_back(f);
+        rc = pf_set_adj(ctx, uid, newf.data(), (int32_t)newf.size());
+        if (rc != PF_OK) break;
+        touched.push_back(uid);
+        Topk t(hold_k);
+        const int32_t q = uid;
+        rc = pf_recommend_collab(ctx, &q, 1, hold_k, 1000, t.uid.data(), t.score.data(), &t.n);
+        if (rc != PF_OK) break;
+        int hits = 0;
+        for (int i = 0; i < t.n && i < hold_k; ++i)
+            if (held.find(t.uid[i]) != held.end()) ++hits;
+        results.push_back((double)hits / (double)hold_k);
+        ++taken;
+    }
+    for (int u : touched) {  // the reference mutated a copy (adj_mod); restore the base rows
+        const std::vector<int>& f = ds->adj_list.find(u)->second;
+        const int r2 = pf_set_adj(ctx, u, f.data(), (int32_t)f.size());
+        if (rc == PF_OK) rc = r2;
+    }
+    if (rc != PF_OK) return rc;
+    const int32_t n = (int32_t)results.size();
+    for (int32_t i = 0; i < n && i < cap; ++i) out_ratios[i] = results[i];
+    *n_out = n;
+    return PF_OK;
+}
+
+// run_recommendation_tests_sample (recommendation_tests.cpp:68-169); a fresh adj_mod per user
+int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5) {
+    if (!ctx || !ds || !out5) return PF_EINVAL;
+    for (int i = 0; i < 5; ++i) out5[i] = 0.0;
+    if (ds->profiles.empty() || ds->adj_list.empty()) return PF_OK;
+    std::vector<int> all;
+    for (auto& kv : ds->profiles) all.push_back(kv.first);
+    std::mt19937 rng(1234567);
+    std::shuffle(all.begin(), all.end(), rng);
+    int taken = 0, hits_graph = 0, hits_collab = 0, hits_interest = 0, club_users = 0;
+    double club_prec = 0.0, club_rec = 0.0;
+    const int K = std::max(topk, 1);
+    for (int uid : all) {
+        if (taken >= sample_size) break;
+        auto itadj = ds->adj_list.find(uid);
+        if (itadj == ds->adj_list.end()) continue;
+        const std::vector<int>& friends = itadj->second;
+        if (friends.size() < 4) continue;
+        const int hold_k = std::max(1, (int)friends.size() / 4);
+        std::vector<int> idx(friends.size());
+        for (size_t i = 0; i < friends.size(); ++i) idx[i] = (int)i;
+        std::shuffle(idx.begin(), idx.end(), rng);
+        std::unordered_set<int> held;
+        for (int i = 0; i < hold_k; ++i) held.insert(friends[idx[i]]);
+        std::vector<int32_t> newf;
+        for (int f : friends)
+            if (held.find(f) == held.end()) newf.push_back(f);
+        int rc = pf_set_adj(ctx, uid, newf.data(), (int32_t)newf.size());
+        if (rc != PF_OK) return rc;
+        const int32_t q = uid;
+        Topk g(K), c(K), in(K), cl(K);
+        rc = pf_recommend_interest(ctx, &q, 1, topk, PF_MODE_FOF, 5000, g.uid.data(), g.score.data(), &g.n);
+        if (rc == PF_OK) rc = pf_recommend_collab(ctx, &q, 1, topk, 5000, c.uid.data(), c.score.data(), &c.n);
+        // recommend_by_interest is recommend_graph_registration (recommender_graph.cpp:224-227)
+        in = g;
+        if (rc == PF_OK) rc = pf_recommend_clubs(ctx, &q, 1, topk, 5000, cl.uid.data(), cl.score.data(), &cl.n);
+        const int r2 = pf_set_adj(ctx, uid, friends.data(), (int32_t)friends.size());
+        if (rc != PF_OK) return rc;
+        if (r2 != PF_OK) return r2;
+        auto any_held = [&](const Topk& t) {
+            for (int i = 0; i < t.n; ++i)
+                if (held.find(t.uid[i]) != held.end()) return true;
+            return false;
+        };
+        hits_graph += any_held(g);
+        hits_collab += any_held(c);
+        hits_interest += any_held(in);
+        const auto& row = ds->rows[ds->profiles.find(uid)->second];
+        std::unordered_set<int> actual;
+        for (uint32_t x : row.clubs) actual.insert((int)x);
+        if (!actual.empty()) {
+            int hit = 0;
+            for (int i = 0; i < cl.n && i < topk; ++i)
+                if (actual.find(cl.uid[i]) != actual.end()) ++hit;
+            club_prec += (double)hit / (double)topk;
+            club_rec += (double)hit / (double)actual.size();
+            ++club_users;
+        }
+        ++taken;
+    }
+    if (taken > 0) {
+        out5[0] = (double)hits_graph / (double)taken;
+        out5[1] = (double)hits_collab / (double)taken;
+        out5[2] = (double)hits_interest / (double)taken;
+    }
+    if (club_users > 0) {
+        out5[3] = club_prec / (double)club_users;
+        out5[4] = club_rec / (double)club_users;
+    }
+    return PF_OK;
+}
+
+}  // extern "C"

@@ -26,11 +26,23 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
            "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read"]
+# include/pokec_io.h: loaders and hold-out drivers
+IO_EXPORTS = ["pf_dataset_load", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
+              "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
+              "pf_holdout_friends", "pf_recommendation_tests"]
+PF_LOAD_REFERENCE_CAP = 100000
 
 
 class PfLayoutStats(ctypes.Structure):
     _fields_ = [("n_slots", ctypes.c_int64), ("stream_bytes", ctypes.c_int64), ("header_bytes", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32)]
+
+
+class PfDatasetInfo(ctypes.Structure):
+    _fields_ = [("lines_read", ctypes.c_int64), ("n_profiles", ctypes.c_int32), ("n_cols", ctypes.c_int32),
+                ("n_adj", ctypes.c_int32), ("median_age", ctypes.c_int32), ("median_loaded", ctypes.c_int32),
+                ("ages_replaced", ctypes.c_int32), ("n_normalizers", ctypes.c_int32),
+                ("vocab_loaded", ctypes.c_int32), ("n_club_names", ctypes.c_int32)]
 
 
 class FasError(RuntimeError):
@@ -73,6 +85,21 @@ def lib():
         L.pf_last_scan_ms.restype = ctypes.c_float
         L.pf_profile_reset.argtypes = [V]
         L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
+        L.pf_dataset_load.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(V)]
+        L.pf_dataset_free.argtypes = [V]
+        L.pf_dataset_free.restype = None
+        L.pf_dataset_desc.argtypes = [V]
+        L.pf_dataset_desc.restype = V
+        L.pf_dataset_info_get.argtypes = [V, ctypes.POINTER(PfDatasetInfo)]
+        L.pf_dataset_column.argtypes = [V, I32]
+        L.pf_dataset_column.restype = ctypes.c_char_p
+        L.pf_dataset_profile_order.argtypes = [V, V, I32, ctypes.POINTER(I32)]
+        L.pf_dataset_adj_order.argtypes = [V, V, I32, ctypes.POINTER(I32)]
+        L.pf_dataset_profile_json.argtypes = [V, I32, V, I64, ctypes.POINTER(I64)]
+        L.pf_dataset_club_name.argtypes = [V, I32]
+        L.pf_dataset_club_name.restype = ctypes.c_char_p
+        L.pf_holdout_friends.argtypes = [V, V, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_recommendation_tests.argtypes = [V, V, I32, I32, V]
         _lib = L
     return _lib
 
@@ -211,3 +238,85 @@ def decode_keys(keys):
     n = ctypes.c_int32()
     lib().pf_decode_keys(keys.ctypes.data, len(keys), ou.ctypes.data, os_.ctypes.data, ctypes.byref(n))
     return ou[:n.value], os_[:n.value]
+
+
+class Dataset:
+    """The reference's start-up loaders over a data directory (pf_dataset_load): the
+    corpus the engine opens on, plus the reference's own iteration orders.  Host only."""
+
+    def __init__(self, root, max_lines=PF_LOAD_REFERENCE_CAP):
+        L = lib()
+        self._L = L
+        self.h = ctypes.c_void_p()
+        rc = L.pf_dataset_load(os.fsencode(root), max_lines, ctypes.byref(self.h))
+        if rc != PF_OK:
+            raise FasError(f"pf_dataset_load failed ({rc}): {L.pf_last_error(None).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.pf_dataset_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def desc_ptr(self):
+        return self._L.pf_dataset_desc(self.h)
+
+    def info(self):
+        s = PfDatasetInfo()
+        self._L.pf_dataset_info_get(self.h, ctypes.byref(s))
+        return s
+
+    def columns(self):
+        out, t = [], 0
+        while True:
+            c = self._L.pf_dataset_column(self.h, t)
+            if c is None:
+                return out
+            out.append(c.decode())
+            t += 1
+
+    def _order(self, fn):
+        n = ctypes.c_int32()
+        fn(self.h, None, 0, ctypes.byref(n))
+        out = np.empty(n.value, np.int32)
+        fn(self.h, out.ctypes.data, n.value, ctypes.byref(n))
+        return out
+
+    def profile_order(self):
+        return self._order(self._L.pf_dataset_profile_order)
+
+    def adj_order(self):
+        return self._order(self._L.pf_dataset_adj_order)
+
+    def profile_json(self, uid):
+        n = ctypes.c_int64()
+        rc = self._L.pf_dataset_profile_json(self.h, uid, None, 0, ctypes.byref(n))
+        if rc == PF_ENOTFOUND:
+            return None
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._L.pf_dataset_profile_json(self.h, uid, buf, n.value + 1, ctypes.byref(n))
+        return buf.value.decode()
+
+    def club_name(self, cid):
+        c = self._L.pf_dataset_club_name(self.h, cid)
+        return None if c is None else c.decode()
+
+    # -- hold-out drivers (A19); `eng` must be open on this dataset's desc
+    def holdout_friends(self, eng, sample_size):
+        cap = max(sample_size, 1)
+        out = np.empty(cap, np.float64)
+        n = ctypes.c_int32()
+        rc = self._L.pf_holdout_friends(eng.h, self.h, sample_size, out.ctypes.data, cap, ctypes.byref(n))
+        eng._check(rc, "pf_holdout_friends")
+        return out[:n.value]
+
+    def recommendation_tests(self, eng, sample_size, topk):
+        out = np.zeros(5, np.float64)
+        rc = self._L.pf_recommendation_tests(eng.h, self.h, sample_size, topk, out.ctypes.data)
+        eng._check(rc, "pf_recommendation_tests")
+        return out

@@ -10,8 +10,8 @@ import pytest
 import pokec_testlib as tl
 
 
-def header_functions():
-    with open(os.path.join(tl.ROOT, "include", "pokec_fas.h")) as f:
+def header_functions(name="pokec_fas.h"):
+    with open(os.path.join(tl.ROOT, "include", name)) as f:
         src = f.read()
     return sorted(set(re.findall(r"\b(pf_[a-z_]+)\s*\(", src)))
 
@@ -24,6 +24,10 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert sorted(pf.EXPORTS) == names
+    io = [n for n in header_functions("pokec_io.h") if n not in names]  # minus pokec_fas.h names it cites
+    for n in io:
+        assert hasattr(L, n), n
+    assert sorted(pf.IO_EXPORTS) == io
     assert L.pf_abi_version() == 1
 
 

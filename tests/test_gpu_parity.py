@@ -141,3 +141,48 @@ def test_kernel_variants(env):
     r = subprocess.run([sys.executable, os.path.join(here, "gpu_variant_check.py")], env={**os.environ, **env},
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_api_cli_transcript_matches_reference():
+    """The product CLI (C++ loaders + engine) answers the reference api_cli's recorded
+    stdin with byte-identical stdout (loader progress, READY, JSON lines)."""
+    import gzip
+    import os
+    import subprocess
+    import tempfile
+    exe = os.path.join(tl.ROOT, "recommendation-system-pokec_amd", "pokec_api_cli")
+    assert os.path.exists(exe), "build with make -C recommendation-system-pokec_amd"
+    m = tl.manifest()["api_cli"]
+    with gzip.open(os.path.join(tl.GOLDEN, "api", "transcript_stdin.txt.gz"), "rb") as f:
+        stdin = f.read()
+    with gzip.open(os.path.join(tl.GOLDEN, "api", "transcript_stdout.txt.gz"), "rb") as f:
+        ref = f.read()
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("api", d)
+        r = subprocess.run([exe, m["load_users"]], cwd=d, input=stdin, capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr.decode()
+    got = r.stdout.decode().splitlines()
+    want = ref.decode().splitlines()
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"line {i}: {g[:200]} != {w[:200]}"
+
+
+def test_holdout_drivers_match_reference():
+    """run_friends_holdout_test / run_recommendation_tests_sample (A19) on the engine,
+    driven by the C++ loaders, against the reference's outputs on corpus A."""
+    import tempfile
+    pf = tl.product()
+    m = tl.manifest()["corpora"]["A"]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        ds = pf.Dataset(d)
+    eng = pf.FasEngine(ds.desc_ptr(), 0)
+    ref = tl.fixture_lines("A", "holdout_friends.txt")  # written with fixed << setprecision(6), test.cpp:95
+    got = [f"{v:.6f}" for v in ds.holdout_friends(eng, m["holdout"])]
+    assert got == ref
+    ref5 = [float(x) for x in tl.fixture_lines("A", "rectests.txt")[0].split()]
+    got5 = ds.recommendation_tests(eng, m["rectest"], 10)
+    assert list(got5) == ref5
+    # the drivers restore the engine's adjacency: a second run gives the same answers
+    assert [f"{v:.6f}" for v in ds.holdout_friends(eng, m["holdout"])] == ref

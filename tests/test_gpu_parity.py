@@ -186,3 +186,45 @@ def test_holdout_drivers_match_reference():
     assert list(got5) == ref5
     # the drivers restore the engine's adjacency: a second run gives the same answers
     assert [f"{v:.6f}" for v in ds.holdout_friends(eng, m["holdout"])] == ref
+
+
+def test_cpp_facade_matches_reference():
+    """include/pokec/recommender.h (the C++ Recommender drop-in), wired like
+    api_cli.cpp:155-163, answers the golden recommender queries, FAS pairs and an
+    all-candidates query bit-exactly; sync_adjacency applies an adj_list edit."""
+    import os
+    import subprocess
+    import tempfile
+    exe = os.path.join(tl.ROOT, "tests", "cpp", "facade_check")
+    assert os.path.exists(exe), "build with make -C recommendation-system-pokec_amd"
+    g = tl.golden_lists("A", "recs.txt")
+    keys = list(g.keys())[::3]
+    a, b, s = tl.golden_pairs("A")
+    allg = tl.golden_lists("A", "all.txt")
+    akey = list(allg.keys())[0]
+    q = [f"{t} {u} {k} {lim}" for t, u, k, lim in keys]
+    q += [f"pair {x} {y}" for x, y in zip(a[:500], b[:500])]
+    q += [f"all {akey[1]} 50 0", "sync 1 2 3 4", "collab 1 10 5000"]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        r = subprocess.run([exe, d], input="\n".join(q) + "\n", capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.splitlines()
+    assert len(out) == len(q)
+    for key, ln in zip(keys, out[:len(keys)]):
+        p = ln.split()
+        items = [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:]]
+        assert int(p[4]) == len(g[key]) and items == g[key], key
+    for i, ln in enumerate(out[len(keys):len(keys) + 500]):
+        assert int(ln.split()[3], 16) == int(s[i]), ln
+    p = out[len(keys) + 500].split()
+    assert [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:]] == allg[akey]
+    assert out[-2] == "sync 1 0"
+    # after the edit, collab for uid 1 equals the engine's with the same adj row
+    corpus = tl.golden_corpus("A")
+    eng = tl.engine(corpus)
+    eng.set_adj(1, [2, 3, 4])
+    (ids, sc), = eng.recommend_collaborative([1], 10, 5000)
+    p = out[-1].split()
+    assert [int(x.split(":")[0]) for x in p[5:]] == list(ids)
+    assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))

@@ -70,7 +70,7 @@ struct pf_ctx {
     pf::HostCorpus hc;
     pf::HostStore hs;       // metadata only after upload (stream freed)
     int64_t stream_bytes = 0, norm_bytes = 0;
-    DBuf d_stream, d_tile_off, d_tile_steps, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
+    DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
     pf::DevStore ds{};
     // workspaces
     DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part;
@@ -175,7 +175,9 @@ void add_image(Images& im, const pf::QImageHost& q) {
     const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
     r.lds_bytes = kv <= stage_limit() ? (uint32_t)kv : 0u;
     im.gtab = im.gtab || r.lds_bytes == 0;
-    const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads + 2048u;
+    // QConst | staged tables | hit lists | hit counts | merge scratch (stage_query's carve)
+    const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads +
+                          4u * kBlockThreads + 2048u;
     im.max_lds = std::max(im.max_lds, need);
     im.refs.push_back(r);
 }
@@ -286,9 +288,10 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     }
     const int nq = (int)idx.size();
     const int tiles = c->tile_end - c->tile_begin;
-    // oversubscribed grid (~8 blocks per CU over the batch): blocks that draw short tiles
-    // finish early and new ones fill in, which balances better than one resident round
-    const int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(8, c->num_cus * 8 / nq)));
+    // one resident round of blocks over the batch: tiles come from a per-query queue, so
+    // the waves that exist balance the work themselves
+    const int per_cu = pf::scan_blocks_per_cu(c->hs.packed, im.gtab, im.max_lds);
+    const int blocks = std::max(1, std::min((tiles + 3) / 4, std::max(1, c->num_cus * per_cu / nq)));
     const size_t refs_b = (size_t)nq * sizeof(pf::QImageRef);
     const size_t rows_b = ((size_t)nq * sizeof(int32_t) + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);  // zeros: the per-launch rendezvous
@@ -377,6 +380,9 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     if (e == hipSuccess) e = upload(c, c->d_stream, hs.stream);
     if (e == hipSuccess) e = upload(c, c->d_tile_off, hs.tile_off);
     if (e == hipSuccess) e = upload(c, c->d_tile_steps, hs.tile_steps);
+    if (e == hipSuccess) e = upload(c, c->d_tile_slot0, hs.tile_slot0);
+    if (e == hipSuccess) e = upload(c, c->d_tile_lgk, hs.tile_lgk);
+    if (e == hipSuccess) e = upload(c, c->d_slot_tile, hs.slot_tile);
     if (e == hipSuccess) e = upload(c, c->d_norms, hs.norms);
     if (e == hipSuccess) e = upload(c, c->d_norm_off, hs.norm_off);
     if (e == hipSuccess) e = upload(c, c->d_hdr0, hs.hdr0);
@@ -394,6 +400,9 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     c->ds.stream = c->d_stream.as<uint4>();
     c->ds.tile_off = c->d_tile_off.as<uint64_t>();
     c->ds.tile_steps = c->d_tile_steps.as<uint32_t>();
+    c->ds.tile_slot0 = c->d_tile_slot0.as<uint32_t>();
+    c->ds.tile_lgk = c->d_tile_lgk.as<uint8_t>();
+    c->ds.slot_tile = c->d_slot_tile.as<uint32_t>();
     c->ds.norms = c->d_norms.as<double>();
     c->ds.norm_off = c->d_norm_off.as<uint64_t>();
     c->ds.hdr0 = c->d_hdr0.as<uint4>();

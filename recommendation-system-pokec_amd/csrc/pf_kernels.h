@@ -18,6 +18,8 @@ struct PairBlock {
 hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t lds, bool gtab,
                        int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* parts, ScanSync* sync,
                        uint64_t* out, const int32_t* out_rows, hipStream_t s);
+// resident scan blocks per CU at this dynamic LDS size (HIP occupancy API)
+int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds);
 // plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
                         uint64_t* out, hipStream_t s);

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "pf_kernels.h"
 
@@ -69,16 +70,17 @@ __device__ __forceinline__ double ratio_term(const QConst& q, int slot, int a, i
 // ---------------------------------------------------------------- query hash (cuckoo)
 struct QView {
     const QConst* q;
-    const uint2* tab;  // T0 clubs | T1 friends | T2 tokens (2^lg each) | T3 excl (2^lg_excl)
+    const uint2* tab;  // packed: T | T3;  wide: T0 | T1 | T2 (2^lg each) | T3 (2^lg_excl)
     const QVal* vals;
-    void* hits;        // LDS [kHitCap][blockDim.x] per-lane token-hit list
+    void* hits;        // LDS [kHitCap + 1][blockDim.x] per-lane token-hit list
+    uint32_t* nh;      // LDS [blockDim.x] hit counts, read across the lanes of a split record
     int lg, lge;
-    uint32_t seed;
+    uint32_t hmul, excl_off;
 };
 
-// 2-choice probe of table `off` (entries) with capacity 2^lg; returns the entry's val or kEmptyVal
+// Wide tables: 2-choice probe of table `off` (entries), capacity 2^lg; val or kEmptyVal
 __device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, uint32_t key) {
-    const uint32_t x = cuckoo_x(key, v.seed);
+    const uint32_t x = cuckoo_x(key, v.hmul);
     const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
     const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
     // a key sits in at most one of its two slots: AND-combining keeps both reads
@@ -88,8 +90,18 @@ __device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, 
     return r1 & r2;
 }
 
+// Packed tables: the same probe with miss = 0 (empty slots are {~0, 0})
+__device__ __forceinline__ uint32_t probe_p(const QView& v, uint32_t off, int lg, uint32_t key) {
+    const uint32_t x = cuckoo_x(key, v.hmul);
+    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
+    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
+    return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
+}
+
+template <bool PACKED>
 __device__ __forceinline__ bool excluded(const QView& v, uint32_t uid) {
-    return probe(v, 3u << v.lg, v.lge, uid) != kEmptyVal;
+    if (PACKED) return probe_p(v, v.excl_off, v.lge, uid) != 0u;
+    return probe(v, v.excl_off, v.lge, uid) != kEmptyVal;
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
@@ -127,37 +139,67 @@ struct HitT<false> {
     __device__ static int32_t tf(type e) { return (int32_t)e.y >> 8; }
 };
 
-template <bool PACKED>
-__device__ __forceinline__ void walk_word(Walk& W, uint32_t w, uint32_t j, uint32_t nc, uint32_t nset, uint32_t len,
-                                          const QView& v, uint32_t hstride) {
-    using H = HitT<PACKED>;
-    const bool ok = j < len;
-    const bool tok = j >= nset;
-    const bool fr = j >= nc;
-    const uint32_t cap = 1u << v.lg;
-    typename H::type* hits = reinterpret_cast<typename H::type*>(v.hits);
-    if (PACKED) {
-        // sets: T0/T1 keyed by the id; tokens: T2 keyed by the word's low 24 bits (col:tid)
-        const uint32_t key = tok ? (w & 0xFFFFFFu) : w;
-        const uint32_t val = probe(v, tok ? 2u * cap : (fr ? cap : 0u), v.lg, key);
-        const bool hit = ok && val != kEmptyVal;
-        W.cnt += (hit && !tok) ? (fr ? 0x10000u : 1u) : 0u;
-        if (tok && hit) {  // rare
-            if (W.nh < kHitCap) reinterpret_cast<uint32_t*>(hits)[W.nh * hstride + threadIdx.x] = val | (w & 0xFF000000u);
-            W.nh += 1;
-        }
-    } else {
-        // wide tokens: (tid, tf << 8 | col) word pairs, probed at the second word
-        const bool second = tok && ((j - nset) & 1u);
-        const uint32_t key = second ? W.pend : w;
-        if (tok && !second) W.pend = w;
-        const uint32_t val = probe(v, tok ? 2u * cap : (fr ? cap : 0u), v.lg, key);
-        const bool hit = ok && (!tok || second) && val != kEmptyVal && (!tok || (val & 0xFFu) == (w & 0xFFu));
-        W.cnt += (hit && !tok) ? (fr ? 0x10000u : 1u) : 0u;
-        if (tok && hit) {
-            if (W.nh < kHitCap) reinterpret_cast<uint2*>(hits)[W.nh * hstride + threadIdx.x] = make_uint2(val, w);
-            W.nh += 1;
-        }
+// One 16-B step (4 record words) of a lane, branch-free.  All four probes are issued
+// before any result is used, so the step's 8 LDS reads are in flight together; then the
+// words update the counters in order.  Every word costs one (possibly dead) hit-list
+// store: a non-hit writes the lane's next free slot, which the next real hit
+// overwrites; hits past kHitCap go to a dump slot (the list then reads as overflowed
+// and the epilogue re-walks the record).
+//
+// Packed corpora: one tagged table, so a word's probe key is the word itself (sets) or
+// kTagTok | its low 24 bits (tokens), and the probe's value is directly the club / friend
+// counter increment or the token's value entry.  sj = the step's first word index in the
+// chunk (wave-uniform), tb = nset - j0 = where the chunk's tokens start, lim = chunk
+// length (MASKED only: lanes of different tiles, whose padding is not guaranteed).
+template <bool MASKED>
+__device__ __forceinline__ void walk_step_p(Walk& W, const uint4& cw, int sj, int tb, int lim, const QView& v,
+                                            uint32_t hstride) {
+    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t val[4];
+    bool tok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        tok[i] = sj + i >= tb;
+        uint32_t key = tok[i] ? (kTagTok | (w[i] & 0xFFFFFFu)) : w[i];
+        if (MASKED) key = sj + i < lim ? key : kPadWord;
+        val[i] = probe_p(v, 0u, v.lg, key);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        W.cnt += tok[i] ? 0u : val[i];
+        const uint32_t slot = (W.nh < kHitCap ? W.nh : kHitCap) * hstride + threadIdx.x;
+        reinterpret_cast<uint32_t*>(v.hits)[slot] = (w[i] & 0xFF000000u) | (val[i] & 0xFFFFFFu);
+        W.nh += (tok[i] && val[i] != 0u) ? 1u : 0u;
+    }
+}
+
+// Wide corpora: three tables, token (tid, tf:col) word pairs probed at the second word.
+__device__ __forceinline__ void walk_step_w(Walk& W, const uint4& cw, uint32_t j0, uint32_t nc, uint32_t nset,
+                                            uint32_t len, const QView& v, uint32_t hstride) {
+    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t val[4];
+    bool tok[4], fr[4], second[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t j = j0 + i;
+        tok[i] = j >= nset;
+        fr[i] = j >= nc;
+        const uint32_t off = ((uint32_t)fr[i] + (uint32_t)tok[i]) << v.lg;  // T0 clubs, T1 friends, T2 tokens
+        second[i] = tok[i] && ((j - nset) & 1u);
+        const uint32_t key = second[i] ? (i ? w[i - 1] : W.pend) : w[i];
+        val[i] = probe(v, off, v.lg, key);
+    }
+    W.pend = w[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t j = j0 + i;
+        const bool ok = j < len;
+        const bool hit = ok && (!tok[i] || second[i]) && val[i] != kEmptyVal &&
+                         (!tok[i] || (val[i] & 0xFFu) == (w[i] & 0xFFu));
+        W.cnt += (hit && !tok[i]) ? (fr[i] ? 0x10000u : 1u) : 0u;
+        const uint32_t slot = (W.nh < kHitCap ? W.nh : kHitCap) * hstride + threadIdx.x;
+        reinterpret_cast<uint2*>(v.hits)[slot] = make_uint2(val[i], w[i]);
+        W.nh += (hit && tok[i]) ? 1u : 0u;
     }
 }
 
@@ -167,38 +209,65 @@ __device__ __forceinline__ double hit_product(const QView& v, uint32_t vi, int32
     return qv.wq * ((double)tf * qv.idf);
 }
 
-__device__ __forceinline__ double col_norm(const DevStore& st, int p, uint64_t cmask, int t) {
-    const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
-    return st.norms[st.norm_off[p >> 6] + (uint64_t)r * kTileSlots + (p & 63)];
+// Where a candidate lives: tile, index in the tile, lanes per record (1 << lgk)
+struct Loc {
+    int tile;
+    int cand;
+    uint32_t lgk;
+};
+
+__device__ __forceinline__ Loc loc_of(const DevStore& st, int p) {
+    Loc l;
+    l.tile = (int)st.slot_tile[p];
+    l.cand = p - (int)st.tile_slot0[l.tile];
+    l.lgk = st.tile_lgk[l.tile];
+    return l;
 }
 
-// Text terms of a lane whose hit list overflowed: re-walk its token words from global
-// memory, accumulating each column's dot in stream order (rare path).
+__device__ __forceinline__ double col_norm(const DevStore& st, const Loc& l, uint64_t cmask, int t) {
+    const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
+    return st.norms[st.norm_off[l.tile] + (uint64_t)r * kTileSlots + l.cand];
+}
+
+// word j of a candidate's record (chunk j / q in lane cand * k + j / q)
+__device__ __forceinline__ uint32_t word_at(const DevStore& st, const Loc& l, uint32_t q, uint32_t j) {
+    const uint32_t c = j / q, o = j - c * q;
+    const uint32_t lane = ((uint32_t)l.cand << l.lgk) + c;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(st.stream + st.tile_off[l.tile]);
+    return base[((size_t)(o >> 2) * kTileSlots + lane) * 4 + (o & 3)];
+}
+
+__device__ __forceinline__ uint32_t record_words(const uint4& h2, bool packed) {
+    return h2.y + h2.z + (packed ? h2.w : 2 * h2.w);
+}
+
+// Text terms of a candidate whose hit list overflowed: re-walk its token words from
+// global memory, accumulating each column's dot in stream order (rare path).
 template <bool PACKED>
-__device__ __forceinline__ double text_terms_slow(const DevStore& st, const QView& v, int p, uint32_t nset,
+__device__ __forceinline__ double text_terms_slow(const DevStore& st, const QView& v, const Loc& l, uint32_t nset,
                                                   uint32_t len, uint64_t cmask, double sum) {
     const QConst& q = *v.q;
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(st.stream + st.tile_off[p >> 6] + (p & 63));
-    auto word = [&](uint32_t j) { return base[(size_t)(j >> 2) * (kTileSlots * 4) + (j & 3)]; };
+    const uint32_t qw = chunk_words(len, l.lgk, PACKED);
     const uint32_t cap = 1u << v.lg;
     int cur = -1;
     double dot = 0.0;
     auto close = [&]() {
         if (cur >= 0 && ((q.colmask >> cur) & 1ull))
-            sum += dot == 0.0 ? q.sig0_col[cur] : text_term(q, cur, dot, col_norm(st, p, cmask, cur));
+            sum += dot == 0.0 ? q.sig0_col[cur] : text_term(q, cur, dot, col_norm(st, l, cmask, cur));
     };
     for (uint32_t j = nset; j < len; j += PACKED ? 1 : 2) {
         uint32_t key, col, val;
         int32_t tf;
         if (PACKED) {
-            const uint32_t w = word(j);
-            key = w & 0xFFFFFFu;
+            const uint32_t w = word_at(st, l, qw, j);
+            key = kTagTok | (w & 0xFFFFFFu);
             col = (w >> kTidBits) & 63u;
             tf = (int32_t)(w >> 24);
-            val = probe(v, 2u * cap, v.lg, key);
+            val = probe_p(v, 0u, v.lg, key);
+            if (val == 0u) val = kEmptyVal;
         } else {
-            const uint32_t w = word(j + 1);
-            key = word(j);
+            const uint32_t w = word_at(st, l, qw, j + 1);
+            key = word_at(st, l, qw, j);
             col = w & 0xFFu;
             tf = (int32_t)w >> 8;
             val = probe(v, 2u * cap, v.lg, key);
@@ -215,53 +284,51 @@ __device__ __forceinline__ double text_terms_slow(const DevStore& st, const QVie
     return sum;
 }
 
-// FAS(A = staged query, B = candidate slot p).  Every lane of the wave calls it.
-template <bool PACKED>
-__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
-    using H = HitT<PACKED>;
-    const QConst& q = *v.q;
-    const uint32_t hstride = blockDim.x;
-    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-    if (active) {
-        h0 = st.hdr0[p];
-        h1 = st.hdr1[p];
-        h2 = st.hdr2[p];
-    }
-    const uint32_t nc = h2.y, nf = h2.z, nt = h2.w;
-    const uint32_t nset = nc + nf;
-    const uint32_t len = PACKED ? nset + nt : nset + 2 * nt;
-    const uint32_t steps = active ? (len + 3) >> 2 : 0;
-    const uint4* base = st.stream + (active ? st.tile_off[p >> 6] + (p & 63) : 0);
-
-    Walk W;
-    W.cnt = 0; W.nh = 0; W.pend = 0;
+// Walk record words [j0, j0 + clen) of the lane's chunk; base = the lane's stream column
+// (step s at base[s * kTileSlots]).  Every lane of the wave calls it (clen = 0 when idle).
+// Double buffer of 4-step groups: the next group's 4 loads are issued before the current
+// group is walked, so every wait is covered by a whole group of work.  (Loads kept in
+// flight across the loop back-edge make the waitcnt pass drain them at the loop head.)
+// MASKED = false (scan): every lane of the wave is in one tile, whose steps come in whole
+// groups with padding words past each chunk, and the stream ends with a group of
+// padding, so loads need no clamp and words no mask.  MASKED = true (pairs): lanes of
+// different tiles; loads are clamped to the lane's last step and words past the chunk
+// are masked.
+template <bool PACKED, bool MASKED>
+__device__ __forceinline__ void walk_chunk(Walk& W, const uint4* base, uint32_t j0, uint32_t clen, uint32_t nc,
+                                           uint32_t nset, const QView& v, uint32_t hstride) {
+    const uint32_t steps = (clen + 3) >> 2;
     const uint32_t smax = wave_max_u32(steps);
-    // Loads past a lane's record re-read its last step (always a valid address); those
-    // words are masked by j < len.
     const uint32_t last = steps ? steps - 1 : 0;
-    auto ld = [&](uint32_t s) { return base[(size_t)(s < last ? s : last) * kTileSlots]; };
-    // Double buffer of 4 steps: the next group's 4 loads are issued before the current
-    // group is walked, so every wait is covered by a whole group of work.  (Loads kept in
-    // flight across the loop back-edge make the waitcnt pass drain them at the loop head.)
-    auto step = [&](const uint4& cur, uint32_t s) {
-        const uint32_t j = s * 4;
-        walk_word<PACKED>(W, cur.x, j + 0, nc, nset, len, v, hstride);
-        walk_word<PACKED>(W, cur.y, j + 1, nc, nset, len, v, hstride);
-        walk_word<PACKED>(W, cur.z, j + 2, nc, nset, len, v, hstride);
-        walk_word<PACKED>(W, cur.w, j + 3, nc, nset, len, v, hstride);
+    auto ld = [&](uint32_t s) { return base[(size_t)(MASKED ? (s < last ? s : last) : s) * kTileSlots]; };
+    const int tb = (int)nset - (int)j0, lim = (int)clen;
+    const uint32_t len = j0 + clen;
+    auto walk = [&](const uint4& c, uint32_t s) {
+        if (PACKED) walk_step_p<MASKED>(W, c, (int)s * 4, tb, lim, v, hstride);
+        else walk_step_w(W, c, j0 + s * 4, nc, nset, len, v, hstride);
     };
     uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
     for (uint32_t s = 0; s < smax; s += 4) {
         const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
-        step(c0, s);
-        step(c1, s + 1);
-        step(c2, s + 2);
-        step(c3, s + 3);
+        walk(c0, s);
+        walk(c1, s + 1);
+        walk(c2, s + 2);
+        walk(c3, s + 3);
         c0 = n0; c1 = n1; c2 = n2; c3 = n3;
     }
-    if (!active) return 0.0f;
+}
 
-    // ---- epilogue: the reference's terms in the reference's order -------------
+// FAS(A = staged query, B = slot p) from the walk's results: the reference's terms in the
+// reference's order.  The candidate's token hits are the hit lists of threads
+// first .. first + nl - 1 (its chunks, in record order); nh_of(g) = hits of thread first + g.
+template <bool PACKED, class NH>
+__device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v, const Loc& l, const uint4& h0,
+                                              const uint4& h1, const uint4& h2, uint32_t cnt, uint32_t first,
+                                              uint32_t nl, NH nh_of) {
+    using H = HitT<PACKED>;
+    const QConst& q = *v.q;
+    const uint32_t hstride = blockDim.x;
+    const uint32_t nc = h2.y, nf = h2.z;
     double sum = 0.0;
     int used = 0;
     const uint32_t pb = h2.x & 0xFFu, gb = (h2.x >> 8) & 0xFFu;
@@ -277,7 +344,7 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
         sum += q.sig_reg[bcnt][m];
         ++used;
     }
-    const int ic = (int)(W.cnt & 0xFFFFu), ifr = (int)(W.cnt >> 16);
+    const int ic = (int)(cnt & 0xFFFFu), ifr = (int)(cnt >> 16);
     if (q.n_clubs > 0 && nc > 0) {
         sum += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs);
         ++used;
@@ -289,23 +356,51 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
     uint64_t common = q.colmask & cmask;
     used += __popcll(common);
-    if (W.nh <= kHitCap) {
+    bool overflow = false;
+    for (uint32_t g = 0; g < nl; ++g) overflow |= nh_of(g) > kHitCap;
+    if (!overflow) {
         const typename H::type* hits = reinterpret_cast<const typename H::type*>(v.hits);
-        uint32_t h = 0;
-        while (common) {
-            const int t = __ffsll((unsigned long long)common) - 1;
-            common &= common - 1;
-            double dot = 0.0;
-            while (h < W.nh) {  // this column's hits, in stream (ascending tid) order
-                const typename H::type e = hits[h * hstride + threadIdx.x];
-                if ((int)H::col(e) != t) break;
-                dot += hit_product(v, H::vi(e), H::tf(e));
-                ++h;
+        // hits of the chunks in order: (g, h) walks thread first + g's list
+        uint32_t g = 0, h = 0, nhg = nh_of(0);
+        typename H::type e{};
+        auto next = [&]() -> bool {
+            while (h >= nhg) {
+                if (++g >= nl) return false;
+                h = 0;
+                nhg = nh_of(g);
             }
-            sum += dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, col_norm(st, p, cmask, t));
+            e = hits[h * hstride + first + g];
+            ++h;
+            return true;
+        };
+        // One pass in the reference's column order, driven by the HIT columns: the wave's
+        // i-th iteration computes every lane's i-th hit column (the only place the
+        // expensive term runs, so lanes stay aligned), after adding the s = 0 term of each
+        // common column the lane skips on the way (cheap table reads).
+        bool have = next();
+        while (have) {
+            const int t = (int)H::col(e);
+            double dot = 0.0;
+            while (have && (int)H::col(e) == t) {  // this column's hits, in stream (ascending tid) order
+                dot += hit_product(v, H::vi(e), H::tf(e));
+                have = next();
+            }
+            uint64_t below = common & ((1ull << t) - 1ull);
+            common &= ~below & ~(1ull << t);
+            while (below) {
+                const int c = __ffsll((unsigned long long)below) - 1;
+                below &= below - 1;
+                sum += q.sig0_col[c];
+            }
+            sum += dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, col_norm(st, l, cmask, t));
+        }
+        while (common) {
+            const int c = __ffsll((unsigned long long)common) - 1;
+            common &= common - 1;
+            sum += q.sig0_col[c];
         }
     } else {
-        sum = text_terms_slow<PACKED>(st, v, p, nset, len, cmask, sum);
+        sum = text_terms_slow<PACKED>(st, v, l, nc + nf, record_words(h2, PACKED), cmask, sum);
     }
     if (used == 0) return 0.0f;
     // recommender_similarity.cpp:114-123
@@ -313,6 +408,36 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     const double F = (double)used / (double)(kNumFixed + q.n_cols);
     if (S <= 0.0 && F <= 0.0) return 0.0f;
     return (float)((2.0 * S * F) / (S + F));
+}
+
+// FAS of slot p by one lane alone (pairs kernel): its chunks are walked one after the
+// other, so its own hit list holds the whole record's hits in order.
+template <bool PACKED>
+__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
+    Loc l{0, 0, 0};
+    if (active) {
+        h0 = st.hdr0[p];
+        h1 = st.hdr1[p];
+        h2 = st.hdr2[p];
+        l = loc_of(st, p);
+    }
+    const uint32_t nc = h2.y, nset = h2.y + h2.z;
+    const uint32_t len = record_words(h2, PACKED);
+    const uint32_t k = active ? 1u << l.lgk : 0u;
+    const uint32_t q = chunk_words(len, l.lgk, PACKED);
+    Walk W;
+    W.cnt = 0; W.nh = 0; W.pend = 0;
+    const uint32_t kmax = wave_max_u32(k);
+    const uint4* tb = st.stream + (active ? st.tile_off[l.tile] + ((uint32_t)l.cand << l.lgk) : 0);
+    for (uint32_t c = 0; c < kmax; ++c) {
+        const uint32_t j0 = c * q;
+        const uint32_t clen = (c < k && len > j0) ? min(q, len - j0) : 0u;
+        walk_chunk<PACKED, true>(W, tb + (c < k ? c : 0), j0, clen, nc, nset, v, blockDim.x);
+    }
+    if (!active) return 0.0f;
+    const uint32_t nh = W.nh;
+    return fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
 }
 
 // ---------------------------------------------------------------- wave top-k
@@ -398,8 +523,9 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     v.q = q;
     v.lg = q->lg;
     v.lge = q->lg_excl;
-    v.seed = q->seed;
-    const uint32_t kb = 8u * ((3u << q->lg) + (1u << q->lg_excl)), vb = (uint32_t)q->n_vals * 16u;
+    v.hmul = q->hmul;
+    v.excl_off = q->excl_off;
+    const uint32_t kb = 8u * (q->excl_off + (1u << q->lg_excl)), vb = (uint32_t)q->n_vals * 16u;
     char* p = smem + sizeof(QConst);
     if constexpr (!GTAB) {
         stage(p, pool + r.keys_off, kb);
@@ -413,6 +539,8 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     }
     v.hits = p;
     p += (size_t)q->n_hits_max * blockDim.x;  // n_hits_max = bytes per lane of the hit list
+    v.nh = reinterpret_cast<uint32_t*>(p);     // per-thread hit counts (split records)
+    p += 4u * blockDim.x;
     *scratch = p;
     __syncthreads();
     return v;
@@ -428,7 +556,7 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
 }
 
 template <bool PACKED, bool GTAB>
-__global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
+__global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                                 const QImageRef* __restrict__ refs, int32_t tile_begin,
                                                                 int32_t tile_end, int32_t k,
                                                                 uint64_t* __restrict__ parts,
@@ -441,14 +569,58 @@ __global__ __launch_bounds__(kScanThreads) void fas_scan_kernel(DevStore st, con
     const QView v = stage_query<GTAB>(smem, pool, r, &scratch);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t list = ~0ull;
-    for (int tile = tile_begin + (int)blockIdx.x * 4 + wave; tile < tile_end; tile += (int)gridDim.x * 4) {
-        const int p = tile * kTileSlots + lane;
-        const bool active = p < st.n_slots;
-        const float f = fas_slot<PACKED>(st, v, p, active);
-        uint64_t key = ~0ull;
+    // Static zig-zag hand-out: tiles are sorted longest first, so band b = tiles
+    // [b*W, (b+1)*W) holds W near-equal tiles; wave w takes one per band, alternating
+    // direction, which evens the sums.  (A shared atomic tile counter serialises at
+    // ~13 ns per fetch and halved the streaming rate; no atomics here.)
+    const int W = (int)gridDim.x * (kScanThreads / 64), wid = (int)blockIdx.x * (kScanThreads / 64) + wave;
+    for (int b = 0;; ++b) {
+        const int tile = tile_begin + b * W + ((b & 1) ? W - 1 - wid : wid);
+        if (tile >= tile_end) break;
+        const uint32_t lgk = st.tile_lgk[tile];
+        const int slot0 = (int)st.tile_slot0[tile];
+        const int cand = lane >> lgk, ci = lane & ((1 << lgk) - 1);
+        const bool active = cand < min(kTileSlots >> lgk, st.n_slots - slot0);
+        const int p = slot0 + cand;
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
         if (active) {
-            const int32_t uid = (int32_t)st.hdr1[p].w;
-            if (!excluded(v, (uint32_t)uid)) key = score_key(f, uid);
+            h0 = st.hdr0[p];
+            h1 = st.hdr1[p];
+            h2 = st.hdr2[p];
+        }
+        const uint32_t nc = h2.y, nset = h2.y + h2.z;
+        const uint32_t len = record_words(h2, PACKED);
+        const uint32_t q = chunk_words(len, lgk, PACKED);
+        const uint32_t j0 = (uint32_t)ci * q;
+        const uint32_t clen = (active && len > j0) ? min(q, len - j0) : 0u;
+        const Loc l{tile, cand, lgk};
+        Walk W;
+        W.cnt = 0; W.nh = 0; W.pend = 0;
+        if (!PACKED && clen > 0 && j0 > 0) W.pend = word_at(st, l, q, j0 - 1);  // a token pair may straddle chunks
+        walk_chunk<PACKED, false>(W, st.stream + st.tile_off[tile] + lane, j0, clen, nc, nset, v, blockDim.x);
+        float f = 0.0f;
+        if (lgk == 0) {
+            if (active) {
+                const uint32_t nh = W.nh;
+                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+            }
+        } else {
+            // a split record: sum the chunk counters over its lanes, publish the hit counts,
+            // and let the record's first lane finish it
+            uint32_t cnt = W.cnt;
+            for (int m = 1; m < (1 << lgk); m <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, m);
+            v.nh[threadIdx.x] = W.nh;
+            __builtin_amdgcn_wave_barrier();
+            if (active && ci == 0) {
+                const uint32_t* nhp = v.nh + threadIdx.x;
+                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
+                                         [&](uint32_t g) { return nhp[g]; });
+            }
+        }
+        uint64_t key = ~0ull;
+        if (active && ci == 0) {
+            const int32_t uid = (int32_t)h1.w;
+            if (!excluded<PACKED>(v, (uint32_t)uid)) key = score_key(f, uid);
         }
         topk_push(list, key, k, lane);
     }
@@ -654,6 +826,23 @@ hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef*
     else { if (gtab) PF_SCAN(false, true); else PF_SCAN(false, false); }
 #undef PF_SCAN
     return hipGetLastError();
+}
+
+int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
+    // the answer depends only on (variant, LDS bytes): cache it, the query is not free
+    static thread_local uint64_t last_key = ~0ull;
+    static thread_local int last_nb = 1;
+    const uint64_t key = ((uint64_t)lds << 2) | ((uint64_t)packed << 1) | (uint64_t)gtab;
+    if (key == last_key) return last_nb;
+    int nb = 0;
+    hipError_t e;
+    if (packed) e = gtab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<true, true>, kScanThreads, lds)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<true, false>, kScanThreads, lds);
+    else e = gtab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<false, true>, kScanThreads, lds)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<false, false>, kScanThreads, lds);
+    last_key = key;
+    last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    return last_nb;
 }
 
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,

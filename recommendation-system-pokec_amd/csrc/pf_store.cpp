@@ -5,6 +5,7 @@
 #include "pf_store.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -212,9 +213,14 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
 
 int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     const int32_t n = hc.n, T = hc.T;
+    // packed (fast) layout: one word per token and one tagged hash table, which needs
+    // tid < 2^18 - 1 (the all-ones token key is the padding word's), 0 <= tf < 256 and
+    // club / friend ids below 2^30 (bits 30-31 are the kind tags)
     bool packed = true;
     for (size_t k = 0; k < hc.tid.size() && packed; ++k)
-        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] >= kTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+    for (size_t k = 0; k < hc.clubs.size() && packed; ++k) packed = hc.clubs[k] < kIdLimit;
+    for (size_t k = 0; k < hc.friends.size() && packed; ++k) packed = hc.friends[k] < kIdLimit;
     if (!packed)
         for (size_t k = 0; k < hc.tf.size(); ++k)
             if (hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23)) { err = "token count outside [-2^23, 2^23)"; return PF_EUNSUPP; }
@@ -238,41 +244,58 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     std::stable_sort(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), [&](int a, int b) { return len[a] > len[b]; });
     hs.slot_of_idx.resize(n);
     for (int p = 0; p < n; ++p) hs.slot_of_idx[hs.idx_of_slot[p]] = p;
-    const int32_t ntiles = (n + kTileSlots - 1) / kTileSlots;
-    hs.tile_off.resize(ntiles);
-    hs.tile_steps.resize(ntiles);
-    hs.norm_off.resize(ntiles);
+    // tiles: take the next 64 >> lgk slots, lgk the smallest split that keeps the tile's
+    // longest chunk (its first record's) within kMaxTileSteps
+    hs.tile_off.clear(); hs.tile_steps.clear(); hs.norm_off.clear(); hs.tile_slot0.clear(); hs.tile_lgk.clear();
+    hs.slot_tile.assign(n, 0);
+    // PF_TILE_STEPS lowers the limit (tests use it to split ordinary records)
+    const char* ts = getenv("PF_TILE_STEPS");
+    const uint32_t max_steps = ts ? std::max<uint32_t>(1, (uint32_t)strtoul(ts, nullptr, 10)) : kMaxTileSteps;
     uint64_t off = 0, noff = 0;
-    for (int t = 0; t < ntiles; ++t) {
-        uint32_t mx = 0, mr = 0;
-        for (int p = t * kTileSlots; p < std::min(n, (t + 1) * kTileSlots); ++p) {
-            mx = std::max(mx, len[hs.idx_of_slot[p]]);
+    for (int s0 = 0; s0 < n;) {
+        const uint32_t mx = len[hs.idx_of_slot[s0]];
+        uint32_t lgk = 0;
+        while (lgk < 6 && (chunk_words(mx, lgk, packed) + 3) / 4 > max_steps) ++lgk;
+        const int cnt = std::min(n - s0, kTileSlots >> lgk);
+        uint32_t mr = 0;
+        for (int p = s0; p < s0 + cnt; ++p) {
             mr = std::max(mr, ncols[hs.idx_of_slot[p]]);
+            hs.slot_tile[p] = (uint32_t)hs.tile_off.size();
         }
-        hs.tile_off[t] = off;
-        hs.tile_steps[t] = (mx + 3) / 4;
-        off += (uint64_t)hs.tile_steps[t] * kTileSlots;
-        hs.norm_off[t] = noff;
+        // steps rounded up to whole 4-step groups: the walk loads whole groups, and what
+        // lies past a chunk is padding, never the next tile
+        const uint32_t steps = ((chunk_words(mx, lgk, packed) + 15) / 16) * 4;
+        hs.tile_off.push_back(off);
+        hs.tile_steps.push_back(steps);
+        hs.tile_slot0.push_back((uint32_t)s0);
+        hs.tile_lgk.push_back((uint8_t)lgk);
+        hs.norm_off.push_back(noff);
+        off += (uint64_t)steps * kTileSlots;
         noff += (uint64_t)mr * kTileSlots;
+        s0 += cnt;
     }
-    hs.stream.assign(off, make_uint4(0, 0, 0, 0));
+    // + one group of padding steps past the end: the scan's walk prefetches the group
+    // after a tile's last one (never used), and a lane with an empty chunk still loads
+    hs.stream.assign(off + 4 * kTileSlots, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     hs.norms.assign(noff, 0.0);
     hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
     par_for(n, [&](int64_t lo, int64_t hi) {
         std::vector<uint32_t> w;
         for (int64_t p = lo; p < hi; ++p) {
             const int i = hs.idx_of_slot[p];
-            const int tile = (int)(p / kTileSlots), lane = (int)(p % kTileSlots);
+            const int tile = (int)hs.slot_tile[p];
+            const uint32_t lgk = hs.tile_lgk[tile];
+            const int cand = (int)(p - hs.tile_slot0[tile]);
             w.clear();
             uint64_t mask = 0;
-            for (int64_t k = hc.club_off[i]; k < hc.club_off[i + 1]; ++k) w.push_back(hc.clubs[k]);
+            for (int64_t k = hc.club_off[i]; k < hc.club_off[i + 1]; ++k) w.push_back(hc.clubs[k] | (packed ? kTagClub : 0u));
             for (int64_t k = hc.friend_off[i]; k < hc.friend_off[i + 1]; ++k) w.push_back(hc.friends[k]);
             uint32_t rank = 0;
             for (int t = 0; t < T; ++t) {
                 const size_t r = (size_t)i * T + t;
                 if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
                 mask |= 1ull << t;
-                hs.norms[hs.norm_off[tile] + (uint64_t)rank * kTileSlots + lane] = hc.sqrt_nb[r];
+                hs.norms[hs.norm_off[tile] + (uint64_t)rank * kTileSlots + cand] = hc.sqrt_nb[r];
                 ++rank;
                 for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
                     if (packed) {
@@ -283,8 +306,14 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                     }
                 }
             }
+            // chunk c of the record goes to lane cand * k + c
+            const uint32_t q = chunk_words((uint32_t)w.size(), lgk, packed);
             uint32_t* base = reinterpret_cast<uint32_t*>(hs.stream.data() + hs.tile_off[tile]);
-            for (size_t q = 0; q < w.size(); ++q) base[((q / 4) * kTileSlots + lane) * 4 + (q % 4)] = w[q];
+            for (size_t x = 0; x < w.size(); ++x) {
+                const uint32_t c = (uint32_t)(x / q), o = (uint32_t)(x % q);
+                const uint32_t lane = ((uint32_t)cand << lgk) + c;
+                base[((o / 4) * kTileSlots + lane) * 4 + (o % 4)] = w[x];
+            }
             auto code = [](const std::unordered_map<int32_t, uint32_t>& m, int32_t v) -> uint32_t {
                 return v < 0 ? kCodeMissing : m.at(v);
             };
@@ -303,18 +332,18 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
 namespace {
 
 // 2-choice cuckoo insertion of (key, val) items into a 2^lg table; false if it does not converge
-bool cuckoo_fill(uint64_t* tab, int lg, uint32_t seed, const std::vector<uint64_t>& items) {
+bool cuckoo_fill(uint64_t* tab, int lg, uint32_t hmul, const std::vector<uint64_t>& items, uint64_t empty) {
     const size_t cap = (size_t)1 << lg;
-    for (size_t i = 0; i < cap; ++i) tab[i] = kEmptyEntry;
+    for (size_t i = 0; i < cap; ++i) tab[i] = empty;
     for (uint64_t it : items) {
         uint64_t cur = it;
-        uint32_t from = cuckoo_h1(cuckoo_x((uint32_t)cur, seed), lg);
+        uint32_t from = cuckoo_h1(cuckoo_x((uint32_t)cur, hmul), lg);
         bool placed = false;
         for (int kick = 0; kick < 500; ++kick) {
-            const uint32_t x = cuckoo_x((uint32_t)cur, seed);
+            const uint32_t x = cuckoo_x((uint32_t)cur, hmul);
             const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
-            if (tab[a] == kEmptyEntry) { tab[a] = cur; placed = true; break; }
-            if (tab[b] == kEmptyEntry) { tab[b] = cur; placed = true; break; }
+            if (tab[a] == empty) { tab[a] = cur; placed = true; break; }
+            if (tab[b] == empty) { tab[b] = cur; placed = true; break; }
             from = (from == a) ? b : a;  // evict from the slot we did not come from
             std::swap(cur, tab[from]);
         }
@@ -381,16 +410,16 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
     c.sig0_clubs = term(PF_F_CLUBS, 0.0);
     c.sig0_friends = term(PF_F_FRIENDS, 0.0);
     // hash items: distinct clubs (T0), distinct friends (T1), (column, token) weights (T2),
-    // exclusions (T3)
+    // exclusions (T3); packed corpora merge T0..T2 into one tagged table (pf_types.h)
     std::vector<uint64_t> items[4];
     std::vector<uint32_t> tmp(hc.clubs.begin() + hc.club_off[i], hc.clubs.begin() + hc.club_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) items[0].push_back(make_entry(x, 0));
+    for (uint32_t x : tmp) items[0].push_back(packed ? make_entry(x | kTagClub, 1u) : make_entry(x, 0));
     tmp.assign(hc.friends.begin() + hc.friend_off[i], hc.friends.begin() + hc.friend_off[i + 1]);
     std::sort(tmp.begin(), tmp.end());
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    for (uint32_t x : tmp) items[1].push_back(make_entry(x, 0));
+    for (uint32_t x : tmp) items[1].push_back(packed ? make_entry(x, 0x10000u) : make_entry(x, 0));
     out.vals.clear();
     c.colmask = 0;
     for (int t = 0; t < T; ++t) {
@@ -405,34 +434,47 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
             v.wq = (double)hc.tf[k] * idf;
             v.idf = idf;
             const uint32_t vi = (uint32_t)out.vals.size();
-            if (packed) items[2].push_back(make_entry(((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k], vi | ((uint32_t)t << kTidBits)));
+            if (packed)
+                items[2].push_back(make_entry(kTagTok | ((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k],
+                                              kTokVal | vi | ((uint32_t)t << kTidBits)));
             else items[2].push_back(make_entry((uint32_t)hc.tid[k], (uint32_t)t | (vi << 8)));
             out.vals.push_back(v);
         }
     }
-    c.n_hits_max = kHitCap * (packed ? 4u : 8u);
+    c.n_hits_max = (kHitCap + 1) * (packed ? 4u : 8u);  // + the dump slot
     if (excl) {
         tmp.assign(excl->begin(), excl->end());
         std::sort(tmp.begin(), tmp.end());
         tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-        for (uint32_t x : tmp) items[3].push_back(make_entry(x, 0));
+        for (uint32_t x : tmp) items[3].push_back(make_entry(x, packed ? 1u : 0u));
     }
     c.n_vals = (int32_t)out.vals.size();
     if (out.vals.size() >= (packed ? (1u << kTidBits) : (1u << 24))) return false;
+    const uint64_t empty = packed ? kEmptyEntryPacked : kEmptyEntry;
+    if (packed) {  // one table T for every record word
+        items[0].insert(items[0].end(), items[1].begin(), items[1].end());
+        items[0].insert(items[0].end(), items[2].begin(), items[2].end());
+        items[1].clear();
+        items[2].clear();
+    }
+    const int ntab = packed ? 1 : 3;
     int lg = std::max({lg_for(items[0].size()), lg_for(items[1].size()), lg_for(items[2].size())});
     int lge = lg_for(items[3].size());
     for (; lg <= kMaxHashLog2; ++lg, ++lge) {
         lge = std::min(lge, kMaxHashLog2);
-        out.keys.assign(((size_t)3 << lg) + ((size_t)1 << lge), kEmptyEntry);
+        const size_t eoff = (size_t)ntab << lg;
+        out.keys.assign(eoff + ((size_t)1 << lge), empty);
         for (uint32_t s = 0; s < 16; ++s) {
-            const uint32_t seed = s * 0x6A09E667u;
+            const uint32_t hmul = kHashMul + 2u * s * 0x6A09E667u;  // odd
             bool ok = true;
-            for (int k = 0; k < 3 && ok; ++k) ok = cuckoo_fill(out.keys.data() + ((size_t)k << lg), lg, seed, items[k]);
-            if (ok) ok = cuckoo_fill(out.keys.data() + ((size_t)3 << lg), lge, seed, items[3]);
+            for (int k = 0; k < ntab && ok; ++k)
+                ok = cuckoo_fill(out.keys.data() + ((size_t)k << lg), lg, hmul, items[k], empty);
+            if (ok) ok = cuckoo_fill(out.keys.data() + eoff, lge, hmul, items[3], empty);
             if (ok) {
                 c.lg = lg;
                 c.lg_excl = lge;
-                c.seed = seed;
+                c.hmul = hmul;
+                c.excl_off = (uint32_t)eoff;
                 return true;
             }
         }

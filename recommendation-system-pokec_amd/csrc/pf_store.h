@@ -36,6 +36,9 @@ struct HostStore {
     std::vector<uint4> stream;
     std::vector<uint64_t> tile_off;
     std::vector<uint32_t> tile_steps;
+    std::vector<uint32_t> tile_slot0;   // first slot of each tile
+    std::vector<uint8_t> tile_lgk;      // log2 of the lanes per candidate (long records are split)
+    std::vector<uint32_t> slot_tile;    // tile of each slot
     std::vector<double> norms;
     std::vector<uint64_t> norm_off;
     std::vector<uint4> hdr0, hdr1, hdr2;

@@ -18,27 +18,49 @@ constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
 constexpr uint32_t kHitCap = 24;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
 constexpr int kMaxHashLog2 = 16;    // cuckoo tables <= 65536 slots (h1/h2 from one 32-bit product)
+constexpr uint32_t kMaxTileSteps = 48;  // a record longer than 48 steps (192 words) is split over lanes
 
-// Query hash: four 2-choice cuckoo tables of 8-byte entries {key, val} (uint2).
-//   T0 clubs    key = club id                      val = 0
-//   T1 friends  key = friend id                    val = 0
-//   T2 tokens   packed: key = col << 18 | tid      val = value index | col << 18
-//               wide:   key = tid                  val = col | value index << 8
-//   T3 excl     key = uid (adj[q] + {q})            val = 0
-// T0..T2 share one capacity 2^lg (so a word's table is base + kind * 2^lg); T3 has its own.
-// Empty slot = {~0, ~0}; a hit needs val != ~0, so an id equal to ~0 cannot fake a match.
-constexpr uint32_t kEmptyVal = 0xFFFFFFFFu;
-constexpr uint64_t kEmptyEntry = ~0ull;
+// Query hash: 2-choice cuckoo tables of 8-byte entries {key, val} (uint2), hashed by one
+// multiply with a per-query odd multiplier (x = key * hmul; slots = two bit fields of x).
+// Packed corpora (the fast path) use ONE table for every record word plus an exclusion
+// table, so a word's probe needs no per-kind table choice:
+//   T   clubs    key = id | kTagClub                val = 1        (counts clubs, low 16 bits)
+//       friends  key = id                           val = 0x10000  (counts friends, high 16 bits)
+//       tokens   key = kTagTok | col << 18 | tid    val = kTokVal | col << 18 | value index
+//   T3  excl     key = uid (adj[q] + {q})            val = 1
+//   empty = {~0, 0}: a miss reads val 0, and the padding word ~0 only ever matches empties
+// Wide corpora keep three tables T0 clubs | T1 friends | T2 tokens (2^lg each), keys
+// untagged (T2: key = tid, val = col | value index << 8), then T3; empty = {~0, ~0}.
+constexpr uint32_t kEmptyVal = 0xFFFFFFFFu;       // wide tables: miss
+constexpr uint64_t kEmptyEntry = ~0ull;           // wide tables: empty slot
+constexpr uint64_t kEmptyEntryPacked = 0xFFFFFFFFull;  // packed tables: {key ~0, val 0}
 constexpr uint32_t kHashMul = 0x9E3779B1u;
+constexpr uint32_t kTagClub = 0x80000000u;
+constexpr uint32_t kTagTok = 0x40000000u;
+constexpr uint32_t kTokVal = 0x01000000u;
+constexpr uint32_t kIdLimit = 0x40000000u;        // packed: club / friend ids below 2^30
+constexpr uint32_t kPadWord = 0xFFFFFFFFu;        // stream padding
 
 // Record stream (per candidate, tile-interleaved in 16-B steps):
 //   clubs[n_clubs] | friends[n_friends] | tokens[n_tok]
-// packed token word = tf << 24 | col << 18 | tid      (tid < 2^18, 0 <= tf < 256, col < 64);
-//   its low 24 bits are exactly the T2 key (col << 18 | tid)
+// packed: club word = id | kTagClub (the T key), friend word = id,
+//   token word = tf << 24 | col << 18 | tid  (tid < 2^18 - 1, 0 <= tf < 256, col < 64);
+//   kTagTok | (low 24 bits) is the T key; every word past a record is kPadWord
 // wide token = 2 words: tid, (tf << 8) | col          (tf in [-2^23, 2^23))
 // Tokens are grouped by column (ascending), ascending tid within a column.
 constexpr uint32_t kTidBits = 18;
 constexpr uint32_t kTidMask = (1u << kTidBits) - 1;
+
+// Tiles: 64 lanes = 64 >> lgk candidates, each candidate's record split into k = 1 << lgk
+// contiguous chunks of q = ceil(len / k) words (rounded up to even in the wide format),
+// chunk c of candidate i in lane i * k + c, so no tile is longer than kMaxTileSteps
+// (unless a single record is longer than 64 * 192 words).  Candidates are sorted by record
+// length, so almost every tile has k = 1.
+__host__ __device__ inline uint32_t chunk_words(uint32_t len, uint32_t lgk, bool packed) {
+    uint32_t q = (len + (1u << lgk) - 1) >> lgk;
+    if (!packed) q = (q + 1) & ~1u;
+    return q;
+}
 
 // Per-slot header, 3 x uint4 (48 B), SoA:
 //   h0 = {colmask lo, colmask hi, completion, age}
@@ -47,7 +69,7 @@ constexpr uint32_t kTidMask = (1u << kTidBits) - 1;
 constexpr uint32_t kCodeMissing = 0xFFu;
 
 // 2-choice cuckoo slots of a 32-bit key: one multiply, two bit fields of the product
-__host__ __device__ inline uint32_t cuckoo_x(uint32_t key, uint32_t seed) { return (key ^ seed) * kHashMul; }
+__host__ __device__ inline uint32_t cuckoo_x(uint32_t key, uint32_t hmul) { return key * hmul; }
 __host__ __device__ inline uint32_t cuckoo_h1(uint32_t x, int lg) { return x >> (32 - lg); }
 __host__ __device__ inline uint32_t cuckoo_h2(uint32_t x, int lg) { return (x >> (32 - 2 * lg)) & ((1u << lg) - 1u); }
 __host__ __device__ inline uint64_t make_entry(uint32_t key, uint32_t val) { return ((uint64_t)val << 32) | key; }
@@ -61,9 +83,9 @@ struct QConst {
     uint32_t pubcode, gencode; // kCodeMissing when < 0
     int32_t a_regcnt;          // parts >= 0 (0 -> region term never used)
     int32_t n_clubs, n_friends;// |A.clubs|, |A.friends| with duplicates
-    int32_t lg;                // capacity log2 of each of T0..T2
+    int32_t lg;                // capacity log2 of T (packed) / of each of T0..T2 (wide)
     int32_t lg_excl;           // capacity log2 of T3
-    uint32_t seed;             // cuckoo hash seed (all tables)
+    uint32_t hmul;             // cuckoo hash multiplier (odd; all tables)
     int32_t n_vals;            // token value entries
     int32_t n_cols;            // T
     double sqrt_clubs, sqrt_friends;     // sqrt((double)|A|)
@@ -78,7 +100,7 @@ struct QConst {
     double zmean[kNormSlots];
     double zsd[kNormSlots];
     uint32_t zmode_lo, zmode_hi, zmode_fx, n_hits_max;  // n_hits_max: hit-list bytes per lane
-    uint32_t pad2;
+    uint32_t excl_off;         // entry offset of T3 (1 << lg packed, 3 << lg wide)
 };
 
 // token value of a query hash entry: dot += wq * (tf * idf)
@@ -87,7 +109,7 @@ struct QVal {
     double idf;
 };
 
-// One query image in device memory: QConst + tables[3 * 2^lg + 2^lg_excl] + vals[n_vals].
+// One query image in device memory: QConst + tables[excl_off + 2^lg_excl] + vals[n_vals].
 struct QImageRef {
     uint32_t const_off;   // byte offset of QConst in the image pool
     uint32_t keys_off;    // byte offset of the key table
@@ -95,11 +117,12 @@ struct QImageRef {
     uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 
-// Per-query rendezvous of one scan launch: blocks finished.  Zeroed by the host before
-// every launch (it rides in the query upload).  Padded to 16 B.
+// Per-query rendezvous of one scan launch: blocks finished (next_tile is reserved).
+// Zeroed by the host before every launch (it rides in the query upload).  16 B.
 struct ScanSync {
     unsigned int done;
-    unsigned int pad[3];
+    unsigned int next_tile;
+    unsigned int pad[2];
 };
 
 // top-k key: ascending key == (score desc, uid asc), recommender_graph.cpp:97-101
@@ -126,8 +149,11 @@ __host__ __device__ inline int32_t key_uid(uint64_t k) {
 struct DevStore {
     const uint4* stream;       // interleaved record stream, [tile][step][lane] uint4
     const uint64_t* tile_off;  // [n_tiles] uint4 offset of each tile
-    const uint32_t* tile_steps;// [n_tiles] 16-B steps of the longest record in the tile
-    const double* norms;       // [tile][rank][lane] sqrt(sum (tf*idf)^2) per non-empty column
+    const uint32_t* tile_steps;// [n_tiles] 16-B steps of the longest chunk in the tile
+    const uint32_t* tile_slot0;// [n_tiles] first slot of the tile
+    const uint8_t* tile_lgk;   // [n_tiles] log2 lanes per candidate
+    const uint32_t* slot_tile; // [n_slots] tile of the slot
+    const double* norms;       // [tile][rank][candidate in tile] sqrt(sum (tf*idf)^2) per non-empty column
     const uint64_t* norm_off;  // [n_tiles] double offset of each tile's norms
     const uint4* hdr0;         // [n_slots]
     const uint4* hdr1;

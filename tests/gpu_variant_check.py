@@ -1,6 +1,7 @@
 """Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_STAGE_LIMIT
-once per process, so each forced kernel variant (global-memory query tables) runs in its
-own process.  Exits non-zero on any mismatch."""
+and PF_TILE_STEPS once per process/context, so each forced kernel variant (global-memory
+query tables, records split over lanes) runs in its own process.  Exits non-zero on any
+mismatch."""
 import sys
 
 import numpy as np

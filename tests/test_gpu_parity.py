@@ -129,11 +129,13 @@ def test_big_top64_vs_oracle(big):
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
-@pytest.mark.parametrize("env", [{"PF_STAGE_LIMIT": "0"}, {"PF_STAGE_LIMIT": "1024"}],
-                         ids=["global-tables", "threshold-1k"])
+@pytest.mark.parametrize("env", [{"PF_STAGE_LIMIT": "0"}, {"PF_STAGE_LIMIT": "1024"}, {"PF_TILE_STEPS": "3"},
+                                 {"PF_TILE_STEPS": "1", "PF_STAGE_LIMIT": "0"}],
+                         ids=["global-tables", "threshold-1k", "split-records", "split-records-global"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
-    query of the batch has tables above 1 KiB (the whole launch then probes global)."""
+    query of the batch has tables above 1 KiB (the whole launch then probes global);
+    records split over up to 64 lanes (tiles capped at 3 or 1 steps)."""
     import os
     import subprocess
     import sys

@@ -226,7 +226,10 @@ __device__ __forceinline__ Loc loc_of(const DevStore& st, int p) {
 
 __device__ __forceinline__ double col_norm(const DevStore& st, const Loc& l, uint64_t cmask, int t) {
     const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
-    return st.norms[st.norm_off[l.tile] + (uint64_t)r * kTileSlots + l.cand];
+    // [tile][candidate][rank]: a candidate's norms share cache lines, so its hit columns
+    // re-use the lines its first one brought in
+    const uint64_t base = st.norm_off[l.tile], mr = (st.norm_off[l.tile + 1] - base) >> 6;
+    return st.norms[base + (uint64_t)l.cand * mr + r];
 }
 
 // word j of a candidate's record (chunk j / q in lane cand * k + j / q)
@@ -329,6 +332,28 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
     const QConst& q = *v.q;
     const uint32_t hstride = blockDim.x;
     const uint32_t nc = h2.y, nf = h2.z;
+    const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    uint64_t common = q.colmask & cmask;
+    bool overflow = false;
+    for (uint32_t g = 0; g < nl; ++g) overflow |= nh_of(g) > kHitCap;
+    // token hits of the chunks in order: (g, h) walks thread first + g's list
+    const typename H::type* hits = reinterpret_cast<const typename H::type*>(v.hits);
+    uint32_t g = 0, h = 0, nhg = overflow ? 0u : nh_of(0);
+    typename H::type e{};
+    auto next = [&]() -> bool {
+        while (h >= nhg) {
+            if (++g >= nl) return false;
+            h = 0;
+            nhg = nh_of(g);
+        }
+        e = hits[h * hstride + first + g];
+        ++h;
+        return true;
+    };
+    bool have = next();
+    // the first hit column's norm (global) is requested now and lands under the fixed terms
+    double nrm = have ? col_norm(st, l, cmask, (int)H::col(e)) : 0.0;
+
     double sum = 0.0;
     int used = 0;
     const uint32_t pb = h2.x & 0xFFu, gb = (h2.x >> 8) & 0xFFu;
@@ -353,38 +378,22 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
         sum += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends);
         ++used;
     }
-    const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
-    uint64_t common = q.colmask & cmask;
     used += __popcll(common);
-    bool overflow = false;
-    for (uint32_t g = 0; g < nl; ++g) overflow |= nh_of(g) > kHitCap;
     if (!overflow) {
-        const typename H::type* hits = reinterpret_cast<const typename H::type*>(v.hits);
-        // hits of the chunks in order: (g, h) walks thread first + g's list
-        uint32_t g = 0, h = 0, nhg = nh_of(0);
-        typename H::type e{};
-        auto next = [&]() -> bool {
-            while (h >= nhg) {
-                if (++g >= nl) return false;
-                h = 0;
-                nhg = nh_of(g);
-            }
-            e = hits[h * hstride + first + g];
-            ++h;
-            return true;
-        };
         // One pass in the reference's column order, driven by the HIT columns: the wave's
         // i-th iteration computes every lane's i-th hit column (the only place the
         // expensive term runs, so lanes stay aligned), after adding the s = 0 term of each
-        // common column the lane skips on the way (cheap table reads).
-        bool have = next();
+        // common column the lane skips on the way (cheap table reads).  The next hit
+        // column's norm is requested before this column's term is computed.
         while (have) {
             const int t = (int)H::col(e);
+            const double nrm_t = nrm;
             double dot = 0.0;
             while (have && (int)H::col(e) == t) {  // this column's hits, in stream (ascending tid) order
                 dot += hit_product(v, H::vi(e), H::tf(e));
                 have = next();
             }
+            if (have) nrm = col_norm(st, l, cmask, (int)H::col(e));
             uint64_t below = common & ((1ull << t) - 1ull);
             common &= ~below & ~(1ull << t);
             while (below) {
@@ -392,7 +401,7 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
                 below &= below - 1;
                 sum += q.sig0_col[c];
             }
-            sum += dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, col_norm(st, l, cmask, t));
+            sum += dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm_t);
         }
         while (common) {
             const int c = __ffsll((unsigned long long)common) - 1;
@@ -569,13 +578,29 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
     const QView v = stage_query<GTAB>(smem, pool, r, &scratch);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t list = ~0ull;
-    // Static zig-zag hand-out: tiles are sorted longest first, so band b = tiles
-    // [b*W, (b+1)*W) holds W near-equal tiles; wave w takes one per band, alternating
-    // direction, which evens the sums.  (A shared atomic tile counter serialises at
-    // ~13 ns per fetch and halved the streaming rate; no atomics here.)
+    // Tile hand-out, longest tiles first.  Static zig-zag for all but the last two bands
+    // (band b = tiles [b*W, (b+1)*W) holds W near-equal tiles; wave w takes one per band,
+    // alternating direction), then the tail from per-XCD counters, so waves that drew
+    // cheap tiles (few hits) take more.  One shared counter for every tile serialises at
+    // ~13 ns per fetch and halved the streaming rate; per-XCD counters on the last
+    // bands only keep the fetches few and uncontended.
     const int W = (int)gridDim.x * (kScanThreads / 64), wid = (int)blockIdx.x * (kScanThreads / 64) + wave;
+    const int ntiles = tile_end - tile_begin;
+    const int nstatic = max(0, ntiles / W - 2) * W;
+    // blocks are dispatched to the 8 XCDs round-robin; with fewer than 8 blocks every
+    // group still has one, so every residue class of the tail is drained
+    const int ngrp = min(8, (int)gridDim.x), xcd = (int)blockIdx.x % ngrp;
+    unsigned* xctr = &sync[blockIdx.y].xcd_next[xcd * 16];
     for (int b = 0;; ++b) {
-        const int tile = tile_begin + b * W + ((b & 1) ? W - 1 - wid : wid);
+        int tile;
+        if (b * W < nstatic) {
+            tile = tile_begin + b * W + ((b & 1) ? W - 1 - wid : wid);
+        } else {
+            unsigned t = 0;
+            if (lane == 0) t = atomicAdd(xctr, 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            tile = tile_begin + nstatic + (int)t * ngrp + xcd;  // group x drains tail tiles = x (mod ngrp)
+        }
         if (tile >= tile_end) break;
         const uint32_t lgk = st.tile_lgk[tile];
         const int slot0 = (int)st.tile_slot0[tile];

@@ -276,6 +276,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     }
     // + one group of padding steps past the end: the scan's walk prefetches the group
     // after a tile's last one (never used), and a lane with an empty chunk still loads
+    hs.norm_off.push_back(noff);  // sentinel: a tile's rank count = (norm_off[t+1] - norm_off[t]) / 64
     hs.stream.assign(off + 4 * kTileSlots, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     hs.norms.assign(noff, 0.0);
     hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
@@ -295,7 +296,8 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                 const size_t r = (size_t)i * T + t;
                 if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
                 mask |= 1ull << t;
-                hs.norms[hs.norm_off[tile] + (uint64_t)rank * kTileSlots + cand] = hc.sqrt_nb[r];
+                const uint64_t mr = (hs.norm_off[tile + 1] - hs.norm_off[tile]) / kTileSlots;
+                hs.norms[hs.norm_off[tile] + (uint64_t)cand * mr + rank] = hc.sqrt_nb[r];
                 ++rank;
                 for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
                     if (packed) {

@@ -117,12 +117,12 @@ struct QImageRef {
     uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 
-// Per-query rendezvous of one scan launch: blocks finished (next_tile is reserved).
-// Zeroed by the host before every launch (it rides in the query upload).  16 B.
+// Per-query rendezvous of one scan launch: blocks finished, and the tail tile counters.
+// Zeroed by the host before every launch (it rides in the query upload).
 struct ScanSync {
     unsigned int done;
-    unsigned int next_tile;
-    unsigned int pad[2];
+    unsigned int pad[31];
+    unsigned int xcd_next[8 * 16];  // tail tile counter per XCD, 64 B apart
 };
 
 // top-k key: ascending key == (score desc, uid asc), recommender_graph.cpp:97-101
@@ -153,8 +153,8 @@ struct DevStore {
     const uint32_t* tile_slot0;// [n_tiles] first slot of the tile
     const uint8_t* tile_lgk;   // [n_tiles] log2 lanes per candidate
     const uint32_t* slot_tile; // [n_slots] tile of the slot
-    const double* norms;       // [tile][rank][candidate in tile] sqrt(sum (tf*idf)^2) per non-empty column
-    const uint64_t* norm_off;  // [n_tiles] double offset of each tile's norms
+    const double* norms;       // [tile][candidate in tile][rank] sqrt(sum (tf*idf)^2) per non-empty column
+    const uint64_t* norm_off;  // [n_tiles + 1] double offset of each tile's norms (64 x ranks per tile)
     const uint4* hdr0;         // [n_slots]
     const uint4* hdr1;
     const uint4* hdr2;

@@ -1,0 +1,69 @@
+"""The multi-GPU exchange of bench.py on CPU: world_size-2 gloo ranks all-gather their
+per-shard top-k keys (the 64-bit (score desc, uid asc) keys of pokec_fas.h) and the
+merge of the gathered keys equals the top-k of the union.  The device merge kernel is
+covered on the GPU (test_gpu_parity.test_sharded_scan_merges_to_single_gpu_result)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _key(score, uid):
+    b = int(np.float32(score).view(np.uint32))
+    if b & 0x7FFFFFFF == 0:
+        b = 0
+    ordv = (~b & 0xFFFFFFFF) if b & 0x80000000 else (b | 0x80000000)
+    return ((~ordv & 0xFFFFFFFF) << 32) | ((uid & 0xFFFFFFFF) ^ 0x80000000)
+
+
+def _worker(rank, world, port, k, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(7)
+    nq, n = 3, 400
+    scores = rng.random((nq, n)).astype(np.float32)
+    scores[:, 10:20] = 0.5  # ties broken by uid
+    uids = np.arange(1, n + 1)
+    shard = np.array_split(np.arange(n), world)[rank]
+    local = np.full((nq, k), np.iinfo(np.uint64).max, np.uint64)
+    for qi in range(nq):
+        keys = sorted(_key(scores[qi, j], int(uids[j])) for j in shard)[:k]
+        local[qi, :len(keys)] = keys
+    t = torch.from_numpy(local.view(np.int64))
+    gathered = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(gathered, t)
+    if rank == 0:
+        allk = np.stack([g.numpy().view(np.uint64) for g in gathered])  # [world][nq][k]
+        ok = True
+        for qi in range(nq):
+            merged = np.sort(allk[:, qi, :].reshape(-1))[:k]
+            ref = np.array(sorted(_key(scores[qi, j], int(uids[j])) for j in range(n))[:k], np.uint64)
+            ok &= bool(np.array_equal(merged, ref))
+        ret.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_allgather_merge_equals_union_topk(world):
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 10, ret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert ret.get(timeout=10) is True

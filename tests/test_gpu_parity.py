@@ -230,3 +230,31 @@ def test_cpp_facade_matches_reference():
     p = out[-1].split()
     assert [int(x.split(":")[0]) for x in p[5:]] == list(ids)
     assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))
+
+
+def test_sharded_scan_merges_to_single_gpu_result(big):
+    """The multi-GPU path on one device: each candidate shard's top-k keys (pf_set_shard +
+    pf_scan_keys_async), concatenated as the all-gather would, merged by
+    pf_merge_keys_async, equal the unsharded scan bit for bit."""
+    import torch
+    pf = tl.product()
+    c, eng, orc = big
+    q = np.array([3, 8, 1000, 15000, 19999], np.int32)
+    k = 10
+    ref = eng.recommend_interest_all(list(q), k)
+    eng2 = tl.engine(c.desc_ptr())
+    s = torch.cuda.Stream()
+    for world in (2, 3):
+        parts = torch.empty((world, len(q), k), dtype=torch.int64, device="cuda")
+        for r in range(world):
+            eng2.set_shard(r, world)
+            eng2.scan_keys_async(q, k, parts[r].data_ptr(), s.cuda_stream)
+        out = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
+        eng2.merge_keys_async(parts.data_ptr(), world, len(q), k, out.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        keys = out.cpu().numpy().view(np.uint64)
+        for i in range(len(q)):
+            uids, scores = pf.decode_keys(keys[i])
+            assert list(uids) == list(ref[i][0]), (world, q[i])
+            assert np.array_equal(scores.view(np.uint32), ref[i][1].view(np.uint32))
+    eng2.set_shard(0, 1)

@@ -229,6 +229,11 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     std::vector<uint32_t> len(n), ncols(n);
     int64_t alg = 0;
     for (int i = 0; i < n; ++i) {
+        // the walk counts club and friend intersections in 16-bit halves of one word
+        if (hc.club_off[i + 1] - hc.club_off[i] > 0xFFFF || hc.friend_off[i + 1] - hc.friend_off[i] > 0xFFFF) {
+            err = "a profile lists more than 65535 clubs or friends";
+            return PF_EUNSUPP;
+        }
         const int64_t nc = hc.club_off[i + 1] - hc.club_off[i], nf = hc.friend_off[i + 1] - hc.friend_off[i];
         const int64_t nt = hc.tok_off[(size_t)(i + 1) * T] - hc.tok_off[(size_t)i * T];
         uint32_t nz = 0;

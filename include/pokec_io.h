@@ -16,6 +16,8 @@
  *                          VocabBuilder::load_vocab (club names only)
  *                                                        src/vocab_builder.cpp:133-197
  *   pf_dataset_profile_json  write_profile_json          src/api_cli.cpp:49-84
+ *   pf_compute_normalizers   compute_column_normalizers + save_column_normalizers
+ *                                                        src/utils.cpp:144-240         (A18)
  *   pf_holdout_friends       run_friends_holdout_test    src/test.cpp:13-105           (A19)
  *   pf_recommendation_tests  run_recommendation_tests_sample
  *                                                        src/recommendation_tests.cpp:68-169 (A19)
@@ -78,6 +80,18 @@ int pf_dataset_adj_order(const pf_dataset* ds, int32_t* out, int32_t cap, int32_
 int pf_dataset_profile_json(const pf_dataset* ds, int32_t uid, char* buf, int64_t cap, int64_t* len);
 /* Club slug for a club id from data/clubs_map.csv (NULL if none). */
 const char* pf_dataset_club_name(const pf_dataset* ds, int32_t club_id);
+
+/* compute_column_normalizers(profiles, text_columns, sample_size, comps_per_user) as
+ * kurs runs it when data/column_normalizers.csv is missing (main.cpp:118-128): the
+ * mt19937(12345) pair sampler over the profiles map in the reference's iteration
+ * order, field and raw-count column similarities, sample mean / sd per key.  A host
+ * statistic of the offline step (the pairs are random, so there is no scan to run),
+ * bit-exact with the reference.  Writes PF_NUM_FIXED + n_cols (mean, sd) pairs in the
+ * pf_corpus_desc slot order to out_mean/out_sd (either may be NULL) and, when
+ * save_csv is not NULL, the CSV save_column_normalizers writes (same key order and
+ * number formatting). */
+int pf_compute_normalizers(const pf_dataset* ds, int32_t sample_size, int32_t comps_per_user, const char* save_csv,
+                           float* out_mean, float* out_sd);
 
 /* run_friends_holdout_test: per tested user, hits/hold_k in file order.
  * ctx must have been opened on pf_dataset_desc(ds); its adjacency is restored on return. */

@@ -16,7 +16,7 @@ exists.  Steps:
 The corpora themselves are NOT committed: tests regenerate them bit-identically
 from the same generator + parameters (recorded in tests/golden/manifest.json).
 
-usage: python oracle/gen_golden.py            (needs `make -C oracle ref` and `make -C tools`)
+usage: python oracle/gen_golden.py [--norms-only]   (needs `make -C oracle ref` and `make -C tools`)
 """
 import gzip
 import json
@@ -61,6 +61,28 @@ def transcript_for(work, uids, load_users="10000"):
     return lines, r.stdout.decode()
 
 
+# compute_column_normalizers goldens (A18): corpus -> (sample_size, comps_per_user)
+NORM_RUNS = {"A": (3000, 5), "B": (1500, 3)}
+
+
+def gen_norms():
+    """ref_norms on corpora A and B: the CSV save_column_normalizers writes and the
+    (mean, sd) float bits, as tests/golden/<corpus>/norms_computed_{csv,bits}.txt.gz."""
+    exe = os.path.join(HERE, "_ref", "ref_norms")
+    for name, (sample, comps) in NORM_RUNS.items():
+        c = CORPORA[name]
+        out = os.path.join(GOLDEN, name)
+        with tempfile.TemporaryDirectory() as work, tempfile.TemporaryDirectory() as raw:
+            corpus = synth.Corpus(n_users=c["n_users"], seed=c["seed"], edge_cases=c["edge_cases"])
+            corpus.write_reference_files(work, normalizers=c["normalizers"], median=c["median"])
+            corpus.close()
+            csv, bits = os.path.join(raw, "norms_computed_csv.txt"), os.path.join(raw, "norms_computed_bits.txt")
+            subprocess.run([exe, work, csv, bits, str(sample), str(comps)], check=True, stdout=subprocess.DEVNULL)
+            for fn in (csv, bits):
+                gz_copy(fn, os.path.join(out, os.path.basename(fn) + ".gz"))
+        print("norms", name, "done", file=sys.stderr)
+
+
 def gz_copy(src, dst):
     with open(src, "rb") as fi, open(dst, "wb") as raw, \
             gzip.GzipFile(fileobj=raw, mode="wb", compresslevel=9, mtime=0) as fo:
@@ -69,6 +91,9 @@ def gz_copy(src, dst):
 
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
+    if "--norms-only" in sys.argv:
+        gen_norms()
+        return
     manifest = {"generator": "tools/pokec_synth.cpp", "corpora": {}, "api_cli": {}}
     for name, c in CORPORA.items():
         out = os.path.join(GOLDEN, name)
@@ -97,6 +122,8 @@ def main():
         with gzip.open(os.path.join(out, "transcript_stdout.txt.gz"), "wt", compresslevel=9) as f:
             f.write(stdout)
     manifest["api_cli"] = dict(API_CORPUS, load_users="10000", uids=uids)
+    gen_norms()
+    manifest["norm_runs"] = {k: list(v) for k, v in NORM_RUNS.items()}
     with open(os.path.join(GOLDEN, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("golden fixtures written to", GOLDEN, file=sys.stderr)

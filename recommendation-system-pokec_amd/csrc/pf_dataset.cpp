@@ -472,9 +472,136 @@ const char* pf_dataset_club_name(const pf_dataset* ds, int32_t club_id) {
 
 }  // extern "C"
 
-// ---------------------------------------------------------------- hold-out drivers (A19)
+// ---------------------------------------------------------------- normalisers (A18)
+#include <cmath>
 #include <random>
 #include <unordered_set>
+
+namespace {
+
+// vec_set_similarity_local (utils.cpp:83-92): B's entries (with duplicates) found in set(A)
+float set_sim(const std::vector<uint32_t>& A, const std::vector<uint32_t>& B) {
+    if (A.empty() || B.empty()) return 0.0f;
+    std::unordered_set<uint32_t> a(A.begin(), A.end());
+    int inter = 0;
+    for (uint32_t v : B) inter += a.count(v) != 0;
+    const double den = std::sqrt((double)A.size()) * std::sqrt((double)B.size());
+    if (den <= 0.0) return 0.0f;
+    return (float)((double)inter / den);
+}
+
+// region_similarity_local (utils.cpp:94-103)
+float region_sim(const int32_t* A, const int32_t* B) {
+    int ac = 0, bc = 0, m = 0;
+    for (int i = 0; i < 3; ++i) {
+        ac += A[i] >= 0;
+        bc += B[i] >= 0;
+        m += A[i] >= 0 && B[i] >= 0 && A[i] == B[i];
+    }
+    if (ac == 0 || bc == 0) return 0.0f;
+    return (float)((double)m / (std::sqrt((double)ac) * std::sqrt((double)bc)));
+}
+
+// cosine_counts_maps_local (utils.cpp:105-121) on one column's (tid, tf) lists.  All its
+// sums are of integer products, exact in double, so the map iteration order is moot.
+float count_cosine(const std::pair<int32_t, int32_t>* a, int na, const std::pair<int32_t, int32_t>* b, int nb) {
+    if (na == 0 || nb == 0) return 0.0f;
+    double sa = 0.0, sb = 0.0, dot = 0.0;
+    for (int i = 0; i < na; ++i) sa += (double)a[i].second * a[i].second;
+    for (int j = 0; j < nb; ++j) sb += (double)b[j].second * b[j].second;
+    if (sa <= 0.0 || sb <= 0.0) return 0.0f;
+    for (int i = 0; i < na; ++i)
+        for (int j = 0; j < nb; ++j)
+            if (a[i].first == b[j].first) dot += (double)a[i].second * b[j].second;
+    const double norm = std::sqrt(sa) * std::sqrt(sb);
+    if (norm <= 0.0) return 0.0f;
+    return (float)(dot / norm);
+}
+
+std::pair<float, float> mean_sd(const std::vector<double>& v) {  // utils.cpp:212-226
+    if (v.empty()) return {0.0f, 1.0f};
+    double mu = 0.0;
+    for (double x : v) mu += x;
+    mu /= (double)v.size();
+    double s = 0.0;
+    if (v.size() > 1) {
+        for (double x : v) {
+            const double d = x - mu;
+            s += d * d;
+        }
+        s = std::sqrt(s / (double)(v.size() - 1));
+        if (s == 0.0) s = 1.0;
+    } else {
+        s = 1.0;
+    }
+    return {(float)mu, (float)s};
+}
+
+}  // namespace
+
+extern "C" int pf_compute_normalizers(const pf_dataset* ds, int32_t sample_size, int32_t comps_per_user,
+                                      const char* save_csv, float* out_mean, float* out_sd) {
+    if (!ds || sample_size < 0 || comps_per_user < 0) return fail("bad argument");
+    const size_t T = ds->cols.size();
+    static const char* const keys[kFixed] = {"public", "gender", "completion", "age", "region", "clubs", "friends"};
+    std::unordered_map<std::string, std::pair<float, float>> result;
+    if (!ds->profiles.empty()) {
+        std::vector<int> ids;  // the profiles map in its iteration order (utils.cpp:163-164)
+        ids.reserve(ds->profiles.size());
+        for (auto& kv : ds->profiles) ids.push_back(kv.first);
+        std::mt19937 rng(12345);
+        std::uniform_int_distribution<size_t> dist(0, ids.size() - 1);
+        const size_t need = (size_t)sample_size * (size_t)comps_per_user;
+        std::unordered_set<uint64_t> seen;
+        std::vector<std::vector<double>> text(T);
+        std::unordered_map<std::string, std::vector<double>> field;  // insertion order as utils.cpp:170-171
+        for (auto k : keys) field[k] = std::vector<double>();
+        std::vector<double>* fv[kFixed];
+        for (int k = 0; k < kFixed; ++k) fv[k] = &field[keys[k]];
+        size_t attempts = 0;
+        while (seen.size() < need && attempts < need * 10) {
+            ++attempts;
+            const int a = ids[dist(rng)];
+            const int b = ids[dist(rng)];
+            if (a == b) continue;
+            uint32_t x = (uint32_t)a, y = (uint32_t)b;  // pair_key_uint64 (utils.cpp:70-75)
+            if (x > y) std::swap(x, y);
+            if (!seen.insert(((uint64_t)x << 32) | y).second) continue;
+            const Row& A = ds->rows[ds->profiles.find(a)->second];
+            const Row& B = ds->rows[ds->profiles.find(b)->second];
+            fv[0]->push_back(A.pub >= 0 && B.pub >= 0 && A.pub == B.pub ? 1.0 : 0.0);
+            fv[1]->push_back(A.gen >= 0 && B.gen >= 0 && A.gen == B.gen ? 1.0 : 0.0);
+            double sc = 0.0, sa = 0.0;
+            if (A.comp > 0 && B.comp > 0) sc = (double)std::min(A.comp, B.comp) / (double)std::max(A.comp, B.comp);
+            if (A.age > 0 && B.age > 0) sa = (double)std::min(A.age, B.age) / (double)std::max(A.age, B.age);
+            fv[2]->push_back(sc);
+            fv[3]->push_back(sa);
+            fv[4]->push_back(region_sim(A.reg, B.reg));
+            fv[5]->push_back(set_sim(A.clubs, B.clubs));
+            fv[6]->push_back(set_sim(A.friends, B.friends));
+            for (size_t t = 0; t < T; ++t)
+                text[t].push_back(count_cosine(A.tok.data() + A.col_off[t], A.col_off[t + 1] - A.col_off[t],
+                                               B.tok.data() + B.col_off[t], B.col_off[t + 1] - B.col_off[t]));
+        }
+        for (auto& kv : field) result[kv.first] = mean_sd(kv.second);
+        for (size_t t = 0; t < T; ++t) result[ds->cols[t]] = mean_sd(text[t]);
+    }
+    for (size_t k = 0; k < kFixed + T; ++k) {
+        auto it = result.find(k < (size_t)kFixed ? std::string(keys[k]) : ds->cols[k - kFixed]);
+        const std::pair<float, float> v = it == result.end() ? std::pair<float, float>(0.0f, 0.0f) : it->second;
+        if (out_mean) out_mean[k] = v.first;
+        if (out_sd) out_sd[k] = v.second;
+    }
+    if (save_csv) {  // save_column_normalizers (utils.cpp:144-153)
+        std::ofstream out(save_csv);
+        if (!out.is_open()) return fail(std::string("cannot write ") + save_csv);
+        out << "column,mean,stddev\n";
+        for (auto& kv : result) out << kv.first << "," << kv.second.first << "," << kv.second.second << "\n";
+    }
+    return PF_OK;
+}
+
+// ---------------------------------------------------------------- hold-out drivers (A19)
 
 namespace {
 

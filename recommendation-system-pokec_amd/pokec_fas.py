@@ -29,7 +29,7 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
-              "pf_holdout_friends", "pf_recommendation_tests"]
+              "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests"]
 PF_LOAD_REFERENCE_CAP = 100000
 
 
@@ -98,6 +98,7 @@ def lib():
         L.pf_dataset_profile_json.argtypes = [V, I32, V, I64, ctypes.POINTER(I64)]
         L.pf_dataset_club_name.argtypes = [V, I32]
         L.pf_dataset_club_name.restype = ctypes.c_char_p
+        L.pf_compute_normalizers.argtypes = [V, I32, I32, ctypes.c_char_p, V, V]
         L.pf_holdout_friends.argtypes = [V, V, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_recommendation_tests.argtypes = [V, V, I32, I32, V]
         _lib = L
@@ -305,6 +306,18 @@ class Dataset:
     def club_name(self, cid):
         c = self._L.pf_dataset_club_name(self.h, cid)
         return None if c is None else c.decode()
+
+    def compute_normalizers(self, sample_size, comps_per_user, save_csv=None):
+        """compute_column_normalizers (+ save_column_normalizers when save_csv): (mean, sd)
+        float arrays in pf_corpus_desc slot order (7 fields, then the text columns)."""
+        K = 7 + len(self.columns())
+        mean, sd = np.zeros(K, np.float32), np.zeros(K, np.float32)
+        rc = self._L.pf_compute_normalizers(self.h, sample_size, comps_per_user,
+                                            None if save_csv is None else os.fsencode(save_csv),
+                                            mean.ctypes.data, sd.ctypes.data)
+        if rc != PF_OK:
+            raise FasError(f"pf_compute_normalizers failed ({rc}): {self._L.pf_last_error(None).decode()}")
+        return mean, sd
 
     # -- hold-out drivers (A19); `eng` must be open on this dataset's desc
     def holdout_friends(self, eng, sample_size):

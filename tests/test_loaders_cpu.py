@@ -152,3 +152,26 @@ def test_loader_line_cap_and_edge_rows():
         assert list(desc_arrays(capped.desc_ptr())["user_id"]) == [5] and capped.info().lines_read == 3
     with pytest.raises(pf.FasError):
         pf.Dataset("/nonexistent/dir")
+
+
+@pytest.mark.parametrize("name", ["A", "B"])
+def test_compute_normalizers_matches_reference(name):
+    """compute_column_normalizers + save_column_normalizers (A18, the kurs path when
+    data/column_normalizers.csv is missing): float bits and the saved CSV text equal the
+    reference's (oracle/ref_norms.cpp goldens)."""
+    pf = tl.product()
+    sample, comps = tl.manifest()["norm_runs"][name]
+    ref_bits = {r.split()[0]: (int(r.split()[1], 16), int(r.split()[2], 16))
+                for r in tl.fixture_lines(name, "norms_computed_bits.txt")}
+    ref_csv = tl.fixture_lines(name, "norms_computed_csv.txt")
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir(name, d)
+        ds = pf.Dataset(d)
+        out = os.path.join(d, "saved.csv")
+        mean, sd = ds.compute_normalizers(sample, comps, out)
+        with open(out) as f:
+            got_csv = [ln.rstrip("\n") for ln in f]
+    keys = tl.FIXED_KEYS + ds.columns()
+    got = {keys[k]: (int(mean[k].view(np.uint32)), int(sd[k].view(np.uint32))) for k in range(len(keys))}
+    assert got == ref_bits
+    assert got_csv == ref_csv

@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
+                    help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,7 +114,10 @@ def main():
     eng = pf.FasEngine(desc, local)
     t2 = time.time()
     eng.set_shard(rank, world)
+    eng.set_scan_kernel({"auto": pf.PF_SCAN_AUTO, "stream": pf.PF_SCAN_STREAM, "postings": pf.PF_SCAN_POSTINGS}
+                        [args.scan_kernel])
     lay = eng.layout()
+    kernel_name = "fas_post_kernel" if lay.scan_kernel == pf.PF_SCAN_POSTINGS else "fas_scan_kernel"
     log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t2 - t1:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
         f"alg {lay.alg_bytes / 1e9:.3f} GB, packed={lay.packed_tokens}")
 
@@ -193,7 +198,7 @@ def main():
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "fas_scan_kernel", "avg_launch_ms": avg_launch_ms,
+                     "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "stream_bytes_per_launch": (lay.stream_bytes + lay.header_bytes) * shard_frac * Q},
         "topk_selfcheck": consistent,

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define PF_ABI_VERSION 1
+#define PF_ABI_VERSION 2
 
 /* status codes */
 #define PF_OK          0
@@ -180,6 +180,16 @@ int pf_set_adj(pf_ctx* ctx, int32_t uid, const int32_t* nbrs, int32_t n);
  * slots split by stream bytes); the multi-GPU path merges the per-shard top-k. */
 int pf_set_shard(pf_ctx* ctx, int32_t shard, int32_t nshards);
 
+/* All-candidates scan kernel.  PF_SCAN_AUTO (default) takes the postings scan
+ * (K5: per-token candidate lists, only the lists the query names are read) when the
+ * corpus fits its encoding, else the record-stream scan (K1: every candidate's record
+ * is walked).  Both give bit-identical results; forcing POSTINGS on a corpus outside
+ * its encoding returns PF_EUNSUPP. */
+#define PF_SCAN_AUTO     0
+#define PF_SCAN_STREAM   1
+#define PF_SCAN_POSTINGS 2
+int pf_set_scan_kernel(pf_ctx* ctx, int32_t kind);
+
 /*
  * Device-resident all-candidates scan for the multi-GPU bench: scores the
  * queries against this context's shard and writes, per query, `topk` packed
@@ -208,6 +218,9 @@ typedef struct pf_layout_stats {
     int64_t alg_bytes;        /* sum 32+4|clubs|+4|friends|+8nnz */
     int32_t packed_tokens;    /* 1 if tokens are stored as one word            */
     int32_t n_tiles;
+    int64_t post_bytes;       /* postings store: entries + norms + cells + headers (0 if absent) */
+    int32_t scan_kernel;      /* kernel the next all-candidates scan uses: PF_SCAN_STREAM / PF_SCAN_POSTINGS */
+    int32_t pad;
 } pf_layout_stats;
 int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
 

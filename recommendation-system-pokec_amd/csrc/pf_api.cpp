@@ -75,6 +75,14 @@ struct pf_ctx {
     // workspaces
     DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part;
     int32_t tile_begin = 0, tile_end = 0;
+    // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
+    pf::HostPost hp;
+    DBuf d_phdr, d_post, d_pnorm, d_cells;
+    pf::PostStore ps{};
+    int64_t post_bytes = 0;
+    int32_t wb_begin = 0, wb_end = 0;
+    int32_t scan_kind = PF_SCAN_AUTO;
+    bool use_post() const { return hp.ok && scan_kind != PF_SCAN_STREAM; }
     // pinned staging ring for the per-call query upload (a slot is reused only after
     // the copy that read it has completed)
     struct Stage {
@@ -271,9 +279,86 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 
 // All-candidates scan for `idx` (valid query indices) into d_keys rows `rows`.
 // One pinned staging buffer [refs | rows | image pool] goes up in a single async copy.
+// Timing events of one scan launch (the profiling pool when pf_profile_reset is on)
+int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
+    e0 = c->ev0;
+    e1 = c->ev1;
+    if (c->prof_on) {
+        if (c->prof_used == c->prof_ev.size()) {
+            hipEvent_t a, b;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b));
+            c->prof_ev.emplace_back(a, b);
+        }
+        e0 = c->prof_ev[c->prof_used].first;
+        e1 = c->prof_ev[c->prof_used].second;
+        ++c->prof_used;
+        timed = true;
+    }
+    return PF_OK;
+}
+
+// K5: the postings scan.  Staging: [image offsets | rows | sync | images].
+int scan_post(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
+              hipStream_t s, bool timed) {
+    const int nq = (int)idx.size();
+    std::vector<uint8_t> pool, img;
+    std::vector<uint32_t> offs;
+    std::vector<int32_t> excl;
+    int max_lists = 0, max_tok = 0;
+    for (int32_t i : idx) {
+        const int32_t u = c->hc.uid[i];
+        excl.clear();
+        auto it = c->hc.adj.find(u);
+        if (it != c->hc.adj.end()) excl = it->second;
+        excl.push_back(u);
+        pf::build_query_post(c->hc, c->hp, i, excl, img);
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(img.data() + sizeof(pf::QConst));
+        max_lists = std::max(max_lists, h->n_tok + h->n_club + h->n_friend);
+        max_tok = std::max(max_tok, h->n_tok);
+        offs.push_back((uint32_t)pool.size());
+        pool.insert(pool.end(), img.begin(), img.end());
+    }
+    const uint32_t wave_lds = pf::post_var_lds(max_tok, max_lists);
+    if (pf::post_lds(wave_lds) > 160u * 1024u) return c->fail(PF_EUNSUPP, "query names too many lists for one workgroup's LDS");
+    const int nwb = c->wb_end - c->wb_begin;
+    const int per_cu = pf::post_blocks_per_cu(wave_lds);
+    const int blocks = std::max(1, std::min(nwb, std::max(1, c->num_cus * per_cu / nq)));
+    const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
+    const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
+    const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
+    const size_t total = offs_b + rows_b + sync_b + pool.size();
+    uint8_t* h = c->stage_acquire(total);
+    if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
+    std::memcpy(h, offs.data(), (size_t)nq * 4);
+    std::memcpy(h + offs_b, rows.data(), (size_t)nq * 4);
+    std::memset(h + offs_b + rows_b, 0, sync_b);
+    std::memcpy(h + offs_b + rows_b + sync_b, pool.data(), pool.size());
+    HIPCHK(c, c->d_pool.ensure(total));
+    HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
+    HIPCHK(c, c->stage_release(s));
+    uint8_t* base = c->d_pool.as<uint8_t>();
+    HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
+    hipEvent_t e0, e1;
+    int rc = scan_events(c, timed, e0, e1);
+    if (rc != PF_OK) return rc;
+    if (timed) HIPCHK(c, hipEventRecord(e0, s));
+    HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
+                              nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
+                              reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
+                              reinterpret_cast<const int32_t*>(base + offs_b), s));
+    if (timed) {
+        HIPCHK(c, hipEventRecord(e1, s));
+        c->last_ev0 = e0;
+        c->last_ev1 = e1;
+    }
+    return PF_OK;
+}
+
 int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
              hipStream_t s, bool timed) {
     if (idx.empty()) return PF_OK;
+    if (c->use_post()) return scan_post(c, idx, rows, k, d_keys, s, timed);
     Images im;
     pf::QImageHost qi;
     std::vector<int32_t> excl;
@@ -311,19 +396,9 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     pf::ScanSync* d_sync = reinterpret_cast<pf::ScanSync*>(base + refs_b + rows_b);
     const uint8_t* d_images = base + refs_b + rows_b + sync_b;
     HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
-    hipEvent_t e0 = c->ev0, e1 = c->ev1;
-    if (c->prof_on) {
-        if (c->prof_used == c->prof_ev.size()) {
-            hipEvent_t a, b;
-            HIPCHK(c, hipEventCreate(&a));
-            HIPCHK(c, hipEventCreate(&b));
-            c->prof_ev.emplace_back(a, b);
-        }
-        e0 = c->prof_ev[c->prof_used].first;
-        e1 = c->prof_ev[c->prof_used].second;
-        ++c->prof_used;
-        timed = true;
-    }
+    hipEvent_t e0, e1;
+    int rc = scan_events(c, timed, e0, e1);
+    if (rc != PF_OK) return rc;
     if (timed) HIPCHK(c, hipEventRecord(e0, s));
     HIPCHK(c, pf::launch_scan(c->ds, d_images, d_refs, im.max_lds, im.gtab, nq, c->tile_begin, c->tile_end, k, blocks,
                               c->d_part.as<uint64_t>(), d_sync, d_keys, d_rows, s));
@@ -370,6 +445,13 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     if (rc != PF_OK) return bail(rc);
     rc = pf::build_store(c->hc, c->hs, c->err);
     if (rc != PF_OK) return bail(rc);
+    pf::build_postings(c->hc, c->hp);  // hp.ok = false: the stream scan serves every query
+    // PF_SCAN=stream|postings sets the context's initial scan kernel (tests force variants
+    // per process with it); pf_set_scan_kernel changes it later
+    if (const char* sk = getenv("PF_SCAN")) {
+        if (!strcmp(sk, "stream")) c->scan_kind = PF_SCAN_STREAM;
+        else if (!strcmp(sk, "postings") && c->hp.ok) c->scan_kind = PF_SCAN_POSTINGS;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         c->err = "stream/event creation failed";
@@ -388,6 +470,13 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     if (e == hipSuccess) e = upload(c, c->d_hdr0, hs.hdr0);
     if (e == hipSuccess) e = upload(c, c->d_hdr1, hs.hdr1);
     if (e == hipSuccess) e = upload(c, c->d_hdr2, hs.hdr2);
+    if (c->hp.ok) {
+        auto& hp = c->hp;
+        if (e == hipSuccess) e = upload(c, c->d_phdr, hp.hdr);
+        if (e == hipSuccess) e = upload(c, c->d_post, hp.post);
+        if (e == hipSuccess) e = upload(c, c->d_pnorm, hp.pnorm);
+        if (e == hipSuccess) e = upload(c, c->d_cells, hp.cells);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         c->hip_fail(e, "corpus upload");
@@ -414,6 +503,23 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     c->ds.n_cols = c->hc.T;
     c->tile_begin = 0;
     c->tile_end = c->ds.n_tiles;
+    if (c->hp.ok) {
+        auto& hp = c->hp;
+        c->post_bytes = (int64_t)hp.hdr.size() * 16 + (int64_t)hp.post.size() * 4 + (int64_t)hp.pnorm.size() * 8 +
+                        (int64_t)hp.cells.size() * 4;
+        std::vector<uint4>().swap(hp.hdr);
+        std::vector<uint32_t>().swap(hp.post);
+        std::vector<double>().swap(hp.pnorm);
+        std::vector<uint32_t>().swap(hp.cells);
+        c->ps.hdr = c->d_phdr.as<uint4>();
+        c->ps.post = c->d_post.as<uint32_t>();
+        c->ps.pnorm = c->d_pnorm.as<double>();
+        c->ps.cells = c->d_cells.as<uint32_t>();
+        c->ps.n = c->hc.n;
+        c->ps.n_blocks = (c->hc.n + pf::kBlockCands - 1) / pf::kBlockCands;
+        c->wb_begin = 0;
+        c->wb_end = c->ps.n_blocks;
+    }
     *out = c;
     return PF_OK;
 }
@@ -732,6 +838,17 @@ int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {
     };
     c->tile_begin = bound(shard);
     c->tile_end = bound(shard + 1);
+    // postings scan: contiguous block ranges of equal candidate count
+    const int64_t nwb = c->ps.n_blocks;
+    c->wb_begin = (int32_t)(nwb * shard / nshards);
+    c->wb_end = (int32_t)(nwb * (shard + 1) / nshards);
+    return PF_OK;
+}
+
+int pf_set_scan_kernel(pf_ctx* c, int32_t kind) {
+    if (!c || kind < PF_SCAN_AUTO || kind > PF_SCAN_POSTINGS) return PF_EINVAL;
+    if (kind == PF_SCAN_POSTINGS && !c->hp.ok) return c->fail(PF_EUNSUPP, "postings store unavailable: " + c->hp.why);
+    c->scan_kind = kind;
     return PF_OK;
 }
 
@@ -777,6 +894,9 @@ int pf_layout(const pf_ctx* c, pf_layout_stats* o) {
     o->alg_bytes = c->hs.alg_bytes;
     o->packed_tokens = c->hs.packed ? 1 : 0;
     o->n_tiles = (int32_t)c->hs.tile_steps.size();
+    o->post_bytes = c->post_bytes;
+    o->scan_kernel = c->use_post() ? PF_SCAN_POSTINGS : PF_SCAN_STREAM;
+    o->pad = 0;
     return PF_OK;
 }
 

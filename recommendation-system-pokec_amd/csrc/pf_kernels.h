@@ -20,6 +20,14 @@ hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef*
                        uint64_t* out, const int32_t* out_rows, hipStream_t s);
 // resident scan blocks per CU at this dynamic LDS size (HIP occupancy API)
 int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds);
+// K5 postings scan over candidate blocks [blk_begin, blk_end) for nq query images (byte
+// offsets img_off[] into pool); var_lds = post_var_lds(max n_tok, max lists of an image)
+uint32_t post_var_lds(int n_tok, int n_lists);
+uint32_t post_lds(uint32_t var_lds);
+hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
+                       int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
+                       const int32_t* out_rows, hipStream_t s);
+int post_blocks_per_cu(uint32_t var_lds);
 // plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
                         uint64_t* out, hipStream_t s);

@@ -564,94 +564,15 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool PACKED, bool GTAB>
-__global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
-                                                                const QImageRef* __restrict__ refs, int32_t tile_begin,
-                                                                int32_t tile_end, int32_t k,
-                                                                uint64_t* __restrict__ parts,
-                                                                ScanSync* __restrict__ sync,
-                                                                uint64_t* __restrict__ out,
-                                                                const int32_t* __restrict__ out_rows) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const QImageRef r = refs[blockIdx.y];
-    char* scratch;
-    const QView v = stage_query<GTAB>(smem, pool, r, &scratch);
+// Block-level end of a scan: merge the 4 wave lists, publish the block's k-list and, in
+// the last block of the query, merge every block's list into out[row] (no second launch).
+// sc: LDS >= 4 * k keys; misc: LDS >= 16 + 4 * kMaxTopK bytes (both idle by now).
+__device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
+                                          uint64_t* __restrict__ parts, uint64_t* __restrict__ out,
+                                          const int32_t* __restrict__ out_rows) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t list = ~0ull;
-    // Tile hand-out, longest tiles first.  Static zig-zag for all but the last two bands
-    // (band b = tiles [b*W, (b+1)*W) holds W near-equal tiles; wave w takes one per band,
-    // alternating direction), then the tail from per-XCD counters, so waves that drew
-    // cheap tiles (few hits) take more.  One shared counter for every tile serialises at
-    // ~13 ns per fetch and halved the streaming rate; per-XCD counters on the last
-    // bands only keep the fetches few and uncontended.
-    const int W = (int)gridDim.x * (kScanThreads / 64), wid = (int)blockIdx.x * (kScanThreads / 64) + wave;
-    const int ntiles = tile_end - tile_begin;
-    const int nstatic = max(0, ntiles / W - 2) * W;
-    // blocks are dispatched to the 8 XCDs round-robin; with fewer than 8 blocks every
-    // group still has one, so every residue class of the tail is drained
-    const int ngrp = min(8, (int)gridDim.x), xcd = (int)blockIdx.x % ngrp;
-    unsigned* xctr = &sync[blockIdx.y].xcd_next[xcd * 16];
-    for (int b = 0;; ++b) {
-        int tile;
-        if (b * W < nstatic) {
-            tile = tile_begin + b * W + ((b & 1) ? W - 1 - wid : wid);
-        } else {
-            unsigned t = 0;
-            if (lane == 0) t = atomicAdd(xctr, 1u);
-            t = __builtin_amdgcn_readfirstlane(t);
-            tile = tile_begin + nstatic + (int)t * ngrp + xcd;  // group x drains tail tiles = x (mod ngrp)
-        }
-        if (tile >= tile_end) break;
-        const uint32_t lgk = st.tile_lgk[tile];
-        const int slot0 = (int)st.tile_slot0[tile];
-        const int cand = lane >> lgk, ci = lane & ((1 << lgk) - 1);
-        const bool active = cand < min(kTileSlots >> lgk, st.n_slots - slot0);
-        const int p = slot0 + cand;
-        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-        if (active) {
-            h0 = st.hdr0[p];
-            h1 = st.hdr1[p];
-            h2 = st.hdr2[p];
-        }
-        const uint32_t nc = h2.y, nset = h2.y + h2.z;
-        const uint32_t len = record_words(h2, PACKED);
-        const uint32_t q = chunk_words(len, lgk, PACKED);
-        const uint32_t j0 = (uint32_t)ci * q;
-        const uint32_t clen = (active && len > j0) ? min(q, len - j0) : 0u;
-        const Loc l{tile, cand, lgk};
-        Walk W;
-        W.cnt = 0; W.nh = 0; W.pend = 0;
-        if (!PACKED && clen > 0 && j0 > 0) W.pend = word_at(st, l, q, j0 - 1);  // a token pair may straddle chunks
-        walk_chunk<PACKED, false>(W, st.stream + st.tile_off[tile] + lane, j0, clen, nc, nset, v, blockDim.x);
-        float f = 0.0f;
-        if (lgk == 0) {
-            if (active) {
-                const uint32_t nh = W.nh;
-                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
-            }
-        } else {
-            // a split record: sum the chunk counters over its lanes, publish the hit counts,
-            // and let the record's first lane finish it
-            uint32_t cnt = W.cnt;
-            for (int m = 1; m < (1 << lgk); m <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, m);
-            v.nh[threadIdx.x] = W.nh;
-            __builtin_amdgcn_wave_barrier();
-            if (active && ci == 0) {
-                const uint32_t* nhp = v.nh + threadIdx.x;
-                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
-                                         [&](uint32_t g) { return nhp[g]; });
-            }
-        }
-        uint64_t key = ~0ull;
-        if (active && ci == 0) {
-            const int32_t uid = (int32_t)h1.w;
-            if (!excluded<PACKED>(v, (uint32_t)uid)) key = score_key(f, uid);
-        }
-        topk_push(list, key, k, lane);
-    }
     // block merge: the 4 wave lists are packed densely (k keys each) and wave 0 takes
     // them 64 at a time, so 4*k <= 64 keys cost a single push
-    uint64_t* sc = reinterpret_cast<uint64_t*>(scratch);
     __syncthreads();
     if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
@@ -662,7 +583,7 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
     ScanSync* sy = sync + blockIdx.y;
     uint64_t* qparts = parts + (size_t)blockIdx.y * gridDim.x * k;
     // tail scratch in the (now idle) hit lists: flag, threshold, block count, block ids
-    int* s_flag = reinterpret_cast<int*>(v.hits);
+    int* s_flag = misc;
     int* s_cnt = s_flag + 1;
     uint64_t* s_T = reinterpret_cast<uint64_t*>(s_flag + 2);
     int* s_blk = s_flag + 4;
@@ -769,6 +690,364 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
     }
 }
 
+template <bool PACKED, bool GTAB>
+__global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, const uint8_t* __restrict__ pool,
+                                                                const QImageRef* __restrict__ refs, int32_t tile_begin,
+                                                                int32_t tile_end, int32_t k,
+                                                                uint64_t* __restrict__ parts,
+                                                                ScanSync* __restrict__ sync,
+                                                                uint64_t* __restrict__ out,
+                                                                const int32_t* __restrict__ out_rows) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const QImageRef r = refs[blockIdx.y];
+    char* scratch;
+    const QView v = stage_query<GTAB>(smem, pool, r, &scratch);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t list = ~0ull;
+    // Tile hand-out, longest tiles first.  Static zig-zag for all but the last two bands
+    // (band b = tiles [b*W, (b+1)*W) holds W near-equal tiles; wave w takes one per band,
+    // alternating direction), then the tail from per-XCD counters, so waves that drew
+    // cheap tiles (few hits) take more.  One shared counter for every tile serialises at
+    // ~13 ns per fetch and halved the streaming rate; per-XCD counters on the last
+    // bands only keep the fetches few and uncontended.
+    const int W = (int)gridDim.x * (kScanThreads / 64), wid = (int)blockIdx.x * (kScanThreads / 64) + wave;
+    const int ntiles = tile_end - tile_begin;
+    const int nstatic = max(0, ntiles / W - 2) * W;
+    // blocks are dispatched to the 8 XCDs round-robin; with fewer than 8 blocks every
+    // group still has one, so every residue class of the tail is drained
+    const int ngrp = min(8, (int)gridDim.x), xcd = (int)blockIdx.x % ngrp;
+    unsigned* xctr = &sync[blockIdx.y].xcd_next[xcd * 16];
+    for (int b = 0;; ++b) {
+        int tile;
+        if (b * W < nstatic) {
+            tile = tile_begin + b * W + ((b & 1) ? W - 1 - wid : wid);
+        } else {
+            unsigned t = 0;
+            if (lane == 0) t = atomicAdd(xctr, 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            tile = tile_begin + nstatic + (int)t * ngrp + xcd;  // group x drains tail tiles = x (mod ngrp)
+        }
+        if (tile >= tile_end) break;
+        const uint32_t lgk = st.tile_lgk[tile];
+        const int slot0 = (int)st.tile_slot0[tile];
+        const int cand = lane >> lgk, ci = lane & ((1 << lgk) - 1);
+        const bool active = cand < min(kTileSlots >> lgk, st.n_slots - slot0);
+        const int p = slot0 + cand;
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
+        if (active) {
+            h0 = st.hdr0[p];
+            h1 = st.hdr1[p];
+            h2 = st.hdr2[p];
+        }
+        const uint32_t nc = h2.y, nset = h2.y + h2.z;
+        const uint32_t len = record_words(h2, PACKED);
+        const uint32_t q = chunk_words(len, lgk, PACKED);
+        const uint32_t j0 = (uint32_t)ci * q;
+        const uint32_t clen = (active && len > j0) ? min(q, len - j0) : 0u;
+        const Loc l{tile, cand, lgk};
+        Walk W;
+        W.cnt = 0; W.nh = 0; W.pend = 0;
+        if (!PACKED && clen > 0 && j0 > 0) W.pend = word_at(st, l, q, j0 - 1);  // a token pair may straddle chunks
+        walk_chunk<PACKED, false>(W, st.stream + st.tile_off[tile] + lane, j0, clen, nc, nset, v, blockDim.x);
+        float f = 0.0f;
+        if (lgk == 0) {
+            if (active) {
+                const uint32_t nh = W.nh;
+                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+            }
+        } else {
+            // a split record: sum the chunk counters over its lanes, publish the hit counts,
+            // and let the record's first lane finish it
+            uint32_t cnt = W.cnt;
+            for (int m = 1; m < (1 << lgk); m <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, m);
+            v.nh[threadIdx.x] = W.nh;
+            __builtin_amdgcn_wave_barrier();
+            if (active && ci == 0) {
+                const uint32_t* nhp = v.nh + threadIdx.x;
+                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
+                                         [&](uint32_t g) { return nhp[g]; });
+            }
+        }
+        uint64_t key = ~0ull;
+        if (active && ci == 0) {
+            const int32_t uid = (int32_t)h1.w;
+            if (!excluded<PACKED>(v, (uint32_t)uid)) key = score_key(f, uid);
+        }
+        topk_push(list, key, k, lane);
+    }
+    scan_tail(list, k, reinterpret_cast<uint64_t*>(scratch), reinterpret_cast<int*>(v.hits), sync, parts, out,
+              out_rows);
+}
+
+// ---------------------------------------------------------------- K5: postings scan
+// All-candidates FAS (A13) through the postings store (pf_types.h): a workgroup scores one
+// block of 1024 consecutive candidates at a time (thread i owns candidates i + 256 kk)
+// from the lists the query names, never the candidates' records:
+//   1. ranges: every list's sub-range for this block (one cell lookup per list);
+//   2. sets: club / friend list entries add their multiplicity to per-candidate LDS
+//      counters (integer, order-free) and the exclusion list marks adj[q] + {q};
+//   3. fixed terms (public .. friends) per owned candidate from its 32-B header;
+//   4. text, one active query column at a time in ascending order: the column's token
+//      lists (<= 8 tokens per pass) write each hit's tf byte at [candidate][token] and its
+//      (candidate, column) norm; the hit candidates are compacted, and their dot (ascending
+//      tid: token order) and cosine -> sigmoid term are computed densely, one candidate per
+//      thread, so the FP64 divisions and exp never run on idle lanes; the owners then add
+//      the column's term, or the s = 0 term of a common column without hits, in the
+//      reference's order (recommender_similarity.cpp:38-113).
+// LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
+// (later the compacted list) | exclusion bits u32[32] | misc u32[4] | QVal[n_tok] |
+// ranges uint2[n_lists].  The tail merge reuses the tf-byte array.
+constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + 128 + 16;
+
+__device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0) {
+    const uint32_t cell = c0 >> L.shift;
+    return make_uint2(L.off + ps.cells[L.cell_off + cell], L.off + ps.cells[L.cell_off + cell + 1]);
+}
+
+// Flattened walk over the entries of lists rng[0 .. nl): thread i takes flat entries
+// i + 256u (u < 2) of every 512-entry group, loads them (and, for token lists, their norms)
+// together, then calls f(list, entry, norm) for each.
+template <bool NORMS, class F>
+__device__ __forceinline__ void walk_lists(const PostStore& ps, const uint2* rng, int nl, F f) {
+    constexpr int U = 2;
+    uint32_t total = 0;
+    for (int j = 0; j < nl; ++j) total += rng[j].y - rng[j].x;
+    for (uint32_t f0 = 0; f0 < total; f0 += U * kPostThreads) {
+        int js[U];
+        uint32_t xs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { js[u] = -1; xs[u] = 0; }
+        uint32_t pre = 0;
+        for (int j = 0; j < nl && pre < f0 + U * kPostThreads; ++j) {
+            const uint2 r = rng[j];
+            const uint32_t len = r.y - r.x;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
+                if (fl - pre < len) { js[u] = j; xs[u] = r.x + (fl - pre); }
+            }
+            pre += len;
+        }
+        uint32_t ent[U];
+        double nv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ent[u] = js[u] >= 0 ? ps.post[xs[u]] : 0u;
+            nv[u] = (NORMS && js[u] >= 0) ? ps.pnorm[xs[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (js[u] >= 0) f(js[u], ent[u], nv[u]);
+    }
+}
+
+__global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
+                                                              const uint32_t* __restrict__ img_off, int32_t blk_begin,
+                                                              int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
+                                                              ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
+                                                              const int32_t* __restrict__ out_rows) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint8_t* img = pool + img_off[blockIdx.y];
+    const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
+    const QTok* toks = reinterpret_cast<const QTok*>(img + H.tok_off);
+    const QCol* cols = reinterpret_cast<const QCol*>(img + H.col_off);
+    const PList* sets = reinterpret_cast<const PList*>(img + H.set_off);
+    const uint32_t* excl = reinterpret_cast<const uint32_t*>(img + H.excl_off);
+    const int tid = (int)threadIdx.x, lane = tid & 63;
+    char* base = smem + sizeof(QConst);
+    uint64_t* tfv = reinterpret_cast<uint64_t*>(base);
+    uint8_t* tfb = reinterpret_cast<uint8_t*>(base);
+    double* nrm = reinterpret_cast<double*>(base + kBlockCands * 8);
+    double* term = reinterpret_cast<double*>(base + kBlockCands * 16);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kBlockCands * 24);
+    uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
+    uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
+    uint32_t* nlist = exb + 32;
+    QVal* qv = reinterpret_cast<QVal*>(base + kPostFixedLds);
+    uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + 16 * H.n_tok);
+    const int nsets = H.n_club + H.n_friend;
+    const int nl = H.n_tok + nsets;
+    stage(smem, img, sizeof(QConst));
+    for (int j = tid; j < H.n_tok; j += kPostThreads) {
+        QVal v;
+        v.wq = toks[j].wq;
+        v.idf = toks[j].idf;
+        qv[j] = v;
+    }
+#pragma unroll
+    for (int kk = 0; kk < kCandsPerThread; ++kk) tfv[kk * kPostThreads + tid] = 0ull;
+    if (tid == 0) *nlist = 0u;
+    const QConst& q = *reinterpret_cast<const QConst*>(smem);
+    uint64_t best = ~0ull;
+    for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end; blk += (int)gridDim.x) {
+        const uint32_t c0 = (uint32_t)blk * kBlockCands;
+        // 1. ranges of every list in this block; headers of the owned candidates
+        for (int j = tid; j < nl; j += kPostThreads)
+            rng[j] = list_range(ps, j < H.n_tok ? toks[j].l : sets[j - H.n_tok], c0);
+        uint4 ha[kCandsPerThread], hb[kCandsPerThread];
+#pragma unroll
+        for (int kk = 0; kk < kCandsPerThread; ++kk) {
+            const uint32_t c = c0 + kk * kPostThreads + tid;
+            const bool a = c < (uint32_t)ps.n;
+            ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
+            hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
+            cnt[kk * kPostThreads + tid] = 0u;
+        }
+        if (tid < 32) exb[tid] = 0u;
+        __syncthreads();
+        // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
+        {
+            uint32_t lo = 0, hi = (uint32_t)H.n_excl;
+            if (hi > kPostThreads) {
+                while (lo < hi) {  // first entry >= c0
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (excl[mid] < c0) lo = mid + 1; else hi = mid;
+                }
+                hi = (uint32_t)H.n_excl;
+            }
+            for (uint32_t b = lo; b < hi; b += kPostThreads) {
+                const uint32_t x = b + tid;
+                const uint32_t e = x < hi ? excl[x] : ~0u;
+                const uint32_t p = e - c0;
+                if (p < (uint32_t)kBlockCands) atomicOr(&exb[p >> 5], 1u << (p & 31));
+                if (__syncthreads_or(e >= c0 + kBlockCands)) break;  // sorted: the rest lies beyond the block
+            }
+        }
+        // 2. clubs / friends
+        walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
+            const uint32_t p = (e >> 8) - c0;
+            if (p < (uint32_t)kBlockCands) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
+        });
+        __syncthreads();
+        // 3. fixed terms, recommender_similarity.cpp:38-91
+        double sum[kCandsPerThread];
+        int used[kCandsPerThread];
+        uint64_t pend[kCandsPerThread];
+        uint32_t skip = 0;  // bit kk: candidate kk absent or excluded
+#pragma unroll
+        for (int kk = 0; kk < kCandsPerThread; ++kk) {
+            const int p = kk * kPostThreads + tid;
+            const uint32_t ct = cnt[p];
+            if (c0 + p >= (uint32_t)ps.n || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
+            const uint64_t cm = (uint64_t)ha[kk].x | ((uint64_t)(ha[kk].y & 0xFFFFu) << 32);
+            pend[kk] = cm & q.colmask;
+            double s = 0.0;
+            int u = 0;
+            const uint32_t pb = (ha[kk].y >> 16) & 0xFFu, gb = ha[kk].y >> 24;
+            if (q.pubcode != kCodeMissing && pb != kCodeMissing) { s += q.sig_pub[pb == q.pubcode]; ++u; }
+            if (q.gencode != kCodeMissing && gb != kCodeMissing) { s += q.sig_gen[gb == q.gencode]; ++u; }
+            const int cb = (int)(int16_t)(ha[kk].z & 0xFFFFu), ab = (int)(int16_t)(ha[kk].z >> 16);
+            if (q.comp > 0 && cb > 0) { s += cb <= kValTab ? q.sig_comp[cb] : ratio_term(q, PF_F_COMPLETION, q.comp, cb); ++u; }
+            if (q.age > 0 && ab > 0) { s += ab <= kValTab ? q.sig_age[ab] : ratio_term(q, PF_F_AGE, q.age, ab); ++u; }
+            const int r0 = (int)hb[kk].x, r1 = (int)hb[kk].y, r2 = (int)hb[kk].z;
+            const int bcnt = (r0 >= 0) + (r1 >= 0) + (r2 >= 0);
+            if (q.a_regcnt > 0 && bcnt > 0) {
+                const int m = (r0 >= 0 && r0 == q.reg[0]) + (r1 >= 0 && r1 == q.reg[1]) + (r2 >= 0 && r2 == q.reg[2]);
+                s += q.sig_reg[bcnt][m];
+                ++u;
+            }
+            const uint32_t nc = ha[kk].w & 0xFFFFu, nf = ha[kk].w >> 16;
+            const int ic = (int)(ct & 0xFFFFu), ifr = (int)(ct >> 16);
+            if (q.n_clubs > 0 && nc > 0) { s += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs); ++u; }
+            if (q.n_friends > 0 && nf > 0) { s += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends); ++u; }
+            sum[kk] = s;
+            used[kk] = u + __popcll(pend[kk]);
+        }
+        __syncthreads();  // the counters' LDS now holds the compacted lists
+        // 4. text columns, ascending
+        for (int ci = 0; ci < H.n_act; ++ci) {
+            const QCol col = cols[ci];
+            const int t = col.t;
+            uint32_t colhit = 0;  // bit kk: owned candidate kk has a hit in column t
+            // a column of more than kChunkToks tokens carries its dot in term[] across passes
+            const bool multi = col.j1 - col.j0 > kChunkToks;
+            if (multi) {
+#pragma unroll
+                for (int kk = 0; kk < kCandsPerThread; ++kk) term[kk * kPostThreads + tid] = 0.0;
+            }
+            for (int js = col.j0; js < col.j1; js += kChunkToks) {
+                const int nj = min(kChunkToks, col.j1 - js);
+                const bool last = js + kChunkToks >= col.j1;
+                walk_lists<true>(ps, rng + js, nj, [&](int j, uint32_t e, double nv) {
+                    const uint32_t p = (e >> 8) - c0;
+                    if (p < (uint32_t)kBlockCands) {
+                        tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
+                        nrm[p] = nv;
+                    }
+                });
+                __syncthreads();
+#pragma unroll
+                for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                    const int p = kk * kPostThreads + tid;
+                    if (tfv[p] != 0ull) colhit |= 1u << kk;
+                    const bool h = (colhit >> kk) & 1u;
+                    const uint64_t m = __ballot(h);
+                    if (m) {
+                        uint32_t b0 = 0;
+                        if (lane == 0) b0 = atomicAdd(nlist, (uint32_t)__popcll(m));
+                        b0 = __builtin_amdgcn_readfirstlane(b0);
+                        if (h) list[b0 + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                    }
+                }
+                __syncthreads();
+                const uint32_t n = *nlist;
+                for (uint32_t i = tid; i < n; i += kPostThreads) {
+                    const int p = list[i];
+                    const uint64_t v = tfv[p];
+                    tfv[p] = 0ull;
+                    double dot = multi ? term[p] : 0.0;
+                    for (int j = 0; j < nj; ++j) {
+                        const uint32_t tf = (uint32_t)(v >> (8 * j)) & 0xFFu;
+                        if (tf) {
+                            const QVal w = qv[js + j];
+                            dot += w.wq * ((double)tf * w.idf);
+                        }
+                    }
+                    term[p] = !last ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
+                }
+                __syncthreads();
+                if (tid == 0) *nlist = 0u;
+            }
+#pragma unroll
+            for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                uint64_t below = pend[kk] & ((1ull << t) - 1ull);
+                pend[kk] &= ~below;
+                while (below) {
+                    const int c = __ffsll((unsigned long long)below) - 1;
+                    below &= below - 1;
+                    sum[kk] += q.sig0_col[c];
+                }
+                if ((pend[kk] >> t) & 1ull) {
+                    sum[kk] += ((colhit >> kk) & 1u) ? term[kk * kPostThreads + tid] : q.sig0_col[t];
+                    pend[kk] &= ~(1ull << t);
+                }
+            }
+        }
+        // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
+#pragma unroll
+        for (int kk = 0; kk < kCandsPerThread; ++kk) {
+            while (pend[kk]) {
+                const int c = __ffsll((unsigned long long)pend[kk]) - 1;
+                pend[kk] &= pend[kk] - 1;
+                sum[kk] += q.sig0_col[c];
+            }
+            uint64_t key = ~0ull;
+            if (!((skip >> kk) & 1u)) {
+                float f = 0.0f;
+                if (used[kk] > 0) {
+                    const double S = sum[kk] / (double)used[kk];
+                    const double F = (double)used[kk] / (double)(kNumFixed + q.n_cols);
+                    f = (S <= 0.0 && F <= 0.0) ? 0.0f : (float)((2.0 * S * F) / (S + F));
+                }
+                key = score_key(f, (int32_t)hb[kk].w);
+            }
+            topk_push(best, key, k, lane);
+        }
+    }
+    // tail scratch in the (idle) tf-byte array: merge keys, then flag / threshold / block ids
+    scan_tail(best, k, tfv, reinterpret_cast<int*>(tfv + 4 * kMaxTopK), sync, parts, out, out_rows);
+}
+
 // ---------------------------------------------------------------- K2: merge
 // Key lists in[part * part_stride + q * query_stride + j] (j < k) -> out[q * k + j]
 // (the cross-shard merge after the all-gather; one block per query, every wave pushes
@@ -866,6 +1145,30 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
     else e = gtab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<false, true>, kScanThreads, lds)
                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_scan_kernel<false, false>, kScanThreads, lds);
     last_key = key;
+    last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    return last_nb;
+}
+
+// K5 dynamic LDS: QConst | fixed per-block arrays | QVal[n_tok] | ranges[n_lists]
+uint32_t post_var_lds(int n_tok, int n_lists) { return (uint32_t)(16 * n_tok + 8 * n_lists); }
+uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
+
+hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
+                       int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
+                       const int32_t* out_rows, hipStream_t s) {
+    if (nq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool, img_off,
+                       blk_begin, blk_end, k, parts, sync, out, out_rows);
+    return hipGetLastError();
+}
+
+int post_blocks_per_cu(uint32_t var_lds) {
+    static thread_local uint32_t last_key = ~0u;
+    static thread_local int last_nb = 1;
+    if (var_lds == last_key) return last_nb;
+    int nb = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel, kPostThreads, post_lds(var_lds));
+    last_key = var_lds;
     last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
     return last_nb;
 }

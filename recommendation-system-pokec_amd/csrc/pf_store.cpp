@@ -367,9 +367,10 @@ int lg_for(size_t n) {
 
 }  // namespace
 
-bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
+// The A side's constants: normaliser modes, glibc-exp sigmoid tables, s = 0 terms,
+// column mask and sqrt(na) per column (recommender_similarity.cpp:10-124).
+static void fill_qconst(const HostCorpus& hc, int32_t i, QConst& c) {
     const int T = hc.T;
-    QConst& c = out.c;
     std::memset(&c, 0, sizeof c);
     c.n_cols = T;
     // normaliser parameters: z = (s-mean)/sd when the key exists and sd > 0, else 6(s-0.5)
@@ -416,6 +417,19 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
     }
     c.sig0_clubs = term(PF_F_CLUBS, 0.0);
     c.sig0_friends = term(PF_F_FRIENDS, 0.0);
+    c.colmask = 0;
+    for (int t = 0; t < T; ++t) {
+        const size_t r = (size_t)i * T + t;
+        c.sig0_col[t] = term(kNumFixed + t, 0.0);
+        c.sqrt_na[t] = hc.sqrt_nb[r];
+        if (hc.tok_off[r + 1] != hc.tok_off[r]) c.colmask |= 1ull << t;
+    }
+}
+
+bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
+    const int T = hc.T;
+    QConst& c = out.c;
+    fill_qconst(hc, i, c);
     // hash items: distinct clubs (T0), distinct friends (T1), (column, token) weights (T2),
     // exclusions (T3); packed corpora merge T0..T2 into one tagged table (pf_types.h)
     std::vector<uint64_t> items[4];
@@ -428,13 +442,9 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
     tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
     for (uint32_t x : tmp) items[1].push_back(packed ? make_entry(x, 0x10000u) : make_entry(x, 0));
     out.vals.clear();
-    c.colmask = 0;
     for (int t = 0; t < T; ++t) {
         const size_t r = (size_t)i * T + t;
-        c.sig0_col[t] = term(kNumFixed + t, 0.0);
-        c.sqrt_na[t] = hc.sqrt_nb[r];
         if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
-        c.colmask |= 1ull << t;
         for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
             const double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;  // recommender.cpp:78
             QVal v;
@@ -487,6 +497,257 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
         }
     }
     return false;
+}
+
+}  // namespace pf
+
+// ---------------------------------------------------------------- postings store (K5)
+namespace pf {
+
+namespace {
+
+// LSD radix sort of 64-bit keys on their low `bits` bits (16-bit digits)
+void radix_sort_u64(std::vector<uint64_t>& a, int bits) {
+    std::vector<uint64_t> b(a.size());
+    for (int sh = 0; sh < bits; sh += 16) {
+        std::vector<size_t> cnt(65537, 0);
+        for (uint64_t x : a) ++cnt[((x >> sh) & 0xFFFF) + 1];
+        for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
+        for (uint64_t x : a) b[cnt[(x >> sh) & 0xFFFF]++] = x;
+        a.swap(b);
+    }
+}
+
+// cell width 2^shift: the smallest >= one wave block holding ~<= 32 of the list's entries
+uint32_t list_shift(uint64_t len, int32_t n) {
+    uint32_t s = kPostMinShift;
+    while (s < 30 && (len << (s + 1)) <= 32ull * (uint64_t)n) ++s;
+    return s;
+}
+
+}  // namespace
+
+void build_postings(const HostCorpus& hc, HostPost& hp) {
+    const int32_t n = hc.n, T = hc.T;
+    hp.ok = false;
+    auto bail = [&](const char* w) {
+        hp.why = w;
+        hp.hdr.clear(); hp.post.clear(); hp.pnorm.clear(); hp.cells.clear(); hp.lists.clear(); hp.tok_list.clear();
+        hp.club_list.clear(); hp.friend_list.clear();
+    };
+    if (n <= 0) return bail("empty corpus");
+    if ((uint32_t)n >= kPostIdxLimit) return bail("more than 2^24 candidates");
+    if (T > kPostMaxCols) return bail("more than 48 text columns");
+    for (int32_t i = 0; i < n; ++i) {
+        if (hc.comp[i] < -32768 || hc.comp[i] > 32767 || hc.age[i] < -32768 || hc.age[i] > 32767)
+            return bail("completion / age outside 16 bits");
+        if (hc.club_off[i + 1] - hc.club_off[i] > 0xFFFF || hc.friend_off[i + 1] - hc.friend_off[i] > 0xFFFF)
+            return bail("more than 65535 clubs or friends");
+    }
+    for (size_t k = 0; k < hc.tid.size(); ++k)
+        if (hc.tid[k] < 0 || hc.tid[k] >= (1 << 22) || hc.tf[k] < 0 || hc.tf[k] > 255)
+            return bail("token id / count outside the packed encoding");
+    // ---- token lists: (column, tid) ascending; entries idx << 8 | tf, tf > 0 only (a tf = 0
+    // token adds +0 to a dot and never decides a hit: recommender.cpp:74-85)
+    hp.tok_list.assign(T, {});
+    std::vector<std::vector<uint32_t>> cnt(T);
+    {
+        std::vector<std::thread> ts;
+        for (int t = 0; t < T; ++t)
+            ts.emplace_back([&, t]() {
+                int32_t mx = -1;
+                for (int32_t i = 0; i < n; ++i)
+                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
+                        mx = std::max(mx, hc.tid[k]);
+                cnt[t].assign((size_t)mx + 1, 0u);
+                for (int32_t i = 0; i < n; ++i)
+                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
+                        if (hc.tf[k] > 0) ++cnt[t][hc.tid[k]];
+            });
+        for (auto& x : ts) x.join();
+    }
+    uint64_t off = 0;
+    std::vector<uint64_t> col_off(T + 1, 0);
+    for (int t = 0; t < T; ++t) {
+        col_off[t] = off;
+        hp.tok_list[t].assign(cnt[t].size(), -1);
+        for (size_t tid = 0; tid < cnt[t].size(); ++tid) {
+            if (!cnt[t][tid]) continue;
+            hp.tok_list[t][tid] = (int32_t)hp.lists.size();
+            hp.lists.push_back(PList{(uint32_t)off, 0u, 0u, cnt[t][tid]});
+            off += cnt[t][tid];
+            if (off >= (1ull << 32)) return bail("more than 2^32 postings");
+        }
+    }
+    col_off[T] = off;
+    hp.tok_entries = (int64_t)off;
+    // ---- set lists: entries idx << 8 | multiplicity (recommender.cpp:119-128 counts B's
+    // duplicates); one list per distinct club / friend id
+    std::vector<uint64_t> ckeys, fkeys;
+    std::vector<uint32_t> tmp;
+    auto collect = [&](const std::vector<int64_t>& o, const std::vector<uint32_t>& ids, std::vector<uint64_t>& keys) -> bool {
+        for (int32_t i = 0; i < n; ++i) {
+            tmp.assign(ids.begin() + o[i], ids.begin() + o[i + 1]);
+            std::sort(tmp.begin(), tmp.end());
+            for (size_t a = 0; a < tmp.size();) {
+                size_t b = a;
+                while (b < tmp.size() && tmp[b] == tmp[a]) ++b;
+                if (b - a > 255) return false;
+                keys.push_back(((uint64_t)tmp[a] << 32) | ((uint64_t)i << 8) | (uint64_t)(b - a));
+                a = b;
+            }
+        }
+        return true;
+    };
+    if (!collect(hc.club_off, hc.clubs, ckeys) || !collect(hc.friend_off, hc.friends, fkeys))
+        return bail("a club / friend id repeats more than 255 times in one profile");
+    radix_sort_u64(ckeys, 64);
+    radix_sort_u64(fkeys, 64);
+    const uint64_t set_off = off;
+    if (off + ckeys.size() + fkeys.size() >= (1ull << 32)) return bail("more than 2^32 postings");
+    hp.post.resize(off + ckeys.size() + fkeys.size());
+    auto add_sets = [&](const std::vector<uint64_t>& keys, std::unordered_map<uint32_t, int32_t>& m) {
+        for (size_t a = 0; a < keys.size();) {
+            const uint32_t id = (uint32_t)(keys[a] >> 32);
+            size_t b = a;
+            while (b < keys.size() && (uint32_t)(keys[b] >> 32) == id) {
+                hp.post[off + (b - a)] = (uint32_t)keys[b];
+                ++b;
+            }
+            m[id] = (int32_t)hp.lists.size();
+            hp.lists.push_back(PList{(uint32_t)off, 0u, 0u, (uint32_t)(b - a)});
+            off += b - a;
+            a = b;
+        }
+    };
+    add_sets(ckeys, hp.club_list);
+    add_sets(fkeys, hp.friend_list);
+    (void)set_off;
+    // ---- token entries and their norms, per column in idx order (lists come out sorted)
+    hp.pnorm.resize(hp.tok_entries);
+    {
+        std::vector<std::thread> ts;
+        for (int t = 0; t < T; ++t)
+            ts.emplace_back([&, t]() {
+                std::vector<uint32_t> cur(cnt[t].size(), 0u);
+                for (size_t tid = 0; tid < cnt[t].size(); ++tid)
+                    if (hp.tok_list[t][tid] >= 0) cur[tid] = hp.lists[hp.tok_list[t][tid]].off;
+                for (int32_t i = 0; i < n; ++i) {
+                    const size_t r = (size_t)i * T + t;
+                    for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
+                        if (hc.tf[k] <= 0) continue;
+                        const uint32_t x = cur[hc.tid[k]]++;
+                        hp.post[x] = ((uint32_t)i << 8) | (uint32_t)hc.tf[k];
+                        hp.pnorm[x] = hc.sqrt_nb[r];
+                    }
+                }
+            });
+        for (auto& x : ts) x.join();
+    }
+    // ---- cells
+    uint64_t coff = 0;
+    for (auto& L : hp.lists) {
+        L.shift = list_shift(L.len, n);
+        L.cell_off = (uint32_t)coff;
+        coff += (((uint64_t)(n - 1) >> L.shift) + 1) + 1;
+        if (coff >= (1ull << 32)) return bail("cell table beyond 2^32 entries");
+    }
+    hp.cells.resize(coff);
+    par_for((int64_t)hp.lists.size(), [&](int64_t lo, int64_t hi) {
+        for (int64_t li = lo; li < hi; ++li) {
+            const PList& L = hp.lists[li];
+            const uint32_t nc = (uint32_t)(((uint64_t)(n - 1) >> L.shift) + 1);
+            uint32_t x = 0;
+            for (uint32_t c = 0; c <= nc; ++c) {
+                const uint64_t lim = (uint64_t)c << L.shift;
+                while (x < L.len && (uint64_t)(hp.post[L.off + x] >> 8) < lim) ++x;
+                hp.cells[L.cell_off + c] = x;
+            }
+        }
+    });
+    // ---- headers
+    hp.hdr.resize(2 * (size_t)n);
+    par_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            uint64_t cm = 0;
+            for (int t = 0; t < T; ++t)
+                if (hc.tok_off[(size_t)i * T + t + 1] > hc.tok_off[(size_t)i * T + t]) cm |= 1ull << t;
+            const uint32_t pb = hc.pub[i] < 0 ? kCodeMissing : hc.pub_code.at(hc.pub[i]);
+            const uint32_t gb = hc.gen[i] < 0 ? kCodeMissing : hc.gen_code.at(hc.gen[i]);
+            const uint32_t nc = (uint32_t)(hc.club_off[i + 1] - hc.club_off[i]);
+            const uint32_t nf = (uint32_t)(hc.friend_off[i + 1] - hc.friend_off[i]);
+            hp.hdr[2 * i] = make_uint4((uint32_t)cm, (uint32_t)((cm >> 32) & 0xFFFFu) | (pb << 16) | (gb << 24),
+                                       ((uint32_t)hc.comp[i] & 0xFFFFu) | ((uint32_t)hc.age[i] << 16), nc | (nf << 16));
+            hp.hdr[2 * i + 1] = make_uint4((uint32_t)hc.reg[3 * i], (uint32_t)hc.reg[3 * i + 1],
+                                           (uint32_t)hc.reg[3 * i + 2], (uint32_t)hc.uid[i]);
+        }
+    });
+    hp.ok = true;
+}
+
+void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const std::vector<int32_t>& excl,
+                      std::vector<uint8_t>& img) {
+    const int T = hc.T;
+    QConst c;
+    fill_qconst(hc, i, c);
+    std::vector<QTok> toks;
+    std::vector<QCol> cols;
+    for (int t = 0; t < T; ++t) {
+        const size_t r = (size_t)i * T + t;
+        const int32_t j0 = (int32_t)toks.size();
+        for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
+            const double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;  // recommender.cpp:78
+            const double wq = (double)hc.tf[k] * idf;
+            if (wq == 0.0) continue;  // adds +-0 to every dot it meets
+            QTok q;
+            q.l = hp.lists[hp.tok_list[t][hc.tid[k]]];  // tf > 0: the query itself is on the list
+            q.wq = wq;
+            q.idf = idf;
+            toks.push_back(q);
+        }
+        if ((int32_t)toks.size() > j0) cols.push_back(QCol{t, j0, (int32_t)toks.size(), 0});
+    }
+    std::vector<PList> sets;
+    auto add_sets = [&](const std::vector<int64_t>& o, const std::vector<uint32_t>& ids,
+                        const std::unordered_map<uint32_t, int32_t>& m) -> int32_t {
+        std::vector<uint32_t> v(ids.begin() + o[i], ids.begin() + o[i + 1]);
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (uint32_t x : v) sets.push_back(hp.lists[m.at(x)]);
+        return (int32_t)v.size();
+    };
+    const int32_t ncl = add_sets(hc.club_off, hc.clubs, hp.club_list);
+    const int32_t nfr = add_sets(hc.friend_off, hc.friends, hp.friend_list);
+    std::vector<uint32_t> ex;
+    for (int32_t u : excl) {
+        const int32_t x = hc.idx_of(u);
+        if (x >= 0) ex.push_back((uint32_t)x);
+    }
+    std::sort(ex.begin(), ex.end());
+    ex.erase(std::unique(ex.begin(), ex.end()), ex.end());
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    QPostHead h{};
+    h.n_tok = (int32_t)toks.size();
+    h.n_act = (int32_t)cols.size();
+    h.n_club = ncl;
+    h.n_friend = nfr;
+    h.n_excl = (int32_t)ex.size();
+    size_t o = a16(sizeof(QConst) + sizeof(QPostHead));
+    h.tok_off = (int32_t)o;
+    o = a16(o + toks.size() * sizeof(QTok));
+    h.col_off = (int32_t)o;
+    o = a16(o + cols.size() * sizeof(QCol));
+    h.set_off = (int32_t)o;
+    o = a16(o + sets.size() * sizeof(PList));
+    h.excl_off = (int32_t)o;
+    o = a16(o + ex.size() * 4);
+    img.assign(o, 0);
+    std::memcpy(img.data(), &c, sizeof c);
+    std::memcpy(img.data() + sizeof(QConst), &h, sizeof h);
+    if (!toks.empty()) std::memcpy(img.data() + h.tok_off, toks.data(), toks.size() * sizeof(QTok));
+    if (!cols.empty()) std::memcpy(img.data() + h.col_off, cols.data(), cols.size() * sizeof(QCol));
+    if (!sets.empty()) std::memcpy(img.data() + h.set_off, sets.data(), sets.size() * sizeof(PList));
+    if (!ex.empty()) std::memcpy(img.data() + h.excl_off, ex.data(), ex.size() * 4);
 }
 
 }  // namespace pf

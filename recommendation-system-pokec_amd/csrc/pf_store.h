@@ -55,7 +55,26 @@ struct QImageHost {
     std::vector<QVal> vals;
 };
 
+// Postings store (K5, pf_types.h), built when the corpus fits its packed encoding.
+struct HostPost {
+    bool ok = false;
+    std::string why;                                   // reason when !ok
+    std::vector<uint4> hdr;                            // [2 * n]
+    std::vector<uint32_t> post;                        // token lists, then club lists, then friend lists
+    std::vector<double> pnorm;                         // [token entries]
+    std::vector<uint32_t> cells;
+    std::vector<PList> lists;
+    std::vector<std::vector<int32_t>> tok_list;        // [col][tid] -> list (-1: none)
+    std::unordered_map<uint32_t, int32_t> club_list, friend_list;
+    int64_t tok_entries = 0;
+};
+
 int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err);
+// fills hp (hp.ok = false with hp.why when the corpus is outside the encoding)
+void build_postings(const HostCorpus& hc, HostPost& hp);
+// Postings query image of candidate idx (pf_types.h layout); excl = uids to exclude
+void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t idx, const std::vector<int32_t>& excl,
+                      std::vector<uint8_t>& img);
 int build_store(const HostCorpus& hc, HostStore& hs, std::string& err);
 // excl: uids to exclude (all-candidates mode), may be null
 // returns false when the cuckoo table cannot be built within kMaxHashLog2

@@ -164,4 +164,56 @@ struct DevStore {
     int32_t n_cols;
 };
 
+// ---------------------------------------------------------------- postings store (K5)
+// The all-candidates scan inverted: for every query token / club / friend, the list of
+// candidates holding it, so a query reads only the lists it names instead of every record.
+// Candidates are in idx order (ascending uid, the reference's tie-break order); a workgroup
+// scores one block of kBlockCands consecutive candidates at a time.
+constexpr int kBlockCands = 1024;          // candidates per workgroup block (4 per thread)
+constexpr int kPostWaves = 4;              // waves per K5 workgroup
+constexpr int kPostThreads = kPostWaves * kWave;
+constexpr int kCandsPerThread = kBlockCands / kPostThreads;
+constexpr int kChunkToks = 8;              // query tokens of one column handled per pass (one tf byte each)
+constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
+constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
+constexpr int kPostMinShift = 10;          // log2(kBlockCands): a cell never splits a block
+
+// One candidate list: entries [off, off + len) of the postings array, sorted by idx.
+// cells[cell_off + c] = first entry (relative) with idx >= c << shift, c = 0 .. ncells,
+// so a block's entries are a sub-range of cell (c0 >> shift) (filtered by idx when
+// shift > kPostMinShift).
+struct PList {
+    uint32_t off, cell_off, shift, len;
+};
+
+// Query token of the postings scan: dot += wq * (tf * idf)  (recommender.cpp:74-85)
+struct QTok {
+    PList l;
+    double wq, idf;
+};
+
+// Active query column: tokens [j0, j1) of the QTok array, in ascending tid order.
+struct QCol {
+    int32_t t, j0, j1, pad;
+};
+
+// Postings query image: QConst | QPostHead | QTok[n_tok] | QCol[n_act] | PList[n_club + n_friend] | int32 excl[n_excl]
+struct QPostHead {
+    int32_t n_tok, n_act, n_club, n_friend;
+    int32_t n_excl, tok_off, col_off, set_off;   // byte offsets from the image start
+    int32_t excl_off, pad0, pad1, pad2;
+};
+
+// Device postings store.  hdr[2 * idx + 0] = {colmask lo, colmask hi16 | pub << 16 | gen << 24,
+// (u16) completion | (u16) age << 16, n_clubs | n_friends << 16}; hdr[2 * idx + 1] =
+// {region0, region1, region2, uid}.
+struct PostStore {
+    const uint4* hdr;
+    const uint32_t* post;     // entries: idx << 8 | tf (token lists), idx << 8 | multiplicity (set lists)
+    const double* pnorm;      // [token entries] sqrt(sum (tf*idf)^2) of the entry's (candidate, column)
+    const uint32_t* cells;
+    int32_t n;                // candidates
+    int32_t n_blocks;         // ceil(n / kBlockCands)
+};
+
 }  // namespace pf

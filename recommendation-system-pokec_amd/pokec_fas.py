@@ -19,13 +19,14 @@ LIB_PATH = os.environ.get("PF_LIB_PATH") or os.path.join(HERE, "libpokec_fas.so"
 PF_OK, PF_EINVAL, PF_ENODEV, PF_ENOMEM, PF_ENOTFOUND, PF_EUNSUPP = 0, -1, -2, -3, -4, -5
 PF_MODE_FOF, PF_MODE_ALL = 0, 1
 PF_FOF_GRAPH, PF_FOF_COLLAB = 0, 1
+PF_SCAN_AUTO, PF_SCAN_STREAM, PF_SCAN_POSTINGS = 0, 1, 2
 MAX_TOPK_DEVICE = 64
 
 # every entry point of include/pokec_fas.h
 EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_users", "pf_idf", "pf_fas_pairs",
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
-           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read"]
+           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_set_scan_kernel"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -35,7 +36,8 @@ PF_LOAD_REFERENCE_CAP = 100000
 
 class PfLayoutStats(ctypes.Structure):
     _fields_ = [("n_slots", ctypes.c_int64), ("stream_bytes", ctypes.c_int64), ("header_bytes", ctypes.c_int64),
-                ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32)]
+                ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32),
+                ("post_bytes", ctypes.c_int64), ("scan_kernel", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 class PfDatasetInfo(ctypes.Structure):
@@ -76,6 +78,7 @@ def lib():
         L.pf_fof_candidates.argtypes = [V, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_set_adj.argtypes = [V, I32, V, I32]
         L.pf_set_shard.argtypes = [V, I32, I32]
+        L.pf_set_scan_kernel.argtypes = [V, I32]
         L.pf_scan_keys_async.argtypes = [V, V, I32, I32, V, V]
         L.pf_merge_keys_async.argtypes = [V, V, I32, I32, I32, V, V]
         L.pf_decode_keys.argtypes = [V, I32, V, V, V]
@@ -204,6 +207,10 @@ class FasEngine:
 
     def set_shard(self, shard, nshards):
         self._check(self._L.pf_set_shard(self.h, shard, nshards), "pf_set_shard")
+
+    def set_scan_kernel(self, kind):
+        """PF_SCAN_AUTO / PF_SCAN_STREAM (record walk, K1) / PF_SCAN_POSTINGS (K5)."""
+        self._check(self._L.pf_set_scan_kernel(self.h, kind), "pf_set_scan_kernel")
 
     # -- device-resident scan for multi-GPU benches (device pointers and a hipStream_t
     #    handle as ints; stream 0 is the HIP null stream, exactly as given)

@@ -57,18 +57,27 @@ def test_recommenders_match_reference(gold):
         _check_lists(got, items, (tag, uid, k, lim))
 
 
-def test_all_candidates_scan_matches_reference(gold):
+SCAN_KERNELS = {"stream": 1, "postings": 2}
+
+
+@pytest.mark.parametrize("kernel", list(SCAN_KERNELS))
+def test_all_candidates_scan_matches_reference(gold, kernel):
     name, corpus, eng = gold
-    g = tl.golden_lists(name, "all.txt")
-    keys = list(g.keys())
-    uids = [k[1] for k in keys]
-    got = eng.recommend_interest_all(uids, 50)
-    for key, res in zip(keys, got):
-        _check_lists(res, g[key], key)
-    # top-10 is the prefix of top-50 (same comparator)
-    got10 = eng.recommend_interest_all(uids, 10)
-    for key, res in zip(keys, got10):
-        _check_lists(res, g[key][:10], key)
+    eng.set_scan_kernel(SCAN_KERNELS[kernel])
+    assert eng.layout().scan_kernel == SCAN_KERNELS[kernel]
+    try:
+        g = tl.golden_lists(name, "all.txt")
+        keys = list(g.keys())
+        uids = [k[1] for k in keys]
+        got = eng.recommend_interest_all(uids, 50)
+        for key, res in zip(keys, got):
+            _check_lists(res, g[key], key)
+        # top-10 is the prefix of top-50 (same comparator)
+        got10 = eng.recommend_interest_all(uids, 10)
+        for key, res in zip(keys, got10):
+            _check_lists(res, g[key][:10], key)
+    finally:
+        eng.set_scan_kernel(0)
 
 
 def test_fof_gathers_match_oracle(gold):
@@ -88,15 +97,55 @@ def big():
     return c, tl.engine(ptr), tl.Oracle(None, desc_ptr=ptr)
 
 
-def test_big_all_candidates_vs_oracle(big):
+def _degrees(c):
+    """Out-degree per uid of a synth corpus (adjacency arrays of its pf_corpus_desc)."""
+    import ctypes
+    d = tl.PfCorpusDesc.from_address(c.desc_ptr())
+    n = d.n_adj
+    uid = np.ctypeslib.as_array(ctypes.cast(d.adj_uid, ctypes.POINTER(ctypes.c_int32)), shape=(n,))
+    off = np.ctypeslib.as_array(ctypes.cast(d.adj_off, ctypes.POINTER(ctypes.c_int64)), shape=(n + 1,))
+    return uid.copy(), np.diff(off)
+
+
+@pytest.mark.parametrize("kernel", list(SCAN_KERNELS))
+def test_big_all_candidates_vs_oracle(big, kernel):
+    """Random queries plus the highest-degree users (exclusion lists beyond one wave's
+    64 lanes) and the densest-text users (columns of more than 8 query tokens)."""
     c, eng, orc = big
     rng = np.random.default_rng(5)
-    q = [int(x) for x in rng.integers(1, 20001, 12)] + [8, 1]
-    got = eng.recommend_interest_all(q, 10)
+    uid, deg = _degrees(c)
+    q = [int(x) for x in rng.integers(1, 20001, 12)] + [8, 1] + [int(x) for x in uid[np.argsort(-deg)[:4]]]
+    assert deg.max() > 64
+    eng.set_scan_kernel(SCAN_KERNELS[kernel])
+    try:
+        got = eng.recommend_interest_all(q, 10)
+    finally:
+        eng.set_scan_kernel(0)
     ref = orc.interest(q, 10, tl.PF_MODE_ALL, 0)
     for u, g, r in zip(q, got, ref):
         assert list(g[0]) == list(r[0]), u
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def test_postings_scan_every_user_small_corpus():
+    """K5 against K1 and the oracle on every query of a 3k-user edge-case corpus: every
+    candidate's score shows up in some top-64, and both kernels agree bit for bit."""
+    c = tl.synth.Corpus(n_users=3000, seed=5, edge_cases=1)
+    ptr = c.desc_ptr()
+    eng, orc = tl.engine(ptr), tl.Oracle(None, desc_ptr=ptr)
+    q = list(range(1, 3001))
+    eng.set_scan_kernel(2)
+    post = eng.recommend_interest_all(q, 64)
+    eng.set_scan_kernel(1)
+    stream = eng.recommend_interest_all(q, 64)
+    ref = orc.interest(q[::50], 64, tl.PF_MODE_ALL, 0)
+    for i, (p, s) in enumerate(zip(post, stream)):
+        assert list(p[0]) == list(s[0]), q[i]
+        assert np.array_equal(p[1].view(np.uint32), s[1].view(np.uint32)), q[i]
+    for u, r in zip(q[::50], ref):
+        p = post[u - 1]
+        assert list(p[0]) == list(r[0]), u
+        assert np.array_equal(p[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
 def test_big_pairs_vs_oracle(big):
@@ -121,17 +170,26 @@ def test_big_collab_and_clubs_vs_oracle(big):
         assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
-def test_big_top64_vs_oracle(big):
+@pytest.mark.parametrize("kernel", list(SCAN_KERNELS))
+def test_big_top64_vs_oracle(big, kernel):
     c, eng, orc = big
     q = [2, 777, 12345, 19999]
-    for u, g, r in zip(q, eng.recommend_interest_all(q, 64), orc.interest(q, 64, tl.PF_MODE_ALL, 0)):
+    eng.set_scan_kernel(SCAN_KERNELS[kernel])
+    try:
+        got = eng.recommend_interest_all(q, 64)
+    finally:
+        eng.set_scan_kernel(0)
+    for u, g, r in zip(q, got, orc.interest(q, 64, tl.PF_MODE_ALL, 0)):
         assert list(g[0]) == list(r[0]), u
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
-@pytest.mark.parametrize("env", [{"PF_STAGE_LIMIT": "0"}, {"PF_STAGE_LIMIT": "1024"}, {"PF_TILE_STEPS": "3"},
-                                 {"PF_TILE_STEPS": "1", "PF_STAGE_LIMIT": "0"}],
-                         ids=["global-tables", "threshold-1k", "split-records", "split-records-global"])
+@pytest.mark.parametrize("env", [{"PF_SCAN": "stream", "PF_STAGE_LIMIT": "0"},
+                                 {"PF_SCAN": "stream", "PF_STAGE_LIMIT": "1024"},
+                                 {"PF_SCAN": "stream", "PF_TILE_STEPS": "3"},
+                                 {"PF_SCAN": "stream", "PF_TILE_STEPS": "1", "PF_STAGE_LIMIT": "0"},
+                                 {"PF_SCAN": "postings"}],
+                         ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
     query of the batch has tables above 1 KiB (the whole launch then probes global);
@@ -244,7 +302,8 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
     ref = eng.recommend_interest_all(list(q), k)
     eng2 = tl.engine(c.desc_ptr())
     s = torch.cuda.Stream()
-    for world in (2, 3):
+    for world, kern in ((2, 1), (3, 1), (2, 2), (3, 2), (7, 2)):
+        eng2.set_scan_kernel(kern)
         parts = torch.empty((world, len(q), k), dtype=torch.int64, device="cuda")
         for r in range(world):
             eng2.set_shard(r, world)

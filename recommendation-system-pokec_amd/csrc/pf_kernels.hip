@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-                                                              const int32_t* __restrict__ out_rows) {
+                                                              const int32_t* __restrict__ out_rows, uint32_t dbg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t* img = pool + img_off[blockIdx.y];
     const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         __syncthreads();
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
         {
-            uint32_t lo = 0, hi = (uint32_t)H.n_excl;
+            uint32_t lo = 0, hi = (dbg & 16) ? 0u : (uint32_t)H.n_excl;
             if (hi > kPostThreads) {
                 while (lo < hi) {  // first entry >= c0
                     const uint32_t mid = (lo + hi) >> 1;
@@ -914,7 +914,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             }
         }
         // 2. clubs / friends
-        walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
+        if (!(dbg & 4)) walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
             const uint32_t p = (e >> 8) - c0;
             if (p < (uint32_t)kBlockCands) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
@@ -955,7 +955,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         }
         __syncthreads();  // the counters' LDS now holds the compacted lists
         // 4. text columns, ascending
-        for (int ci = 0; ci < H.n_act; ++ci) {
+        for (int ci = 0; ci < ((dbg & 8) ? 0 : H.n_act); ++ci) {
             const QCol col = cols[ci];
             const int t = col.t;
             uint32_t colhit = 0;  // bit kk: owned candidate kk has a hit in column t
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             for (int js = col.j0; js < col.j1; js += kChunkToks) {
                 const int nj = min(kChunkToks, col.j1 - js);
                 const bool last = js + kChunkToks >= col.j1;
-                walk_lists<true>(ps, rng + js, nj, [&](int j, uint32_t e, double nv) {
+                if (!(dbg & 1)) walk_lists<true>(ps, rng + js, nj, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
                     if (p < (uint32_t)kBlockCands) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                             dot += w.wq * ((double)tf * w.idf);
                         }
                     }
-                    term[p] = !last ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
+                    term[p] = (!last || (dbg & 2)) ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
                 __syncthreads();
                 if (tid == 0) *nlist = 0u;
@@ -1149,6 +1149,16 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
     return last_nb;
 }
 
+// PF_K5_DBG: bit mask that switches K5 phases off (profiling only; results are wrong then):
+// 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions
+static uint32_t post_dbg() {
+    static const uint32_t v = [] {
+        const char* e = getenv("PF_K5_DBG");
+        return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+    }();
+    return v;
+}
+
 // K5 dynamic LDS: QConst | fixed per-block arrays | QVal[n_tok] | ranges[n_lists]
 uint32_t post_var_lds(int n_tok, int n_lists) { return (uint32_t)(16 * n_tok + 8 * n_lists); }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
@@ -1158,7 +1168,7 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
                        const int32_t* out_rows, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     hipLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool, img_off,
-                       blk_begin, blk_end, k, parts, sync, out, out_rows);
+                       blk_begin, blk_end, k, parts, sync, out, out_rows, post_dbg());
     return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for n in io:
         assert hasattr(L, n), n
     assert sorted(pf.IO_EXPORTS) == io
-    assert L.pf_abi_version() == 1
+    assert L.pf_abi_version() == 2
 
 
 def _key(score, uid):

@@ -11,9 +11,11 @@ bytes) for the whole batch, the per-shard top-10 keys are exchanged with one RCC
 all-gather over xGMI and merged on device.  Per-GPU work is fixed (1.6M pairs/step):
 weak scaling.  value = candidates scored / s over the whole job.
 
-Also reports the roofline of the dominant kernel (fas_scan_kernel, HIP events around
-every launch) and the CPU baseline (oracle/refcpu.cpp, the reference algorithm with its
-unordered_map data structures, single thread, bounded sample of the same corpus).
+Also reports the roofline of the dominant kernel (fas_post_kernel, the postings scan, by
+default; fas_scan_kernel, the record-stream scan, with --scan-kernel stream; HIP events
+around every launch) with both the algorithmic rate and the measured DRAM share, and the
+CPU baseline (oracle/refcpu.cpp, the reference algorithm with its unordered_map data
+structures, single thread, bounded sample of the same corpus).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N

@@ -841,6 +841,58 @@ __device__ __forceinline__ void walk_lists(const PostStore& ps, const uint2* rng
     }
 }
 
+// gpre[j] = sum of the lengths of ranges 0 .. j-1 (j <= nl), by one wave
+__device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, int nl, int lane) {
+    uint32_t carry = 0;
+    for (int b = 0; b < nl; b += 64) {
+        const int j = b + lane;
+        const uint32_t len = j < nl ? rng[j].y - rng[j].x : 0u;
+        uint32_t x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) x += y;
+        }
+        if (j < nl) gpre[j] = carry + x - len;
+        carry += (uint32_t)__shfl((int)x, 63);
+    }
+    if (lane == 0) gpre[nl] = carry;
+}
+
+// The entries of token lists js .. js + nj - 1 (nj <= 8) flattened over the workgroup, with
+// the block's token prefix gpre: a thread finds the list of a flat entry in 3 bisection
+// steps.  Two entries per thread and group of 512, loaded together, then f(list - js, entry, norm).
+template <class F>
+__device__ __forceinline__ void walk_chunk(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
+                                           F f) {
+    static_assert(kChunkToks <= 8, "3 bisection steps cover 8 lists");
+    const uint32_t base = gpre[js], total = gpre[js + nj] - base;
+    for (uint32_t f0 = 0; f0 < total; f0 += 2 * kPostThreads) {
+        int jj[2];
+        uint32_t xs[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
+            int j = js;  // last list starting at or before fl
+            if (j + 4 < js + nj && gpre[j + 4] - base <= fl) j += 4;
+            if (j + 2 < js + nj && gpre[j + 2] - base <= fl) j += 2;
+            if (j + 1 < js + nj && gpre[j + 1] - base <= fl) j += 1;
+            jj[u] = fl < total ? j : -1;
+            xs[u] = fl < total ? rng[j].x + (fl - (gpre[j] - base)) : 0u;
+        }
+        uint32_t ent[2];
+        double nv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            ent[u] = jj[u] >= 0 ? ps.post[xs[u]] : 0u;
+            nv[u] = jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (jj[u] >= 0) f(jj[u] - js, ent[u], nv[u]);
+    }
+}
+
 __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
@@ -865,6 +917,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
     uint32_t* nlist = exb + 32;
     QVal* qv = reinterpret_cast<QVal*>(base + kPostFixedLds);
     uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + 16 * H.n_tok);
+    uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
     const int nsets = H.n_club + H.n_friend;
     const int nl = H.n_tok + nsets;
     stage(smem, img, sizeof(QConst));
@@ -895,6 +948,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         }
         if (tid < 32) exb[tid] = 0u;
         __syncthreads();
+        if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
         {
             uint32_t lo = 0, hi = (dbg & 16) ? 0u : (uint32_t)H.n_excl;
@@ -968,7 +1022,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             for (int js = col.j0; js < col.j1; js += kChunkToks) {
                 const int nj = min(kChunkToks, col.j1 - js);
                 const bool last = js + kChunkToks >= col.j1;
-                if (!(dbg & 1)) walk_lists<true>(ps, rng + js, nj, [&](int j, uint32_t e, double nv) {
+                if (!(dbg & 1)) walk_chunk(ps, rng, gpre, js, nj, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
                     if (p < (uint32_t)kBlockCands) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
@@ -1160,7 +1214,7 @@ static uint32_t post_dbg() {
 }
 
 // K5 dynamic LDS: QConst | fixed per-block arrays | QVal[n_tok] | ranges[n_lists]
-uint32_t post_var_lds(int n_tok, int n_lists) { return (uint32_t)(16 * n_tok + 8 * n_lists); }
+uint32_t post_var_lds(int n_tok, int n_lists) { return (uint32_t)(16 * n_tok + 8 * n_lists + 4 * (n_tok + 1) + 15) & ~15u; }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,

@@ -317,3 +317,46 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
             assert list(uids) == list(ref[i][0]), (world, q[i])
             assert np.array_equal(scores.view(np.uint32), ref[i][1].view(np.uint32))
     eng2.set_shard(0, 1)
+
+
+def test_full_size_kernels_agree():
+    """BASELINE cfg 2 size (1,632,803 users): the postings scan (K5), the record-stream scan
+    (K1) and the pair kernel (K1') are three independent GPU paths; on the full corpus
+    their top-k ids and FAS bits agree, the top-k is sorted by the reference comparator,
+    and the 2-shard merge equals the single-shard result."""
+    import torch
+    pf = tl.product()
+    c = tl.synth.Corpus(n_users=1632803, seed=1, edge_cases=0, threads=16)
+    eng = tl.engine(c.desc_ptr())
+    rng = np.random.default_rng(21)
+    q = [int(x) for x in rng.integers(1, 1632804, 6)]
+    k = 10
+    eng.set_scan_kernel(2)
+    post = eng.recommend_interest_all(q, k)
+    eng.set_scan_kernel(1)
+    stream = eng.recommend_interest_all(q, k)
+    eng.set_scan_kernel(0)
+    for u, p, s in zip(q, post, stream):
+        assert len(p[0]) == k and list(p[0]) == list(s[0]), u
+        assert np.array_equal(p[1].view(np.uint32), s[1].view(np.uint32)), u
+        # comparator: score desc, uid asc (recommender_graph.cpp:97-101)
+        pairs = list(zip(p[1].tolist(), p[0].tolist()))
+        assert pairs == sorted(pairs, key=lambda x: (-x[0], x[1])), u
+        # K1' rescoring of the same pairs
+        again = eng.fas_pairs(np.full(k, u, np.int32), p[0])
+        assert np.array_equal(again.view(np.uint32), p[1].view(np.uint32)), u
+    s = torch.cuda.Stream()
+    parts = torch.empty((2, len(q), k), dtype=torch.int64, device="cuda")
+    for r in range(2):
+        eng.set_shard(r, 2)
+        eng.scan_keys_async(np.array(q, np.int32), k, parts[r].data_ptr(), s.cuda_stream)
+    out = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
+    eng.merge_keys_async(parts.data_ptr(), 2, len(q), k, out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    eng.set_shard(0, 1)
+    keys = out.cpu().numpy().view(np.uint64)
+    for i in range(len(q)):
+        uids, scores = pf.decode_keys(keys[i])
+        assert list(uids) == list(post[i][0])
+        assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32))
+    eng.close()

@@ -21,6 +21,8 @@
  *   pf_holdout_friends       run_friends_holdout_test    src/test.cpp:13-105           (A19)
  *   pf_recommendation_tests  run_recommendation_tests_sample
  *                                                        src/recommendation_tests.cpp:68-169 (A19)
+ *   pf_eval_holdout_friends / pf_eval_recommendation_tests: the same two drivers batched and
+ *                            sharded over GPUs (F1, cfg 5)
  *
  * The loaders keep the reference's hash containers (same key types, same
  * insertion sequence), so every order the reference derives from
@@ -100,6 +102,24 @@ int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, d
 /* run_recommendation_tests_sample: out[5] = {graph_hit_rate, collab_hit_rate,
  * interest_hit_rate, avg_club_prec_at_k, avg_club_recall_at_k}. */
 int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5);
+
+/* Batched, shardable forms of the two drivers (BASELINE cfg 5).  The plan
+ * (sampled users and their held-out friends, in the sequential driver's rng order) is computed
+ * up front; each user's query reads the adjacency it would have seen (test.cpp: every earlier
+ * user's edit, one adj_mod for the run; recommendation_tests.cpp: only its own row) through a
+ * view, so users are independent: shard s of n evaluates plan entries i with i % n == s,
+ * `batch` users per GPU pass, and writes per-entry results (other entries untouched):
+ *   pf_eval_holdout_friends:      out_ratio[i]
+ *   pf_eval_recommendation_tests: out_hits[3i .. 3i+2] = graph / collaborative / interest hit
+ *                                 (0/1); out_club[2i], out_club[2i+1] = club precision,
+ *                                 recall@k, NaN for a user without clubs.
+ * *n_plan = plan length.  Averaging the merged entries in plan order reproduces
+ * pf_holdout_friends / pf_recommendation_tests bit for bit. */
+int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard,
+                            int32_t nshards, int32_t batch, double* out_ratio, int32_t cap, int32_t* n_plan);
+int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                 int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
+                                 double* out_club, int32_t cap, int32_t* n_plan);
 
 #ifdef __cplusplus
 }

@@ -10,10 +10,12 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
+#include "pf_batch.h"
 #include "pf_kernels.h"
 #include "pf_store.h"
 #include "pokec_fas.h"
@@ -191,18 +193,18 @@ void add_image(Images& im, const pf::QImageHost& q) {
 }
 
 // recommender_graph.cpp:10-31 (friends + FoFs, first-seen order, limit after every push)
-std::vector<int32_t> gather_graph(const pf::HostCorpus& hc, int32_t u, int32_t limit) {
+std::vector<int32_t> gather_graph(const pf::AdjView& V, int32_t u, int32_t limit) {
     std::vector<int32_t> out;
-    auto it = hc.adj.find(u);
-    if (it == hc.adj.end()) return out;
+    const std::vector<int32_t>* ru = V.row(u);
+    if (!ru) return out;
     std::unordered_set<int32_t> seen;
-    for (int32_t f : it->second) {
+    for (int32_t f : *ru) {
         if (f == u) continue;
         if (seen.insert(f).second) out.push_back(f);
         if ((int32_t)out.size() >= limit) return out;
-        auto jt = hc.adj.find(f);
-        if (jt == hc.adj.end()) continue;
-        for (int32_t x : jt->second) {
+        const std::vector<int32_t>* rf = V.row(f);
+        if (!rf) continue;
+        for (int32_t x : *rf) {
             if (x == u || !seen.insert(x).second) continue;
             out.push_back(x);
             if ((int32_t)out.size() >= limit) return out;
@@ -212,15 +214,15 @@ std::vector<int32_t> gather_graph(const pf::HostCorpus& hc, int32_t u, int32_t l
 }
 
 // recommender_graph.cpp:114-125 (FoFs only; inner loop breaks at the limit)
-std::vector<int32_t> gather_collab(const pf::HostCorpus& hc, int32_t u, int32_t limit) {
+std::vector<int32_t> gather_collab(const pf::AdjView& V, int32_t u, int32_t limit) {
     std::vector<int32_t> out;
-    auto it = hc.adj.find(u);
-    if (it == hc.adj.end()) return out;
+    const std::vector<int32_t>* ru = V.row(u);
+    if (!ru) return out;
     std::unordered_set<int32_t> seen;
-    for (int32_t f : it->second) {
-        auto jt = hc.adj.find(f);
-        if (jt == hc.adj.end()) continue;  // skips the limit check too (recommender_graph.cpp:117-118)
-        for (int32_t x : jt->second) {
+    for (int32_t f : *ru) {
+        const std::vector<int32_t>* rf = V.row(f);
+        if (!rf) continue;  // skips the limit check too (recommender_graph.cpp:117-118)
+        for (int32_t x : *rf) {
             if (x == u) continue;
             if (seen.insert(x).second) out.push_back(x);
             if ((int32_t)out.size() >= limit) break;
@@ -230,41 +232,80 @@ std::vector<int32_t> gather_collab(const pf::HostCorpus& hc, int32_t u, int32_t 
     return out;
 }
 
+pf::AdjView plain_view(const pf_ctx* c) {
+    pf::AdjView v;
+    v.base = &c->hc.adj;
+    return v;
+}
+
 // FAS(A = qidx[g], B = slots[g][j]) for every group g, on the GPU.
+// Groups go to the GPU in chunks (<= 4096 distinct queries, <= 8M pairs per launch); each
+// distinct query's image is built once per chunk, on host threads.
 int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std::vector<int32_t>>& slots,
               std::vector<std::vector<float>>& out) {
     out.assign(qidx.size(), {});
-    Images im;
-    std::vector<pf::PairBlock> blocks;
-    std::vector<int32_t> flat;
-    pf::QImageHost qi;
-    for (size_t g = 0; g < qidx.size(); ++g) {
-        out[g].assign(slots[g].size(), 0.f);
-        if (slots[g].empty()) continue;
-        if (!pf::build_query(c->hc, c->hs.packed, qidx[g], nullptr, qi)) return c->fail(PF_EUNSUPP, "query hash table too large");
-        const int32_t img = (int32_t)im.refs.size();
-        add_image(im, qi);
-        for (size_t b = 0; b < slots[g].size(); b += 256) {
-            pf::PairBlock pb{img, (int32_t)flat.size(), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
-            blocks.push_back(pb);
-            for (size_t j = b; j < b + (size_t)pb.count; ++j) flat.push_back(slots[g][j]);
+    for (size_t g = 0; g < qidx.size(); ++g) out[g].assign(slots[g].size(), 0.f);
+    size_t g0 = 0;
+    while (g0 < qidx.size()) {
+        // chunk [g0, g1)
+        std::unordered_map<int32_t, int32_t> img_of;
+        std::vector<int32_t> uq;
+        size_t g1 = g0, pairs = 0;
+        for (; g1 < qidx.size(); ++g1) {
+            if (slots[g1].empty()) continue;
+            const bool fresh = !img_of.count(qidx[g1]);
+            if (g1 > g0 && ((fresh && uq.size() >= 4096) || pairs + slots[g1].size() > (8u << 20))) break;
+            if (fresh) {
+                img_of.emplace(qidx[g1], (int32_t)uq.size());
+                uq.push_back(qidx[g1]);
+            }
+            pairs += slots[g1].size();
         }
+        if (pairs == 0) { g0 = g1; continue; }
+        std::vector<pf::QImageHost> qi(uq.size());
+        std::vector<uint8_t> ok(uq.size(), 1);
+        {
+            const int th = (int)std::min<size_t>(16, std::max<size_t>(1, uq.size() / 16));
+            std::vector<std::thread> ts;
+            for (int w = 0; w < th; ++w)
+                ts.emplace_back([&, w]() {
+                    for (size_t i = (size_t)w; i < uq.size(); i += (size_t)th)
+                        ok[i] = pf::build_query(c->hc, c->hs.packed, uq[i], nullptr, qi[i]) ? 1 : 0;
+                });
+            for (auto& t : ts) t.join();
+        }
+        for (uint8_t x : ok)
+            if (!x) return c->fail(PF_EUNSUPP, "query hash table too large");
+        Images im;
+        for (auto& x : qi) add_image(im, x);
+        std::vector<pf::PairBlock> blocks;
+        std::vector<int32_t> flat;
+        flat.reserve(pairs);
+        for (size_t g = g0; g < g1; ++g) {
+            if (slots[g].empty()) continue;
+            const int32_t img = img_of.at(qidx[g]);
+            for (size_t b = 0; b < slots[g].size(); b += 256) {
+                pf::PairBlock pb{img, (int32_t)flat.size(), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
+                blocks.push_back(pb);
+                for (size_t j = b; j < b + (size_t)pb.count; ++j) flat.push_back(slots[g][j]);
+            }
+        }
+        HIPCHK(c, upload(c, c->d_pool, im.pool));
+        HIPCHK(c, upload(c, c->d_refs, im.refs));
+        HIPCHK(c, upload(c, c->d_blocks, blocks));
+        HIPCHK(c, upload(c, c->d_slots, flat));
+        HIPCHK(c, c->d_scores.ensure(flat.size() * sizeof(float)));
+        HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
+                                   c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
+                                   c->d_scores.as<float>(), c->stream));
+        std::vector<float> res(flat.size());
+        HIPCHK(c, hipMemcpyAsync(res.data(), c->d_scores.p, res.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        size_t o = 0;
+        for (size_t g = g0; g < g1; ++g)
+            for (size_t j = 0; j < slots[g].size(); ++j) out[g][j] = res[o++];
+        g0 = g1;
     }
-    if (flat.empty()) return PF_OK;
-    HIPCHK(c, upload(c, c->d_pool, im.pool));
-    HIPCHK(c, upload(c, c->d_refs, im.refs));
-    HIPCHK(c, upload(c, c->d_blocks, blocks));
-    HIPCHK(c, upload(c, c->d_slots, flat));
-    HIPCHK(c, c->d_scores.ensure(flat.size() * sizeof(float)));
-    HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
-                               c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
-                               c->d_scores.as<float>(), c->stream));
-    std::vector<float> res(flat.size());
-    HIPCHK(c, hipMemcpyAsync(res.data(), c->d_scores.p, res.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    size_t o = 0;
-    for (size_t g = 0; g < qidx.size(); ++g)
-        for (size_t j = 0; j < slots[g].size(); ++j) out[g][j] = res[o++];
     return PF_OK;
 }
 
@@ -410,7 +451,217 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     return PF_OK;
 }
 
+int emit_jobs(pf_ctx* c, std::vector<pf::Job>& jobs, int topk, int32_t* ou, float* os, int32_t* oc) {
+    for (size_t i = 0; i < jobs.size(); ++i) oc[i] = 0;
+    if (topk == 0 || jobs.empty()) return PF_OK;
+    const int rc = pf::run_jobs(c, jobs);
+    if (rc != PF_OK) return rc;
+    for (size_t i = 0; i < jobs.size(); ++i) emit(jobs[i].out, (int)i, topk, ou, os, oc);
+    return PF_OK;
+}
+
 }  // namespace
+
+namespace pf {
+
+const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c) { return c->hc.adj; }
+
+// Every job's FAS pairs in two GPU stages (stage 2: the clubs recommender's friend-of-friend
+// pairs, which depend on stage 1's friend weights), then the reference's host arithmetic.
+int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
+    const auto& hc = c->hc;
+    const auto& slot_of = c->hs.slot_of_idx;
+    struct St {
+        int32_t iq = -1;
+        int g0 = -1, g1 = -1;             // stage-1 groups
+        std::vector<int32_t> cuid;        // interest / collab: candidate uids of the scored pairs
+        std::vector<int32_t> friends;     // collab / clubs: the query's adjacency row
+        std::vector<int32_t> fidx, fuid;  // distinct friends with a profile
+        std::unordered_map<int32_t, int32_t> fpos;
+        std::vector<int32_t> grp;         // clubs: stage-2 group per friend
+    };
+    std::vector<St> st(jobs.size());
+    std::vector<int32_t> qidx;
+    std::vector<std::vector<int32_t>> slots;
+    auto add = [&](int32_t q, std::vector<int32_t>&& sl) {
+        qidx.push_back(q);
+        slots.push_back(std::move(sl));
+        return (int)qidx.size() - 1;
+    };
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        Job& J = jobs[i];
+        St& S = st[i];
+        J.out.clear();
+        const int32_t u = J.uid;
+        if (J.topk <= 0) continue;
+        if (J.kind == kJobInterest) {
+            S.iq = hc.idx_of(u);
+            if (S.iq < 0) continue;  // recommender_graph.cpp:39-40
+            std::unordered_set<int32_t> skip;
+            if (const std::vector<int32_t>* r = J.view.row(u)) skip.insert(r->begin(), r->end());
+            skip.insert(u);
+            std::vector<int32_t> sl;
+            if (J.all_candidates) {
+                for (int32_t j = 0; j < hc.n; ++j)
+                    if (!skip.count(hc.uid[j])) { sl.push_back(slot_of[j]); S.cuid.push_back(hc.uid[j]); }
+            } else {
+                for (int32_t x : gather_graph(J.view, u, J.limit)) {
+                    if (skip.count(x)) continue;
+                    const int32_t ix = hc.idx_of(x);
+                    if (ix < 0) continue;
+                    sl.push_back(slot_of[ix]);
+                    S.cuid.push_back(x);
+                }
+            }
+            S.g0 = add(S.iq, std::move(sl));
+        } else if (J.kind == kJobCollab) {
+            if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
+            std::vector<int32_t> cand = gather_collab(J.view, u, J.limit);
+            S.iq = hc.idx_of(u);
+            if (S.iq < 0) continue;  // recommender_graph.cpp:130
+            for (int32_t f : S.friends) {  // distinct friends with a profile -> matrix rows
+                const int32_t ix = hc.idx_of(f);
+                if (ix < 0 || S.fpos.count(f)) continue;
+                S.fpos.emplace(f, (int32_t)S.fidx.size());
+                S.fidx.push_back(ix);
+            }
+            std::vector<int32_t> cs;
+            for (int32_t x : cand) {
+                if (x == u) continue;
+                const int32_t ix = hc.idx_of(x);
+                if (ix < 0) continue;
+                cs.push_back(slot_of[ix]);
+                S.cuid.push_back(x);
+            }
+            // sim_u_f (float, recommender_graph.cpp:132-136), then M[f][c]
+            std::vector<int32_t> fs;
+            for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
+            S.g0 = add(S.iq, std::move(fs));
+            for (int32_t ix : S.fidx) S.g1 = add(ix, std::vector<int32_t>(cs));
+            S.g1 = S.g0 + 1;
+        } else {
+            S.iq = hc.idx_of(u);
+            if (S.iq < 0) continue;  // recommender_clubs.cpp:13-16
+            if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
+            for (int32_t f : S.friends) {  // pass 1: w_f = FAS(q, f) for distinct friends with a profile
+                const int32_t ix = hc.idx_of(f);
+                if (ix < 0 || S.fpos.count(f)) continue;
+                S.fpos.emplace(f, (int32_t)S.fidx.size());
+                S.fidx.push_back(ix);
+                S.fuid.push_back(f);
+            }
+            std::vector<int32_t> fs;
+            for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
+            S.g0 = add(S.iq, std::move(fs));
+        }
+    }
+    std::vector<std::vector<float>> res;
+    int rc = run_pairs(c, qidx, slots, res);
+    if (rc != PF_OK) return rc;
+    // stage 2: FAS(f, fof) for every fof of every positive-weight friend (clubs)
+    std::vector<int32_t> qidx2;
+    std::vector<std::vector<int32_t>> slots2;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        Job& J = jobs[i];
+        St& S = st[i];
+        if (J.kind != kJobClubs || S.iq < 0 || J.topk <= 0) continue;
+        const std::vector<float>& w = res[S.g0];
+        S.grp.assign(S.fidx.size(), -1);
+        for (size_t r = 0; r < S.fidx.size(); ++r) {
+            if ((double)w[r] <= 0.0) continue;
+            const std::vector<int32_t>* rf = J.view.row(S.fuid[r]);
+            if (!rf) continue;
+            std::vector<int32_t> sl;
+            for (int32_t x : *rf) {
+                if (x == J.uid) continue;
+                const int32_t ix = hc.idx_of(x);
+                if (ix < 0) continue;
+                sl.push_back(slot_of[ix]);
+            }
+            S.grp[r] = (int32_t)qidx2.size();
+            qidx2.push_back(S.fidx[r]);
+            slots2.push_back(std::move(sl));
+        }
+    }
+    std::vector<std::vector<float>> res2;
+    rc = run_pairs(c, qidx2, slots2, res2);
+    if (rc != PF_OK) return rc;
+    // collaborative sums on the GPU (K4), all collab jobs in one pass per job
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        Job& J = jobs[i];
+        St& S = st[i];
+        if (J.topk <= 0 || S.iq < 0) continue;
+        Ranked r;
+        if (J.kind == kJobInterest) {
+            const std::vector<float>& sc = res[S.g0];
+            r.reserve(sc.size());
+            for (size_t j = 0; j < sc.size(); ++j) r.emplace_back(S.cuid[j], sc[j]);
+        } else if (J.kind == kJobCollab) {
+            const int F = (int)S.friends.size(), nc = (int)S.cuid.size();
+            if (nc == 0) continue;
+            std::vector<float> w(F, 0.f), M((size_t)S.fidx.size() * nc);
+            std::vector<int32_t> wrow(F, -1);
+            for (int j = 0; j < F; ++j) {
+                auto rt = S.fpos.find(S.friends[j]);
+                if (rt == S.fpos.end()) continue;
+                wrow[j] = rt->second;
+                w[j] = res[S.g0][rt->second];
+            }
+            for (size_t rr = 0; rr < S.fidx.size(); ++rr)
+                std::copy(res[S.g1 + rr].begin(), res[S.g1 + rr].end(), M.begin() + rr * nc);
+            HIPCHK(c, upload(c, c->d_scores, M));
+            HIPCHK(c, upload(c, c->d_w, w));
+            HIPCHK(c, upload(c, c->d_wrow, wrow));
+            HIPCHK(c, c->d_csum.ensure((size_t)nc * sizeof(float)));
+            HIPCHK(c, pf::launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(), F, nc,
+                                            c->d_csum.as<float>(), c->stream));
+            std::vector<float> sc(nc);
+            HIPCHK(c, hipMemcpyAsync(sc.data(), c->d_csum.p, nc * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            for (int j = 0; j < nc; ++j) r.emplace_back(S.cuid[j], sc[j]);
+        } else {
+            // club accumulation in the reference's exact loop order (double sums)
+            const std::vector<float>& w = res[S.g0];
+            std::unordered_set<int32_t> own;
+            for (int64_t k = hc.club_off[S.iq]; k < hc.club_off[S.iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
+            std::unordered_map<int32_t, double> score;
+            for (int32_t f : S.friends) {
+                auto pt = S.fpos.find(f);
+                if (pt == S.fpos.end()) continue;
+                const double wf = w[pt->second];
+                if (wf <= 0.0) continue;
+                const int32_t ix = S.fidx[pt->second];
+                for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                    if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
+            }
+            for (int32_t f : S.friends) {
+                auto pt = S.fpos.find(f);
+                if (pt == S.fpos.end()) continue;
+                const int32_t g = S.grp[pt->second];
+                const double wf = w[pt->second];
+                if (wf <= 0.0 || g < 0) continue;
+                const std::vector<int32_t>* rf = J.view.row(f);
+                size_t j = 0;
+                for (int32_t x : *rf) {
+                    if (x == J.uid) continue;
+                    const int32_t ix = hc.idx_of(x);
+                    if (ix < 0) continue;
+                    const double sv = res2[g][j++];
+                    if (sv <= 0.0) continue;
+                    const double addv = wf * sv;
+                    for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                        if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += addv;
+                }
+            }
+            for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
+        }
+        rank(r, J.topk);
+        J.out = std::move(r);
+    }
+    return PF_OK;
+}
+
+}  // namespace pf
 
 extern "C" {
 
@@ -604,45 +855,16 @@ int pf_recommend_interest(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk,
         return PF_OK;
     }
     // FoF-limited (reference) mode, or ALL with topk beyond the in-kernel bound
-    std::vector<int32_t> qidx, qrow;
-    std::vector<std::vector<int32_t>> slots, cuid;
+    std::vector<pf::Job> jobs(nq);
     for (int i = 0; i < nq; ++i) {
-        const int32_t u = q[i];
-        const int32_t iq = c->hc.idx_of(u);
-        if (iq < 0) continue;  // recommender_graph.cpp:39-40
-        std::unordered_set<int32_t> skip;
-        auto it = c->hc.adj.find(u);
-        if (it != c->hc.adj.end()) skip.insert(it->second.begin(), it->second.end());
-        skip.insert(u);
-        std::vector<int32_t> s, us;
-        if (mode == PF_MODE_ALL) {
-            for (int32_t j = 0; j < c->hc.n; ++j)
-                if (!skip.count(c->hc.uid[j])) { s.push_back(c->hs.slot_of_idx[j]); us.push_back(c->hc.uid[j]); }
-        } else {
-            for (int32_t x : gather_graph(c->hc, u, limit)) {
-                if (skip.count(x)) continue;
-                int32_t ix = c->hc.idx_of(x);
-                if (ix < 0) continue;
-                s.push_back(c->hs.slot_of_idx[ix]);
-                us.push_back(x);
-            }
-        }
-        qidx.push_back(iq);
-        qrow.push_back(i);
-        slots.push_back(std::move(s));
-        cuid.push_back(std::move(us));
+        jobs[i].kind = pf::kJobInterest;
+        jobs[i].uid = q[i];
+        jobs[i].topk = topk;
+        jobs[i].limit = limit;
+        jobs[i].all_candidates = mode == PF_MODE_ALL;
+        jobs[i].view = plain_view(c);
     }
-    std::vector<std::vector<float>> res;
-    int rc = run_pairs(c, qidx, slots, res);
-    if (rc != PF_OK) return rc;
-    for (size_t g = 0; g < qidx.size(); ++g) {
-        Ranked r;
-        r.reserve(res[g].size());
-        for (size_t j = 0; j < res[g].size(); ++j) r.emplace_back(cuid[g][j], res[g][j]);
-        rank(r, topk);
-        emit(r, qrow[g], topk, ou, os, oc);
-    }
-    return PF_OK;
+    return emit_jobs(c, jobs, topk, ou, os, oc);
 }
 
 // recommender_graph.cpp:105-222
@@ -650,168 +872,37 @@ int pf_recommend_collab(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, i
                         float* os, int32_t* oc) {
     if (!c || nq < 0 || topk < 0 || (nq && (!q || !oc))) return PF_EINVAL;
     (void)hipSetDevice(c->device);
+    std::vector<pf::Job> jobs(nq);
     for (int i = 0; i < nq; ++i) {
-        oc[i] = 0;
-        const int32_t u = q[i];
-        std::vector<int32_t> friends;
-        auto it = c->hc.adj.find(u);
-        if (it != c->hc.adj.end()) friends = it->second;
-        std::vector<int32_t> cand = gather_collab(c->hc, u, limit);
-        const int32_t iq = c->hc.idx_of(u);
-        if (iq < 0) continue;
-        // distinct friends with a profile -> matrix rows
-        std::unordered_map<int32_t, int32_t> row_of;
-        std::vector<int32_t> fidx;
-        for (int32_t f : friends) {
-            int32_t ix = c->hc.idx_of(f);
-            if (ix < 0 || row_of.count(f)) continue;
-            row_of.emplace(f, (int32_t)fidx.size());
-            fidx.push_back(ix);
-        }
-        std::vector<int32_t> cslots, cuids;
-        for (int32_t x : cand) {
-            if (x == u) continue;
-            int32_t ix = c->hc.idx_of(x);
-            if (ix < 0) continue;
-            cslots.push_back(c->hs.slot_of_idx[ix]);
-            cuids.push_back(x);
-        }
-        // sim_u_f (float, recommender_graph.cpp:132-136) and M[f][c] on the GPU
-        std::vector<int32_t> qs;
-        std::vector<std::vector<int32_t>> ss;
-        qs.push_back(iq);
-        ss.emplace_back();
-        for (int32_t ix : fidx) ss[0].push_back(c->hs.slot_of_idx[ix]);
-        for (int32_t ix : fidx) { qs.push_back(ix); ss.push_back(cslots); }
-        std::vector<std::vector<float>> res;
-        int rc = run_pairs(c, qs, ss, res);
-        if (rc != PF_OK) return rc;
-        const int F = (int)friends.size(), nc = (int)cslots.size();
-        if (nc == 0) continue;
-        std::vector<float> w(F, 0.f), M((size_t)fidx.size() * nc);
-        std::vector<int32_t> wrow(F, -1);
-        for (int j = 0; j < F; ++j) {
-            auto rt = row_of.find(friends[j]);
-            if (rt == row_of.end()) continue;
-            wrow[j] = rt->second;
-            w[j] = res[0][rt->second];
-        }
-        for (size_t r = 0; r < fidx.size(); ++r) std::copy(res[r + 1].begin(), res[r + 1].end(), M.begin() + r * nc);
-        HIPCHK(c, upload(c, c->d_scores, M));
-        HIPCHK(c, upload(c, c->d_w, w));
-        HIPCHK(c, upload(c, c->d_wrow, wrow));
-        HIPCHK(c, c->d_csum.ensure((size_t)nc * sizeof(float)));
-        HIPCHK(c, pf::launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(), F, nc,
-                                        c->d_csum.as<float>(), c->stream));
-        std::vector<float> sc(nc);
-        HIPCHK(c, hipMemcpyAsync(sc.data(), c->d_csum.p, nc * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        Ranked r;
-        for (int j = 0; j < nc; ++j) r.emplace_back(cuids[j], sc[j]);
-        rank(r, topk);
-        emit(r, i, topk, ou, os, oc);
+        jobs[i].kind = pf::kJobCollab;
+        jobs[i].uid = q[i];
+        jobs[i].topk = topk;
+        jobs[i].limit = limit;
+        jobs[i].view = plain_view(c);
     }
-    return PF_OK;
+    return emit_jobs(c, jobs, topk, ou, os, oc);
 }
 
 // recommender_clubs.cpp:10-73
-int pf_recommend_clubs(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t /*limit*/, int32_t* ou,
+int pf_recommend_clubs(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
                        float* os, int32_t* oc) {
     if (!c || nq < 0 || topk < 0 || (nq && (!q || !oc))) return PF_EINVAL;
     (void)hipSetDevice(c->device);
-    const auto& hc = c->hc;
+    std::vector<pf::Job> jobs(nq);
     for (int i = 0; i < nq; ++i) {
-        oc[i] = 0;
-        const int32_t u = q[i];
-        const int32_t iq = hc.idx_of(u);
-        if (iq < 0) continue;
-        std::vector<int32_t> friends;
-        auto it = hc.adj.find(u);
-        if (it != hc.adj.end()) friends = it->second;
-        // pass 1: w_f = FAS(q, f) for distinct friends with a profile
-        std::unordered_map<int32_t, int32_t> fpos;
-        std::vector<int32_t> fidx, fuid;
-        for (int32_t f : friends) {
-            int32_t ix = hc.idx_of(f);
-            if (ix < 0 || fpos.count(f)) continue;
-            fpos.emplace(f, (int32_t)fidx.size());
-            fidx.push_back(ix);
-            fuid.push_back(f);
-        }
-        std::vector<std::vector<float>> res;
-        {
-            std::vector<int32_t> qs{iq};
-            std::vector<std::vector<int32_t>> ss(1);
-            for (int32_t ix : fidx) ss[0].push_back(c->hs.slot_of_idx[ix]);
-            int rc = run_pairs(c, qs, ss, res);
-            if (rc != PF_OK) return rc;
-        }
-        std::vector<float> w(res[0]);
-        // pass 2: FAS(f, fof) for every fof of every positive-weight friend
-        std::vector<int32_t> qs;
-        std::vector<std::vector<int32_t>> ss;
-        std::vector<int32_t> grp(fidx.size(), -1);
-        for (size_t r = 0; r < fidx.size(); ++r) {
-            if ((double)w[r] <= 0.0) continue;
-            auto jt = hc.adj.find(fuid[r]);
-            if (jt == hc.adj.end()) continue;
-            std::vector<int32_t> s;
-            for (int32_t x : jt->second) {
-                if (x == u) continue;
-                int32_t ix = hc.idx_of(x);
-                if (ix < 0) continue;
-                s.push_back(c->hs.slot_of_idx[ix]);
-            }
-            grp[r] = (int32_t)qs.size();
-            qs.push_back(fidx[r]);
-            ss.push_back(std::move(s));
-        }
-        std::vector<std::vector<float>> sff;
-        int rc = run_pairs(c, qs, ss, sff);
-        if (rc != PF_OK) return rc;
-        // club accumulation in the reference's exact loop order (double sums)
-        std::unordered_set<int32_t> own;
-        for (int64_t k = hc.club_off[iq]; k < hc.club_off[iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
-        std::unordered_map<int32_t, double> score;
-        for (int32_t f : friends) {
-            auto pt = fpos.find(f);
-            if (pt == fpos.end()) continue;
-            double wf = w[pt->second];
-            if (wf <= 0.0) continue;
-            int32_t ix = fidx[pt->second];
-            for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
-        }
-        for (int32_t f : friends) {
-            auto pt = fpos.find(f);
-            if (pt == fpos.end()) continue;
-            int32_t g = grp[pt->second];
-            double wf = w[pt->second];
-            if (wf <= 0.0 || g < 0) continue;
-            auto jt = hc.adj.find(f);
-            size_t j = 0;
-            for (int32_t x : jt->second) {
-                if (x == u) continue;
-                int32_t ix = hc.idx_of(x);
-                if (ix < 0) continue;
-                double s = sff[g][j++];
-                if (s <= 0.0) continue;
-                double add = wf * s;
-                for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                    if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += add;
-            }
-        }
-        Ranked r;
-        for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
-        rank(r, topk);
-        emit(r, i, topk, ou, os, oc);
+        jobs[i].kind = pf::kJobClubs;
+        jobs[i].uid = q[i];
+        jobs[i].topk = topk;
+        jobs[i].limit = limit;
+        jobs[i].view = plain_view(c);
     }
-    return PF_OK;
+    return emit_jobs(c, jobs, topk, ou, os, oc);
 }
 
 int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {
     if (!c || !n || (cap > 0 && !out)) return PF_EINVAL;
-    std::vector<int32_t> v = flavour == PF_FOF_COLLAB ? gather_collab(c->hc, uid, limit) : gather_graph(c->hc, uid, limit);
+    const pf::AdjView V = plain_view(c);
+    std::vector<int32_t> v = flavour == PF_FOF_COLLAB ? gather_collab(V, uid, limit) : gather_graph(V, uid, limit);
     for (int32_t i = 0; i < (int32_t)v.size() && i < cap; ++i) out[i] = v[i];
     *n = (int32_t)v.size();
     return PF_OK;

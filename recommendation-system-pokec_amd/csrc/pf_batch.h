@@ -1,0 +1,53 @@
+// pf_batch.h — engine-internal batched recommenders (pf_api.cpp) for the C ABI entry points
+// and the batched hold-out drivers (pf_dataset.cpp).  Not part of the public ABI.
+#pragma once
+#include <climits>
+#include <cstdint>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+struct pf_ctx;
+
+namespace pf {
+
+// The adjacency one query sees (adj_list with edits), without copying it:
+//   own_row: this query's own row replaced (recommendation_tests.cpp:111-114, a fresh copy
+//            per user);
+//   over:    rows edited by earlier users of a cumulative test, each visible to queries whose
+//            version is >= the edit's (test.cpp:35,73, one adj_mod for the whole run).
+struct AdjView {
+    const std::unordered_map<int32_t, std::vector<int32_t>>* base = nullptr;
+    const std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>>* over = nullptr;
+    int32_t version = 0;
+    int32_t own = INT32_MIN;
+    const std::vector<int32_t>* own_row = nullptr;
+    const std::vector<int32_t>* row(int32_t v) const {
+        if (own_row && v == own) return own_row;
+        if (over) {
+            auto it = over->find(v);
+            if (it != over->end() && it->second.first <= version) return &it->second.second;
+        }
+        auto it = base->find(v);
+        return it == base->end() ? nullptr : &it->second;
+    }
+};
+
+enum JobKind { kJobInterest = 0, kJobCollab = 1, kJobClubs = 2 };
+
+// One recommender call: recommend_by_interest (FoF-limited, or every candidate when
+// all_candidates), recommend_collaborative or recommend_clubs_collab for uid under view.
+struct Job {
+    int kind = kJobInterest;
+    int32_t uid = 0, topk = 0, limit = 0;
+    bool all_candidates = false;
+    AdjView view;
+    std::vector<std::pair<int32_t, float>> out;  // ranked (id, score), <= topk
+};
+
+// Runs every job; their FAS pairs go to the GPU together (one pair-kernel launch per stage
+// and chunk).  0 = OK, else a PF_* status.
+int run_jobs(pf_ctx* c, std::vector<Job>& jobs);
+const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c);
+
+}  // namespace pf

@@ -16,6 +16,7 @@
 #include <utility>
 #include <vector>
 
+#include "pf_batch.h"
 #include "pokec_io.h"
 
 namespace pf {
@@ -742,6 +743,192 @@ int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
     if (club_users > 0) {
         out5[3] = club_prec / (double)club_users;
         out5[4] = club_rec / (double)club_users;
+    }
+    return PF_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- batched, sharded drivers (F1)
+// The sequential drivers above mutate the engine's adjacency between users, so one user runs
+// at a time.  Their plans (sampled users, held-out friends) depend only on the rng stream, so
+// they are computed up front here; every user's query then reads its adjacency through a view
+// (pf_batch.h) and users run in batches (one GPU pair launch per stage), sharded over ranks.
+
+namespace {
+
+struct PlanEntry {
+    int32_t uid = 0;
+    int hold_k = 0;
+    std::vector<int32_t> newf;
+    std::unordered_set<int> held;
+};
+
+// test.cpp:13-60 (candidates with >= 20 friends, shuffled; hold F/5 per user)
+std::vector<PlanEntry> plan_friends(const pf_dataset* ds, int32_t sample_size) {
+    std::vector<PlanEntry> plan;
+    std::vector<int> candidates;
+    for (auto& kv : ds->profiles) {
+        auto it = ds->adj_list.find(kv.first);
+        if (it == ds->adj_list.end()) continue;
+        if ((int)it->second.size() >= 20) candidates.push_back(kv.first);
+    }
+    if (candidates.empty()) return plan;
+    std::mt19937 rng(1234567);
+    std::shuffle(candidates.begin(), candidates.end(), rng);
+    for (int uid : candidates) {
+        if ((int32_t)plan.size() >= sample_size) break;
+        const std::vector<int>& friends = ds->adj_list.find(uid)->second;
+        const int F = (int)friends.size();
+        if (F < 2) continue;
+        const int hold_k = F / 5;
+        if (hold_k <= 0) continue;
+        std::vector<int> idx(F);
+        for (int i = 0; i < F; ++i) idx[i] = i;
+        std::shuffle(idx.begin(), idx.end(), rng);
+        PlanEntry e;
+        e.uid = uid;
+        e.hold_k = hold_k;
+        for (int i = 0; i < hold_k; ++i) e.held.insert(friends[idx[i]]);
+        for (int f : friends)
+            if (e.held.find(f) == e.held.end()) e.newf.push_back(f);
+        plan.push_back(std::move(e));
+    }
+    return plan;
+}
+
+// recommendation_tests.cpp:76-115 (all profiles shuffled; degree >= 4; hold max(1, F/4))
+std::vector<PlanEntry> plan_rec(const pf_dataset* ds, int32_t sample_size) {
+    std::vector<PlanEntry> plan;
+    if (ds->profiles.empty() || ds->adj_list.empty()) return plan;
+    std::vector<int> all;
+    for (auto& kv : ds->profiles) all.push_back(kv.first);
+    std::mt19937 rng(1234567);
+    std::shuffle(all.begin(), all.end(), rng);
+    for (int uid : all) {
+        if ((int32_t)plan.size() >= sample_size) break;
+        auto itadj = ds->adj_list.find(uid);
+        if (itadj == ds->adj_list.end()) continue;
+        const std::vector<int>& friends = itadj->second;
+        if (friends.size() < 4) continue;
+        const int hold_k = std::max(1, (int)friends.size() / 4);
+        std::vector<int> idx(friends.size());
+        for (size_t i = 0; i < friends.size(); ++i) idx[i] = (int)i;
+        std::shuffle(idx.begin(), idx.end(), rng);
+        PlanEntry e;
+        e.uid = uid;
+        e.hold_k = hold_k;
+        for (int i = 0; i < hold_k; ++i) e.held.insert(friends[idx[i]]);
+        for (int f : friends)
+            if (e.held.find(f) == e.held.end()) e.newf.push_back(f);
+        plan.push_back(std::move(e));
+    }
+    return plan;
+}
+
+bool bad_shard(int32_t shard, int32_t nshards, int32_t batch) {
+    return nshards < 1 || shard < 0 || shard >= nshards || batch < 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard, int32_t nshards,
+                            int32_t batch, double* out_ratio, int32_t cap, int32_t* n_plan) {
+    if (!ctx || !ds || !n_plan || (cap > 0 && !out_ratio) || bad_shard(shard, nshards, batch)) return PF_EINVAL;
+    const std::vector<PlanEntry> plan = plan_friends(ds, sample_size);
+    *n_plan = (int32_t)plan.size();
+    // one adj_mod for the whole run (test.cpp:35,73): user i sees the rows of users 0..i edited
+    std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>> over;
+    for (size_t i = 0; i < plan.size(); ++i) over[plan[i].uid] = {(int32_t)i, plan[i].newf};
+    const auto& base = pf::base_adj(ctx);
+    std::vector<int32_t> mine;
+    for (int32_t i = shard; i < (int32_t)plan.size(); i += nshards) mine.push_back(i);
+    for (size_t b = 0; b < mine.size(); b += (size_t)batch) {
+        const size_t e = std::min(mine.size(), b + (size_t)batch);
+        std::vector<pf::Job> jobs(e - b);
+        for (size_t x = b; x < e; ++x) {
+            const PlanEntry& pe = plan[mine[x]];
+            pf::Job& J = jobs[x - b];
+            J.kind = pf::kJobCollab;
+            J.uid = pe.uid;
+            J.topk = pe.hold_k;
+            J.limit = 1000;  // test.cpp:75
+            J.view.base = &base;
+            J.view.over = &over;
+            J.view.version = mine[x];
+        }
+        const int rc = pf::run_jobs(ctx, jobs);
+        if (rc != PF_OK) return rc;
+        for (size_t x = b; x < e; ++x) {
+            const PlanEntry& pe = plan[mine[x]];
+            const auto& out = jobs[x - b].out;
+            int hits = 0;
+            for (int i = 0; i < (int)out.size() && i < pe.hold_k; ++i)
+                if (pe.held.find(out[i].first) != pe.held.end()) ++hits;
+            if (mine[x] < cap) out_ratio[mine[x]] = (double)hits / (double)pe.hold_k;
+        }
+    }
+    return PF_OK;
+}
+
+int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
+                                 int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, int32_t cap,
+                                 int32_t* n_plan) {
+    if (!ctx || !ds || !n_plan || (cap > 0 && (!out_hits || !out_club)) || bad_shard(shard, nshards, batch))
+        return PF_EINVAL;
+    const std::vector<PlanEntry> plan = plan_rec(ds, sample_size);
+    *n_plan = (int32_t)plan.size();
+    const auto& base = pf::base_adj(ctx);
+    std::vector<int32_t> mine;
+    for (int32_t i = shard; i < (int32_t)plan.size(); i += nshards) mine.push_back(i);
+    for (size_t b = 0; b < mine.size(); b += (size_t)batch) {
+        const size_t e = std::min(mine.size(), b + (size_t)batch);
+        // per user: graph (= interest, recommender_graph.cpp:224-227), collaborative, clubs; limit 5000
+        std::vector<pf::Job> jobs(3 * (e - b));
+        for (size_t x = b; x < e; ++x) {
+            const PlanEntry& pe = plan[mine[x]];
+            for (int kind = 0; kind < 3; ++kind) {
+                pf::Job& J = jobs[3 * (x - b) + kind];
+                J.kind = kind == 0 ? pf::kJobInterest : (kind == 1 ? pf::kJobCollab : pf::kJobClubs);
+                J.uid = pe.uid;
+                J.topk = topk;
+                J.limit = 5000;
+                J.view.base = &base;  // a fresh adj_mod per user: only its own row edited
+                J.view.own = pe.uid;
+                J.view.own_row = &pe.newf;
+            }
+        }
+        const int rc = pf::run_jobs(ctx, jobs);
+        if (rc != PF_OK) return rc;
+        for (size_t x = b; x < e; ++x) {
+            const int32_t i = mine[x];
+            if (i >= cap) continue;
+            const PlanEntry& pe = plan[i];
+            auto any_held = [&](const pf::Job& J) {
+                for (auto& kv : J.out)
+                    if (pe.held.find(kv.first) != pe.held.end()) return true;
+                return false;
+            };
+            const pf::Job& g = jobs[3 * (x - b)];
+            out_hits[3 * (size_t)i] = (int8_t)any_held(g);
+            out_hits[3 * (size_t)i + 1] = (int8_t)any_held(jobs[3 * (x - b) + 1]);
+            out_hits[3 * (size_t)i + 2] = (int8_t)any_held(g);
+            const auto& row = ds->rows[ds->profiles.find(pe.uid)->second];
+            std::unordered_set<int> actual;
+            for (uint32_t c : row.clubs) actual.insert((int)c);
+            out_club[2 * (size_t)i] = NAN;
+            out_club[2 * (size_t)i + 1] = NAN;
+            if (!actual.empty()) {
+                const auto& cl = jobs[3 * (x - b) + 2].out;
+                int hit = 0;
+                for (int j = 0; j < (int)cl.size() && j < topk; ++j)
+                    if (actual.find(cl[j].first) != actual.end()) ++hit;
+                out_club[2 * (size_t)i] = (double)hit / (double)topk;
+                out_club[2 * (size_t)i + 1] = (double)hit / (double)actual.size();
+            }
+        }
     }
     return PF_OK;
 }

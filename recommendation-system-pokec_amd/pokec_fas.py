@@ -30,7 +30,8 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
-              "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests"]
+              "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests",
+              "pf_eval_holdout_friends", "pf_eval_recommendation_tests"]
 PF_LOAD_REFERENCE_CAP = 100000
 
 
@@ -104,6 +105,8 @@ def lib():
         L.pf_compute_normalizers.argtypes = [V, I32, I32, ctypes.c_char_p, V, V]
         L.pf_holdout_friends.argtypes = [V, V, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_recommendation_tests.argtypes = [V, V, I32, I32, V]
+        L.pf_eval_holdout_friends.argtypes = [V, V, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_eval_recommendation_tests.argtypes = [V, V, I32, I32, I32, I32, I32, V, V, I32, ctypes.POINTER(I32)]
         _lib = L
     return _lib
 
@@ -340,3 +343,53 @@ class Dataset:
         rc = self._L.pf_recommendation_tests(eng.h, self.h, sample_size, topk, out.ctypes.data)
         eng._check(rc, "pf_recommendation_tests")
         return out
+
+    # -- batched, sharded drivers (F1, cfg 5): per-plan-entry results of this shard, NaN / -1 elsewhere
+    def eval_holdout_friends(self, eng, sample_size, shard=0, nshards=1, batch=256):
+        cap = max(int(sample_size), 1)
+        out = np.full(cap, np.nan)
+        n = ctypes.c_int32()
+        rc = self._L.pf_eval_holdout_friends(eng.h, self.h, sample_size, shard, nshards, batch, out.ctypes.data, cap,
+                                             ctypes.byref(n))
+        eng._check(rc, "pf_eval_holdout_friends")
+        return out[:n.value]
+
+    def eval_recommendation_tests(self, eng, sample_size, topk, shard=0, nshards=1, batch=128):
+        cap = max(int(sample_size), 1)
+        hits = np.full((cap, 3), -1, np.int8)
+        club = np.full((cap, 2), np.nan)
+        n = ctypes.c_int32()
+        rc = self._L.pf_eval_recommendation_tests(eng.h, self.h, sample_size, topk, shard, nshards, batch,
+                                                  hits.ctypes.data, club.ctypes.data, cap, ctypes.byref(n))
+        eng._check(rc, "pf_eval_recommendation_tests")
+        return hits[:n.value], club[:n.value]
+
+
+def merge_shards(parts):
+    """Entries of plan arrays filled by shards s = 0..n-1 (entry i belongs to shard i % n)."""
+    parts = [np.asarray(p) for p in parts]
+    out = parts[0].copy()
+    for s, p in enumerate(parts):
+        out[s::len(parts)] = p[s::len(parts)]
+    return out
+
+
+def rec_tests_summary(hits, club):
+    """run_recommendation_tests_sample's five averages from per-user entries, summed in plan
+    order exactly like recommendation_tests.cpp:130-169."""
+    out = np.zeros(5, np.float64)
+    n = len(hits)
+    if n:
+        for j in range(3):
+            out[j] = float(int(np.sum(hits[:, j], dtype=np.int64))) / float(n)
+    prec = rec = 0.0
+    users = 0
+    for p, r in club:
+        if p == p:  # not NaN: the user has clubs
+            prec += float(p)
+            rec += float(r)
+            users += 1
+    if users:
+        out[3] = prec / users
+        out[4] = rec / users
+    return out

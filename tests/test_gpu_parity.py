@@ -360,3 +360,29 @@ def test_full_size_kernels_agree():
         assert list(uids) == list(post[i][0])
         assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32))
     eng.close()
+
+
+def test_batched_sharded_holdout_drivers_equal_sequential():
+    """F1 / cfg 5: the batched drivers (adjacency views instead of edits, users batched and
+    sharded) reproduce the sequential drivers bit for bit on corpus A, for 1 and 3 shards and
+    batch sizes 1 and 64 (test.cpp's cumulative edits included)."""
+    import tempfile
+    pf = tl.product()
+    m = tl.manifest()["corpora"]["A"]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        ds = pf.Dataset(d)
+    eng = pf.FasEngine(ds.desc_ptr(), 0)
+    seq = ds.holdout_friends(eng, m["holdout"])
+    seq5 = ds.recommendation_tests(eng, m["rectest"], 10)
+    for nshards, batch in ((1, 64), (3, 1), (3, 64)):
+        parts = [ds.eval_holdout_friends(eng, m["holdout"], s, nshards, batch) for s in range(nshards)]
+        got = pf.merge_shards(parts)
+        assert np.array_equal(got.view(np.uint64), seq.view(np.uint64)), (nshards, batch)
+        hp = [ds.eval_recommendation_tests(eng, m["rectest"], 10, s, nshards, batch) for s in range(nshards)]
+        hits = pf.merge_shards([h for h, _ in hp])
+        club = pf.merge_shards([c for _, c in hp])
+        assert (hits >= 0).all()
+        assert list(pf.rec_tests_summary(hits, club)) == list(seq5), (nshards, batch)
+    # the engine's own adjacency is untouched: the sequential driver still matches
+    assert np.array_equal(ds.holdout_friends(eng, m["holdout"]).view(np.uint64), seq.view(np.uint64))

@@ -75,7 +75,7 @@ struct pf_ctx {
     DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
     pf::DevStore ds{};
     // workspaces
-    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part;
+    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
     int32_t tile_begin = 0, tile_end = 0;
     // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
     pf::HostPost hp;
@@ -467,36 +467,47 @@ namespace pf {
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c) { return c->hc.adj; }
 
 // Every job's FAS pairs in two GPU stages (stage 2: the clubs recommender's friend-of-friend
-// pairs, which depend on stage 1's friend weights), then the reference's host arithmetic.
+// pairs, which depend on stage 1's friend weights), the collaborative sums in one K4 launch,
+// then the reference's host arithmetic.  The per-job host work runs on threads.
+template <class F>
+static void par_jobs(size_t n, F f) {
+    const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / 4, std::thread::hardware_concurrency())));
+    if (th <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (size_t w = 0; w < th; ++w)
+        ts.emplace_back([&, w]() {
+            for (size_t i = w; i < n; i += th) f(i);
+        });
+    for (auto& t : ts) t.join();
+}
+
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
     const auto& hc = c->hc;
     const auto& slot_of = c->hs.slot_of_idx;
     struct St {
         int32_t iq = -1;
         int g0 = -1, g1 = -1;             // stage-1 groups
+        std::vector<std::pair<int32_t, std::vector<int32_t>>> groups;  // (query idx, candidate slots)
         std::vector<int32_t> cuid;        // interest / collab: candidate uids of the scored pairs
         std::vector<int32_t> friends;     // collab / clubs: the query's adjacency row
         std::vector<int32_t> fidx, fuid;  // distinct friends with a profile
         std::unordered_map<int32_t, int32_t> fpos;
         std::vector<int32_t> grp;         // clubs: stage-2 group per friend
+        int64_t coff = -1;                // collab: offset of its sums
     };
     std::vector<St> st(jobs.size());
-    std::vector<int32_t> qidx;
-    std::vector<std::vector<int32_t>> slots;
-    auto add = [&](int32_t q, std::vector<int32_t>&& sl) {
-        qidx.push_back(q);
-        slots.push_back(std::move(sl));
-        return (int)qidx.size() - 1;
-    };
-    for (size_t i = 0; i < jobs.size(); ++i) {
+    par_jobs(jobs.size(), [&](size_t i) {
         Job& J = jobs[i];
         St& S = st[i];
         J.out.clear();
         const int32_t u = J.uid;
-        if (J.topk <= 0) continue;
+        if (J.topk <= 0) return;
         if (J.kind == kJobInterest) {
             S.iq = hc.idx_of(u);
-            if (S.iq < 0) continue;  // recommender_graph.cpp:39-40
+            if (S.iq < 0) return;  // recommender_graph.cpp:39-40
             std::unordered_set<int32_t> skip;
             if (const std::vector<int32_t>* r = J.view.row(u)) skip.insert(r->begin(), r->end());
             skip.insert(u);
@@ -513,12 +524,12 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
                     S.cuid.push_back(x);
                 }
             }
-            S.g0 = add(S.iq, std::move(sl));
+            S.groups.emplace_back(S.iq, std::move(sl));
         } else if (J.kind == kJobCollab) {
             if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
             std::vector<int32_t> cand = gather_collab(J.view, u, J.limit);
             S.iq = hc.idx_of(u);
-            if (S.iq < 0) continue;  // recommender_graph.cpp:130
+            if (S.iq < 0) return;  // recommender_graph.cpp:130
             for (int32_t f : S.friends) {  // distinct friends with a profile -> matrix rows
                 const int32_t ix = hc.idx_of(f);
                 if (ix < 0 || S.fpos.count(f)) continue;
@@ -536,12 +547,11 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
             // sim_u_f (float, recommender_graph.cpp:132-136), then M[f][c]
             std::vector<int32_t> fs;
             for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
-            S.g0 = add(S.iq, std::move(fs));
-            for (int32_t ix : S.fidx) S.g1 = add(ix, std::vector<int32_t>(cs));
-            S.g1 = S.g0 + 1;
+            S.groups.emplace_back(S.iq, std::move(fs));
+            for (int32_t ix : S.fidx) S.groups.emplace_back(ix, cs);
         } else {
             S.iq = hc.idx_of(u);
-            if (S.iq < 0) continue;  // recommender_clubs.cpp:13-16
+            if (S.iq < 0) return;  // recommender_clubs.cpp:13-16
             if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
             for (int32_t f : S.friends) {  // pass 1: w_f = FAS(q, f) for distinct friends with a profile
                 const int32_t ix = hc.idx_of(f);
@@ -552,19 +562,29 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
             }
             std::vector<int32_t> fs;
             for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
-            S.g0 = add(S.iq, std::move(fs));
+            S.groups.emplace_back(S.iq, std::move(fs));
         }
+    });
+    std::vector<int32_t> qidx;
+    std::vector<std::vector<int32_t>> slots;
+    for (St& S : st) {
+        if (S.groups.empty()) continue;
+        S.g0 = (int)qidx.size();
+        S.g1 = S.g0 + 1;
+        for (auto& g : S.groups) {
+            qidx.push_back(g.first);
+            slots.push_back(std::move(g.second));
+        }
+        S.groups.clear();
     }
     std::vector<std::vector<float>> res;
     int rc = run_pairs(c, qidx, slots, res);
     if (rc != PF_OK) return rc;
     // stage 2: FAS(f, fof) for every fof of every positive-weight friend (clubs)
-    std::vector<int32_t> qidx2;
-    std::vector<std::vector<int32_t>> slots2;
-    for (size_t i = 0; i < jobs.size(); ++i) {
+    par_jobs(jobs.size(), [&](size_t i) {
         Job& J = jobs[i];
         St& S = st[i];
-        if (J.kind != kJobClubs || S.iq < 0 || J.topk <= 0) continue;
+        if (J.kind != kJobClubs || S.iq < 0 || J.topk <= 0) return;
         const std::vector<float>& w = res[S.g0];
         S.grp.assign(S.fidx.size(), -1);
         for (size_t r = 0; r < S.fidx.size(); ++r) {
@@ -578,85 +598,114 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
                 if (ix < 0) continue;
                 sl.push_back(slot_of[ix]);
             }
-            S.grp[r] = (int32_t)qidx2.size();
-            qidx2.push_back(S.fidx[r]);
-            slots2.push_back(std::move(sl));
+            S.grp[r] = (int32_t)S.groups.size();
+            S.groups.emplace_back(S.fidx[r], std::move(sl));
         }
+    });
+    std::vector<int32_t> qidx2;
+    std::vector<std::vector<int32_t>> slots2;
+    std::vector<int32_t> gbase(jobs.size(), 0);
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        gbase[i] = (int32_t)qidx2.size();
+        for (auto& g : st[i].groups) {
+            qidx2.push_back(g.first);
+            slots2.push_back(std::move(g.second));
+        }
+        st[i].groups.clear();
     }
     std::vector<std::vector<float>> res2;
     rc = run_pairs(c, qidx2, slots2, res2);
     if (rc != PF_OK) return rc;
-    // collaborative sums on the GPU (K4), all collab jobs in one pass per job
-    for (size_t i = 0; i < jobs.size(); ++i) {
-        Job& J = jobs[i];
-        St& S = st[i];
-        if (J.topk <= 0 || S.iq < 0) continue;
-        Ranked r;
-        if (J.kind == kJobInterest) {
-            const std::vector<float>& sc = res[S.g0];
-            r.reserve(sc.size());
-            for (size_t j = 0; j < sc.size(); ++j) r.emplace_back(S.cuid[j], sc[j]);
-        } else if (J.kind == kJobCollab) {
+    // collaborative sums (K4): every collab job of the batch in one launch
+    {
+        std::vector<CollabSum> cj;
+        std::vector<float> M, w;
+        std::vector<int32_t> wrow;
+        int64_t ctot = 0;
+        int max_nc = 0;
+        for (size_t i = 0; i < jobs.size(); ++i) {
+            St& S = st[i];
+            if (jobs[i].kind != kJobCollab || S.iq < 0 || jobs[i].topk <= 0 || S.cuid.empty()) continue;
             const int F = (int)S.friends.size(), nc = (int)S.cuid.size();
-            if (nc == 0) continue;
-            std::vector<float> w(F, 0.f), M((size_t)S.fidx.size() * nc);
-            std::vector<int32_t> wrow(F, -1);
+            CollabSum js{(int64_t)M.size(), ctot, (int32_t)w.size(), F, nc, 0};
             for (int j = 0; j < F; ++j) {
                 auto rt = S.fpos.find(S.friends[j]);
-                if (rt == S.fpos.end()) continue;
-                wrow[j] = rt->second;
-                w[j] = res[S.g0][rt->second];
+                wrow.push_back(rt == S.fpos.end() ? -1 : rt->second);
+                w.push_back(rt == S.fpos.end() ? 0.f : res[S.g0][rt->second]);
             }
-            for (size_t rr = 0; rr < S.fidx.size(); ++rr)
-                std::copy(res[S.g1 + rr].begin(), res[S.g1 + rr].end(), M.begin() + rr * nc);
+            for (size_t rr = 0; rr < S.fidx.size(); ++rr) M.insert(M.end(), res[S.g1 + rr].begin(), res[S.g1 + rr].end());
+            S.coff = ctot;
+            ctot += nc;
+            max_nc = std::max(max_nc, nc);
+            cj.push_back(js);
+        }
+        std::vector<float> sums((size_t)ctot);
+        if (!cj.empty()) {
             HIPCHK(c, upload(c, c->d_scores, M));
             HIPCHK(c, upload(c, c->d_w, w));
             HIPCHK(c, upload(c, c->d_wrow, wrow));
-            HIPCHK(c, c->d_csum.ensure((size_t)nc * sizeof(float)));
-            HIPCHK(c, pf::launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(), F, nc,
-                                            c->d_csum.as<float>(), c->stream));
-            std::vector<float> sc(nc);
-            HIPCHK(c, hipMemcpyAsync(sc.data(), c->d_csum.p, nc * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, upload(c, c->d_cjobs, cj));
+            HIPCHK(c, c->d_csum.ensure((size_t)ctot * sizeof(float)));
+            for (size_t b = 0; b < cj.size(); b += 65535)
+                HIPCHK(c, launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(),
+                                            c->d_cjobs.as<CollabSum>() + b, (int)std::min<size_t>(65535, cj.size() - b),
+                                            max_nc, c->d_csum.as<float>(), c->stream));
+            HIPCHK(c, hipMemcpyAsync(sums.data(), c->d_csum.p, sums.size() * sizeof(float), hipMemcpyDeviceToHost,
+                                     c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            for (int j = 0; j < nc; ++j) r.emplace_back(S.cuid[j], sc[j]);
-        } else {
-            // club accumulation in the reference's exact loop order (double sums)
-            const std::vector<float>& w = res[S.g0];
-            std::unordered_set<int32_t> own;
-            for (int64_t k = hc.club_off[S.iq]; k < hc.club_off[S.iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
-            std::unordered_map<int32_t, double> score;
-            for (int32_t f : S.friends) {
-                auto pt = S.fpos.find(f);
-                if (pt == S.fpos.end()) continue;
-                const double wf = w[pt->second];
-                if (wf <= 0.0) continue;
-                const int32_t ix = S.fidx[pt->second];
-                for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                    if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
-            }
-            for (int32_t f : S.friends) {
-                auto pt = S.fpos.find(f);
-                if (pt == S.fpos.end()) continue;
-                const int32_t g = S.grp[pt->second];
-                const double wf = w[pt->second];
-                if (wf <= 0.0 || g < 0) continue;
-                const std::vector<int32_t>* rf = J.view.row(f);
-                size_t j = 0;
-                for (int32_t x : *rf) {
-                    if (x == J.uid) continue;
-                    const int32_t ix = hc.idx_of(x);
-                    if (ix < 0) continue;
-                    const double sv = res2[g][j++];
-                    if (sv <= 0.0) continue;
-                    const double addv = wf * sv;
-                    for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                        if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += addv;
-                }
-            }
-            for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
         }
-        rank(r, J.topk);
-        J.out = std::move(r);
+        par_jobs(jobs.size(), [&](size_t i) {
+            Job& J = jobs[i];
+            St& S = st[i];
+            if (J.topk <= 0 || S.iq < 0) return;
+            Ranked r;
+            if (J.kind == kJobInterest) {
+                const std::vector<float>& sc = res[S.g0];
+                r.reserve(sc.size());
+                for (size_t j = 0; j < sc.size(); ++j) r.emplace_back(S.cuid[j], sc[j]);
+            } else if (J.kind == kJobCollab) {
+                if (S.coff < 0) return;
+                for (size_t j = 0; j < S.cuid.size(); ++j) r.emplace_back(S.cuid[j], sums[S.coff + j]);
+            } else {
+                // club accumulation in the reference's exact loop order (double sums)
+                const std::vector<float>& wv = res[S.g0];
+                std::unordered_set<int32_t> own;
+                for (int64_t k = hc.club_off[S.iq]; k < hc.club_off[S.iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
+                std::unordered_map<int32_t, double> score;
+                for (int32_t f : S.friends) {
+                    auto pt = S.fpos.find(f);
+                    if (pt == S.fpos.end()) continue;
+                    const double wf = wv[pt->second];
+                    if (wf <= 0.0) continue;
+                    const int32_t ix = S.fidx[pt->second];
+                    for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                        if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
+                }
+                for (int32_t f : S.friends) {
+                    auto pt = S.fpos.find(f);
+                    if (pt == S.fpos.end()) continue;
+                    const int32_t g = S.grp[pt->second];
+                    const double wf = wv[pt->second];
+                    if (wf <= 0.0 || g < 0) continue;
+                    const std::vector<float>& sf = res2[gbase[i] + g];
+                    const std::vector<int32_t>* rf = J.view.row(f);
+                    size_t j = 0;
+                    for (int32_t x : *rf) {
+                        if (x == J.uid) continue;
+                        const int32_t ix = hc.idx_of(x);
+                        if (ix < 0) continue;
+                        const double sv = sf[j++];
+                        if (sv <= 0.0) continue;
+                        const double addv = wf * sv;
+                        for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
+                            if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += addv;
+                    }
+                }
+                for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
+            }
+            rank(r, J.topk);
+            J.out = std::move(r);
+        });
     }
     return PF_OK;
 }

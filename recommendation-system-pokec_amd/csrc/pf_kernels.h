@@ -34,7 +34,13 @@ hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int
 hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
                         bool gtab, const PairBlock* blocks, int nblocks, const int32_t* slots, float* out,
                         hipStream_t s);
-hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, int F, int nc, float* out,
-                             hipStream_t s);
+// one collaborative query of a K4 batch: M rows at moff ([rows][nc]), w / row at woff ([F]),
+// scores to out + coff ([nc])
+struct CollabSum {
+    int64_t moff, coff;
+    int32_t woff, F, nc, pad;
+};
+hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, const CollabSum* jobs, int njobs,
+                             int max_nc, float* out, hipStream_t s);
 
 }  // namespace pf

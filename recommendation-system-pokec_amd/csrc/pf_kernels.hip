@@ -1156,20 +1156,22 @@ __global__ __launch_bounds__(256) void fas_pairs_kernel(DevStore st, const uint8
 }
 
 // ---------------------------------------------------------------- K4: collaborative sum
-// score(c) = sum over friend-list positions j (in order) of (double)w[j] * (double)M[row[j]][c]
-// (recommender_graph.cpp:167-180); row[j] < 0 -> friend skipped.
+// For each collaborative query J (blockIdx.y): score(c) = sum over friend-list positions j (in
+// order) of (double)w[j] * (double)M[row[j]][c] (recommender_graph.cpp:167-180); row[j] < 0 ->
+// friend skipped.  One launch serves a batch of queries.
 __global__ __launch_bounds__(256) void collab_sum_kernel(const float* __restrict__ M, const float* __restrict__ w,
-                                                         const int32_t* __restrict__ row, int32_t F, int32_t nc,
-                                                         float* __restrict__ out) {
+                                                         const int32_t* __restrict__ row,
+                                                         const CollabSum* __restrict__ jobs, float* __restrict__ out) {
+    const CollabSum J = jobs[blockIdx.y];
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nc) return;
+    if (c >= J.nc) return;
     double s = 0.0;
-    for (int j = 0; j < F; ++j) {
-        const int r = row[j];
+    for (int j = 0; j < J.F; ++j) {
+        const int r = row[J.woff + j];
         if (r < 0) continue;
-        s += (double)w[j] * (double)M[(size_t)r * nc + c];
+        s += (double)w[J.woff + j] * (double)M[J.moff + (size_t)r * J.nc + c];
     }
-    out[c] = (float)s;
+    out[J.coff + c] = (float)s;
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1257,9 +1259,10 @@ hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef
     return hipGetLastError();
 }
 
-hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, int F, int nc, float* out, hipStream_t s) {
-    if (nc <= 0) return hipSuccess;
-    hipLaunchKernelGGL(collab_sum_kernel, dim3((nc + 255) / 256), dim3(256), 0, s, M, w, row, F, nc, out);
+hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, const CollabSum* jobs, int njobs,
+                             int max_nc, float* out, hipStream_t s) {
+    if (njobs <= 0 || max_nc <= 0) return hipSuccess;
+    hipLaunchKernelGGL(collab_sum_kernel, dim3((max_nc + 255) / 256, njobs), dim3(256), 0, s, M, w, row, jobs, out);
     return hipGetLastError();
 }
 

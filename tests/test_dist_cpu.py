@@ -67,3 +67,67 @@ def test_gloo_allgather_merge_equals_union_topk(world):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert ret.get(timeout=10) is True
+
+
+def _eval_worker(rank, world, port, ret):
+    """tools/eval_holdout.py's exchange: each rank fills the plan entries i % world == rank
+    (NaN / -1 elsewhere), one all-gather, merge_shards, averages in plan order."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "recommendation-system-pokec_amd"))
+    import pokec_fas as pf
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(3)
+    n = 101
+    ratios = rng.random(n)
+    hits = (rng.random((n, 3)) < 0.3).astype(np.int8)
+    club = rng.random((n, 2))
+    club[rng.random(n) < 0.4] = np.nan  # users without clubs
+    mine_r = np.full(n, np.nan)
+    mine_h = np.full((n, 3), -1, np.int8)
+    mine_c = np.full((n, 2), np.nan)
+    mine_r[rank::world] = ratios[rank::world]
+    mine_h[rank::world] = hits[rank::world]
+    mine_c[rank::world] = club[rank::world]
+
+    def gather(a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return [p.numpy() for p in parts]
+
+    r = pf.merge_shards(gather(mine_r))
+    h = pf.merge_shards(gather(mine_h))
+    c = pf.merge_shards(gather(mine_c))
+    if rank == 0:
+        ok = np.array_equal(r.view(np.uint64), ratios.view(np.uint64)) and np.array_equal(h, hits)
+        got = pf.rec_tests_summary(h, c)
+        # the sequential driver's arithmetic (recommendation_tests.cpp:130-169)
+        prec = rec = 0.0
+        users = 0
+        for p, q in club:
+            if p == p:
+                prec += p
+                rec += q
+                users += 1
+        ref = [hits[:, 0].sum() / n, hits[:, 1].sum() / n, hits[:, 2].sum() / n, prec / users, rec / users]
+        ok = ok and [float(x) for x in got] == [float(x) for x in ref]
+        ret.put(bool(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_eval_shards_merge_to_plan_order(world):
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, world, port, ret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert ret.get(timeout=10) is True

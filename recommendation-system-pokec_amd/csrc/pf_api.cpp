@@ -816,7 +816,15 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         c->ps.pnorm = c->d_pnorm.as<double>();
         c->ps.cells = c->d_cells.as<uint32_t>();
         c->ps.n = c->hc.n;
-        c->ps.n_blocks = (c->hc.n + pf::kBlockCands - 1) / pf::kBlockCands;
+        // block size: the LDS capacity.  Sizing blocks to fill whole waves of resident
+        // workgroups (798 at 1.6M) measured slower (258 vs 244 us): per-block costs dominate
+        // the half-empty last wave.  PF_K5_BLOCK overrides it (tests, experiments).
+        {
+            int64_t b = pf::kBlockCands;
+            if (const char* e = getenv("PF_K5_BLOCK")) b = strtol(e, nullptr, 10);
+            c->ps.bsize = (int32_t)std::max<int64_t>(64, std::min<int64_t>(pf::kBlockCands, b));
+        }
+        c->ps.n_blocks = (c->hc.n + c->ps.bsize - 1) / c->ps.bsize;
         c->wb_begin = 0;
         c->wb_end = c->ps.n_blocks;
     }

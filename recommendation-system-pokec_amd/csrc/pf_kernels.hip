@@ -799,9 +799,9 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 // ranges uint2[n_lists].  The tail merge reuses the tf-byte array.
 constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + 128 + 16;
 
-__device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0) {
-    const uint32_t cell = c0 >> L.shift;
-    return make_uint2(L.off + ps.cells[L.cell_off + cell], L.off + ps.cells[L.cell_off + cell + 1]);
+// entries of list L for candidates [c0, c1] (cells c0 >> shift .. c1 >> shift)
+__device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0, uint32_t c1) {
+    return make_uint2(L.off + ps.cells[L.cell_off + (c0 >> L.shift)], L.off + ps.cells[L.cell_off + (c1 >> L.shift) + 1]);
 }
 
 // Flattened walk over the entries of lists rng[0 .. nl): thread i takes flat entries
@@ -933,15 +933,17 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
     for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end; blk += (int)gridDim.x) {
-        const uint32_t c0 = (uint32_t)blk * kBlockCands;
+        const uint32_t B = (uint32_t)ps.bsize;
+        const uint32_t c0 = (uint32_t)blk * B;
+        const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
         // 1. ranges of every list in this block; headers of the owned candidates
         for (int j = tid; j < nl; j += kPostThreads)
-            rng[j] = list_range(ps, j < H.n_tok ? toks[j].l : sets[j - H.n_tok], c0);
+            rng[j] = list_range(ps, j < H.n_tok ? toks[j].l : sets[j - H.n_tok], c0, c1);
         uint4 ha[kCandsPerThread], hb[kCandsPerThread];
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
-            const bool a = c < (uint32_t)ps.n;
+            const bool a = c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B;
             ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
             hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
             cnt[kk * kPostThreads + tid] = 0u;
@@ -963,14 +965,14 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                 const uint32_t x = b + tid;
                 const uint32_t e = x < hi ? excl[x] : ~0u;
                 const uint32_t p = e - c0;
-                if (p < (uint32_t)kBlockCands) atomicOr(&exb[p >> 5], 1u << (p & 31));
-                if (__syncthreads_or(e >= c0 + kBlockCands)) break;  // sorted: the rest lies beyond the block
+                if (p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
+                if (__syncthreads_or(e >= c0 + B)) break;  // sorted: the rest lies beyond the block
             }
         }
         // 2. clubs / friends
         if (!(dbg & 4)) walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
             const uint32_t p = (e >> 8) - c0;
-            if (p < (uint32_t)kBlockCands) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
+            if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
         __syncthreads();
         // 3. fixed terms, recommender_similarity.cpp:38-91
@@ -982,7 +984,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const int p = kk * kPostThreads + tid;
             const uint32_t ct = cnt[p];
-            if (c0 + p >= (uint32_t)ps.n || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
+            if ((uint32_t)p >= B || c0 + p > c1 || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
             const uint64_t cm = (uint64_t)ha[kk].x | ((uint64_t)(ha[kk].y & 0xFFFFu) << 32);
             pend[kk] = cm & q.colmask;
             double s = 0.0;
@@ -1024,7 +1026,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                 const bool last = js + kChunkToks >= col.j1;
                 if (!(dbg & 1)) walk_chunk(ps, rng, gpre, js, nj, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
-                    if (p < (uint32_t)kBlockCands) {
+                    if (p < B) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
                         nrm[p] = nv;
                     }

@@ -169,14 +169,14 @@ struct DevStore {
 // candidates holding it, so a query reads only the lists it names instead of every record.
 // Candidates are in idx order (ascending uid, the reference's tie-break order); a workgroup
 // scores one block of kBlockCands consecutive candidates at a time.
-constexpr int kBlockCands = 1024;          // candidates per workgroup block (4 per thread)
+constexpr int kBlockCands = 1024;          // LDS capacity of a workgroup block (4 candidates per thread)
 constexpr int kPostWaves = 4;              // waves per K5 workgroup
 constexpr int kPostThreads = kPostWaves * kWave;
 constexpr int kCandsPerThread = kBlockCands / kPostThreads;
 constexpr int kChunkToks = 8;              // query tokens of one column handled per pass (one tf byte each)
 constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
 constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
-constexpr int kPostMinShift = 10;          // log2(kBlockCands): a cell never splits a block
+constexpr int kPostMinShift = 9;           // cells of >= 512 candidates: a block spans at most 3
 
 // One candidate list: entries [off, off + len) of the postings array, sorted by idx.
 // cells[cell_off + c] = first entry (relative) with idx >= c << shift, c = 0 .. ncells,
@@ -213,7 +213,8 @@ struct PostStore {
     const double* pnorm;      // [token entries] sqrt(sum (tf*idf)^2) of the entry's (candidate, column)
     const uint32_t* cells;
     int32_t n;                // candidates
-    int32_t n_blocks;         // ceil(n / kBlockCands)
+    int32_t n_blocks;         // ceil(n / bsize)
+    int32_t bsize;            // candidates per block (<= kBlockCands), chosen so the blocks fill whole waves of resident workgroups
 };
 
 }  // namespace pf

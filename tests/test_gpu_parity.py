@@ -188,8 +188,11 @@ def test_big_top64_vs_oracle(big, kernel):
                                  {"PF_SCAN": "stream", "PF_STAGE_LIMIT": "1024"},
                                  {"PF_SCAN": "stream", "PF_TILE_STEPS": "3"},
                                  {"PF_SCAN": "stream", "PF_TILE_STEPS": "1", "PF_STAGE_LIMIT": "0"},
-                                 {"PF_SCAN": "postings"}],
-                         ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings"])
+                                 {"PF_SCAN": "postings"},
+                                 {"PF_SCAN": "postings", "PF_K5_BLOCK": "64"},
+                                 {"PF_SCAN": "postings", "PF_K5_BLOCK": "333"}],
+                         ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings",
+                              "postings-block64", "postings-block333"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
     query of the batch has tables above 1 KiB (the whole launch then probes global);

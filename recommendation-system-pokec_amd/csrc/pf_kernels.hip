@@ -566,7 +566,7 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
 
 // Block-level end of a scan: merge the 4 wave lists, publish the block's k-list and, in
 // the last block of the query, merge every block's list into out[row] (no second launch).
-// sc: LDS >= 4 * k keys; misc: LDS >= 16 + 4 * kMaxTopK bytes (both idle by now).
+// sc: LDS >= (waves) * k keys; misc: LDS >= 16 + 4 * kMaxTopK bytes (both idle by now).
 __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
                                           uint64_t* __restrict__ parts, uint64_t* __restrict__ out,
                                           const int32_t* __restrict__ out_rows) {
@@ -589,7 +589,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
     int* s_blk = s_flag + 4;
     if (wave == 0) {
         uint64_t acc = ~0ull;
-        const int n = (kScanThreads / 64) * k;
+        const int n = (int)(blockDim.x >> 6) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         if (lane < k) st_agent(qparts + (size_t)blockIdx.x * k + lane, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -610,7 +610,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
     const int j = min(k, max(1, (2 * k + nb - 1) / nb));
     const int n1 = nb * j;
     list = ~0ull;
-    for (int base = wave * 512; base < n1; base += kScanThreads * 8) {
+    for (int base = wave * 512; base < n1; base += (int)blockDim.x * 8) {
         uint64_t x[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -628,7 +628,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
     __syncthreads();
     uint64_t acc = ~0ull;
     if (wave == 0) {
-        const int n = (kScanThreads / 64) * k;
+        const int n = (int)(blockDim.x >> 6) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         if (lane == 0) *s_T = rdlane64(acc, k - 1);
     }
@@ -638,7 +638,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
         // fewer than k keys among the first j of every block: merge every list in full
         list = ~0ull;
         const int total = nb * k;
-        for (int base = wave * 512; base < total; base += kScanThreads * 8) {
+        for (int base = wave * 512; base < total; base += (int)blockDim.x * 8) {
             uint64_t x[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -653,7 +653,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
         __syncthreads();
         if (wave == 0) {
             acc = ~0ull;
-            const int n = (kScanThreads / 64) * k;
+            const int n = (int)(blockDim.x >> 6) * k;
             for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
             if (lane < k) out[(size_t)row * k + lane] = acc;
         }
@@ -661,7 +661,7 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
     }
     // Pass 2: the remaining keys of the blocks whose j-th key is <= T
     if (j < k) {
-        for (int b = (int)threadIdx.x; b < nb; b += kScanThreads) {
+        for (int b = (int)threadIdx.x; b < nb; b += (int)blockDim.x) {
             const uint64_t y = ld_agent(qparts + (size_t)b * k + (j - 1));
             if (y <= T) {
                 const int p = atomicAdd(s_cnt, 1);
@@ -797,7 +797,7 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 // LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
 // (later the compacted list) | exclusion bits u32[32] | misc u32[4] | QVal[n_tok] |
 // ranges uint2[n_lists].  The tail merge reuses the tf-byte array.
-constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + 128 + 16;
+constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16;
 
 // entries of list L for candidates [c0, c1] (cells c0 >> shift .. c1 >> shift)
 __device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0, uint32_t c1) {
@@ -914,7 +914,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kBlockCands * 24);
     uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
-    uint32_t* nlist = exb + 32;
+    uint32_t* nlist = exb + kBlockCands / 32;
     QVal* qv = reinterpret_cast<QVal*>(base + kPostFixedLds);
     uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + 16 * H.n_tok);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
@@ -948,7 +948,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
             cnt[kk * kPostThreads + tid] = 0u;
         }
-        if (tid < 32) exb[tid] = 0u;
+        if (tid < kBlockCands / 32) exb[tid] = 0u;
         __syncthreads();
         if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
@@ -1101,7 +1101,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         }
     }
     // tail scratch in the (idle) tf-byte array: merge keys, then flag / threshold / block ids
-    scan_tail(best, k, tfv, reinterpret_cast<int*>(tfv + 4 * kMaxTopK), sync, parts, out, out_rows);
+    scan_tail(best, k, tfv, reinterpret_cast<int*>(tfv + kPostWaves * kMaxTopK), sync, parts, out, out_rows);
 }
 
 // ---------------------------------------------------------------- K2: merge

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "pf_kernels.h"
@@ -1212,7 +1213,9 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 static uint32_t post_dbg() {
     static const uint32_t v = [] {
         const char* e = getenv("PF_K5_DBG");
-        return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+        const uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+        if (x) fprintf(stderr, "pokec_fas: PF_K5_DBG=%#x switches postings-scan phases off; scores are wrong\n", x);
+        return x;
     }();
     return v;
 }

@@ -945,8 +945,8 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
             const bool a = c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B;
-            ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
-            hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
+            ha[kk] = (a && !(dbg & 128)) ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
+            hb[kk] = (a && !(dbg & 128)) ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
             cnt[kk * kPostThreads + tid] = 0u;
         }
         if (tid < kBlockCands / 32) exb[tid] = 0u;
@@ -990,6 +990,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             pend[kk] = cm & q.colmask;
             double s = 0.0;
             int u = 0;
+            if (dbg & 32) { sum[kk] = 0.0; used[kk] = 1; continue; }
             const uint32_t pb = (ha[kk].y >> 16) & 0xFFu, gb = ha[kk].y >> 24;
             if (q.pubcode != kCodeMissing && pb != kCodeMissing) { s += q.sig_pub[pb == q.pubcode]; ++u; }
             if (q.gencode != kCodeMissing && gb != kCodeMissing) { s += q.sig_gen[gb == q.gencode]; ++u; }
@@ -1081,6 +1082,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             }
         }
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
+        uint64_t keys[kCandsPerThread];
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             while (pend[kk]) {
@@ -1098,7 +1100,20 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                 }
                 key = score_key(f, (int32_t)hb[kk].w);
             }
-            topk_push(best, key, k, lane);
+            keys[kk] = key;
+        }
+        // each lane's 4 keys ascending, then pushed best-first: after the first push the
+        // wave's threshold rejects most of the rest, so at most one 64-key sort per block
+        static_assert(kCandsPerThread == 4, "4-key sorting network");
+        auto cas = [&](int a, int b) {
+            const uint64_t x = keys[a], y = keys[b];
+            keys[a] = x < y ? x : y;
+            keys[b] = x < y ? y : x;
+        };
+        cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+        if (!(dbg & 64)) {
+#pragma unroll
+            for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         }
     }
     // tail scratch in the (idle) tf-byte array: merge keys, then flag / threshold / block ids
@@ -1209,7 +1224,8 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 }
 
 // PF_K5_DBG: bit mask that switches K5 phases off (profiling only; results are wrong then):
-// 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions
+// 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions, 32 fixed terms,
+// 64 top-k pushes, 128 header loads
 static uint32_t post_dbg() {
     static const uint32_t v = [] {
         const char* e = getenv("PF_K5_DBG");

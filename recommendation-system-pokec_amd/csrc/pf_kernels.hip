@@ -790,15 +790,24 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 //   3. fixed terms (public .. friends) per owned candidate from its 32-B header;
 //   4. text, one active query column at a time in ascending order: the column's token
 //      lists (<= 8 tokens per pass) write each hit's tf byte at [candidate][token] and its
-//      (candidate, column) norm; the hit candidates are compacted, and their dot (ascending
-//      tid: token order) and cosine -> sigmoid term are computed densely, one candidate per
+//      (candidate, column) norm; each wave lists its hit candidates in its own segment
+//      (ballot + popcount, no atomics), and their dot (ascending tid: token order, only the
+//      hit bytes visited) and cosine -> sigmoid term are computed densely, one candidate per
 //      thread, so the FP64 divisions and exp never run on idle lanes; the owners then add
 //      the column's term, or the s = 0 term of a common column without hits, in the
 //      reference's order (recommender_similarity.cpp:38-113).
 // LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
-// (later the compacted list) | exclusion bits u32[32] | misc u32[4] | QVal[n_tok] |
-// ranges uint2[n_lists].  The tail merge reuses the tf-byte array.
+// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | per-wave hit counts u32[4] |
+// PTok[n_tok] | ranges uint2[n_lists] | prefix u32[n_tok + 1].  The tail merge reuses the
+// tf-byte array.
 constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16;
+static_assert(kPostWaves == 4, "per-wave hit counts live in the 4 misc words");
+
+// A query token in LDS: its weight and idf, and the products for tf = 1 and 2 (the common
+// cases), each computed as the reference does, wq * (tf * idf) (recommender.cpp:74-85).
+struct PTok {
+    double p1, p2, wq, idf;
+};
 
 // entries of list L for candidates [c0, c1] (cells c0 >> shift .. c1 >> shift)
 __device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0, uint32_t c1) {
@@ -865,7 +874,7 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
 // steps.  Two entries per thread and group of 512, loaded together, then f(list - js, entry, norm).
 template <class F>
 __device__ __forceinline__ void walk_chunk(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
-                                           F f) {
+                                           uint32_t dbg, uint32_t c0, F f) {
     static_assert(kChunkToks <= 8, "3 bisection steps cover 8 lists");
     const uint32_t base = gpre[js], total = gpre[js + nj] - base;
     for (uint32_t f0 = 0; f0 < total; f0 += 2 * kPostThreads) {
@@ -885,12 +894,17 @@ __device__ __forceinline__ void walk_chunk(const PostStore& ps, const uint2* rng
         double nv[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            ent[u] = jj[u] >= 0 ? ps.post[xs[u]] : 0u;
-            nv[u] = jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
+            if (dbg & 512) {  // no loads: a synthetic hit per flat entry
+                ent[u] = jj[u] >= 0 ? ((c0 + xs[u] % 1024u) << 8 | 1u) : 0u;
+                nv[u] = 1.0;
+            } else {
+                ent[u] = jj[u] >= 0 ? ps.post[xs[u]] : 0u;
+                nv[u] = jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
+            }
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-            if (jj[u] >= 0) f(jj[u] - js, ent[u], nv[u]);
+            if (jj[u] >= 0 && (!(dbg & 256) || (ent[u] == 0xFFFFFFFFu && nv[u] == -1.0))) f(jj[u] - js, ent[u], nv[u]);
     }
 }
 
@@ -916,21 +930,22 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
     uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
     uint32_t* nlist = exb + kBlockCands / 32;
-    QVal* qv = reinterpret_cast<QVal*>(base + kPostFixedLds);
-    uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + 16 * H.n_tok);
+    PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
+    uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + sizeof(PTok) * H.n_tok);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
     const int nsets = H.n_club + H.n_friend;
     const int nl = H.n_tok + nsets;
     stage(smem, img, sizeof(QConst));
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
-        QVal v;
+        PTok v;
         v.wq = toks[j].wq;
         v.idf = toks[j].idf;
-        qv[j] = v;
+        v.p1 = v.wq * (1.0 * v.idf);
+        v.p2 = v.wq * (2.0 * v.idf);
+        pt[j] = v;
     }
 #pragma unroll
     for (int kk = 0; kk < kCandsPerThread; ++kk) tfv[kk * kPostThreads + tid] = 0ull;
-    if (tid == 0) *nlist = 0u;
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
     for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end; blk += (int)gridDim.x) {
@@ -978,7 +993,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
         __syncthreads();
         // 3. fixed terms, recommender_similarity.cpp:38-91
         double sum[kCandsPerThread];
-        int used[kCandsPerThread];
+        uint32_t used = 0;  // byte kk: terms used by candidate kk (<= 7 + 48)
         uint64_t pend[kCandsPerThread];
         uint32_t skip = 0;  // bit kk: candidate kk absent or excluded
 #pragma unroll
@@ -990,7 +1005,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             pend[kk] = cm & q.colmask;
             double s = 0.0;
             int u = 0;
-            if (dbg & 32) { sum[kk] = 0.0; used[kk] = 1; continue; }
+            if (dbg & 32) { sum[kk] = 0.0; used |= 1u << (8 * kk); continue; }
             const uint32_t pb = (ha[kk].y >> 16) & 0xFFu, gb = ha[kk].y >> 24;
             if (q.pubcode != kCodeMissing && pb != kCodeMissing) { s += q.sig_pub[pb == q.pubcode]; ++u; }
             if (q.gencode != kCodeMissing && gb != kCodeMissing) { s += q.sig_gen[gb == q.gencode]; ++u; }
@@ -1009,7 +1024,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             if (q.n_clubs > 0 && nc > 0) { s += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs); ++u; }
             if (q.n_friends > 0 && nf > 0) { s += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends); ++u; }
             sum[kk] = s;
-            used[kk] = u + __popcll(pend[kk]);
+            used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
         }
         __syncthreads();  // the counters' LDS now holds the compacted lists
         // 4. text columns, ascending
@@ -1026,7 +1041,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             for (int js = col.j0; js < col.j1; js += kChunkToks) {
                 const int nj = min(kChunkToks, col.j1 - js);
                 const bool last = js + kChunkToks >= col.j1;
-                if (!(dbg & 1)) walk_chunk(ps, rng, gpre, js, nj, [&](int j, uint32_t e, double nv) {
+                if (!(dbg & 1)) walk_chunk(ps, rng, gpre, js, nj, dbg, c0, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
                     if (p < B) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
@@ -1034,37 +1049,45 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                     }
                 });
                 __syncthreads();
+                {  // each wave lists its hit candidates in its own segment: no atomics
+                    uint16_t* wl = list + (tid >> 6) * (kBlockCands / kPostWaves);
+                    uint32_t nw = 0;
 #pragma unroll
-                for (int kk = 0; kk < kCandsPerThread; ++kk) {
-                    const int p = kk * kPostThreads + tid;
-                    if (tfv[p] != 0ull) colhit |= 1u << kk;
-                    const bool h = (colhit >> kk) & 1u;
-                    const uint64_t m = __ballot(h);
-                    if (m) {
-                        uint32_t b0 = 0;
-                        if (lane == 0) b0 = atomicAdd(nlist, (uint32_t)__popcll(m));
-                        b0 = __builtin_amdgcn_readfirstlane(b0);
-                        if (h) list[b0 + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                    for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                        const int p = kk * kPostThreads + tid;
+                        if (tfv[p] != 0ull) colhit |= 1u << kk;
+                        if (dbg & 2048) { tfv[p] = 0ull; continue; }
+                        const bool h = (colhit >> kk) & 1u;
+                        const uint64_t m = __ballot(h);
+                        if (h) wl[nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                        nw += (uint32_t)__popcll(m);
                     }
+                    if (lane == 0) nlist[tid >> 6] = nw;
                 }
                 __syncthreads();
-                const uint32_t n = *nlist;
+                const uint32_t n0 = nlist[0], n1 = nlist[1], n2 = nlist[2];
+                const uint32_t n = n0 + n1 + n2 + nlist[3];
                 for (uint32_t i = tid; i < n; i += kPostThreads) {
-                    const int p = list[i];
-                    const uint64_t v = tfv[p];
+                    uint32_t r = i, w = 0;  // item i -> (wave segment w, position r)
+                    if (r >= n0) { r -= n0; ++w; if (r >= n1) { r -= n1; ++w; if (r >= n2) { r -= n2; ++w; } } }
+                    const int p = list[w * (kBlockCands / kPostWaves) + r];
+                    uint64_t v = tfv[p];
                     tfv[p] = 0ull;
+                    if (dbg & 1024) { term[p] = (double)v; continue; }
                     double dot = multi ? term[p] : 0.0;
-                    for (int j = 0; j < nj; ++j) {
+                    while (v) {  // the hit tokens in ascending order
+                        const int j = (__ffsll((unsigned long long)v) - 1) >> 3;
                         const uint32_t tf = (uint32_t)(v >> (8 * j)) & 0xFFu;
-                        if (tf) {
-                            const QVal w = qv[js + j];
-                            dot += w.wq * ((double)tf * w.idf);
-                        }
+                        v &= ~(0xFFull << (8 * j));
+                        const double* pw = &pt[js + j].p1;  // p1, p2, wq, idf
+                        double x;
+                        if (tf <= 2u) x = pw[tf - 1u];
+                        else x = pw[2] * ((double)tf * pw[3]);
+                        dot += x;
                     }
                     term[p] = (!last || (dbg & 2)) ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
                 __syncthreads();
-                if (tid == 0) *nlist = 0u;
             }
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) {
@@ -1093,12 +1116,14 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
             uint64_t key = ~0ull;
             if (!((skip >> kk) & 1u)) {
                 float f = 0.0f;
-                if (used[kk] > 0) {
-                    const double S = sum[kk] / (double)used[kk];
-                    const double F = (double)used[kk] / (double)(kNumFixed + q.n_cols);
+                const int uk = (int)((used >> (8 * kk)) & 0xFFu);
+                if (uk > 0) {
+                    const double S = sum[kk] / (double)uk;
+                    const double F = (double)uk / (double)(kNumFixed + q.n_cols);
                     f = (S <= 0.0 && F <= 0.0) ? 0.0f : (float)((2.0 * S * F) / (S + F));
                 }
-                key = score_key(f, (int32_t)hb[kk].w);
+                // keyed by idx (idx order = uid order); uids are filled in before the merge
+                key = score_key(f, (int32_t)(c0 + kk * kPostThreads + tid));
             }
             keys[kk] = key;
         }
@@ -1115,6 +1140,11 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         }
+    }
+    // idx -> uid in the wave's list (the same order: uid ascending == idx ascending)
+    if (lane < k && best != ~0ull) {
+        const uint32_t idx = (uint32_t)best ^ 0x80000000u;
+        best = (best & 0xFFFFFFFF00000000ull) | (ps.hdr[2 * (size_t)idx + 1].w ^ 0x80000000u);
     }
     // tail scratch in the (idle) tf-byte array: merge keys, then flag / threshold / block ids
     scan_tail(best, k, tfv, reinterpret_cast<int*>(tfv + kPostWaves * kMaxTopK), sync, parts, out, out_rows);
@@ -1225,7 +1255,8 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 
 // PF_K5_DBG: bit mask that switches K5 phases off (profiling only; results are wrong then):
 // 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions, 32 fixed terms,
-// 64 top-k pushes, 128 header loads
+// 64 top-k pushes, 128 header loads, 256 text scatter LDS writes (entries still loaded),
+// 512 text entry loads (synthetic hits instead), 1024 dense dots and terms, 2048 hit compaction
 static uint32_t post_dbg() {
     static const uint32_t v = [] {
         const char* e = getenv("PF_K5_DBG");
@@ -1236,8 +1267,10 @@ static uint32_t post_dbg() {
     return v;
 }
 
-// K5 dynamic LDS: QConst | fixed per-block arrays | QVal[n_tok] | ranges[n_lists]
-uint32_t post_var_lds(int n_tok, int n_lists) { return (uint32_t)(16 * n_tok + 8 * n_lists + 4 * (n_tok + 1) + 15) & ~15u; }
+// K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | ranges[n_lists] | prefix[n_tok + 1]
+uint32_t post_var_lds(int n_tok, int n_lists) {
+    return (uint32_t)(sizeof(PTok) * n_tok + 8 * n_lists + 4 * (n_tok + 1) + 15) & ~15u;
+}
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,

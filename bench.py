@@ -9,7 +9,9 @@ queries: at N GPUs the batch holds N distinct query users (1 at N=1, i.e. exactl
 config 2), every rank scores its candidate shard (1/N of the corpus, split by stream
 bytes) for the whole batch, the per-shard top-10 keys are exchanged with one RCCL
 all-gather over xGMI and merged on device.  Per-GPU work is fixed (1.6M pairs/step):
-weak scaling.  value = candidates scored / s over the whole job.
+weak scaling.  value = candidates scored / s over the whole job.  With --workload cfg4 a
+step is a fixed batch of 1024 queries (SURVEY D1 cfg 4, seed 3) over the sharded candidates:
+strong scaling.
 
 Also reports the roofline of the dominant kernel (fas_post_kernel, the postings scan, by
 default; fas_scan_kernel, the record-stream scan, with --scan-kernel stream; HIP events
@@ -17,7 +19,8 @@ around every launch) with both the algorithmic rate and the measured DRAM share,
 CPU baseline (oracle/refcpu.cpp, the reference algorithm with its unordered_map data
 structures, single thread, bounded sample of the same corpus).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]        (cfg 2, the headline)
+    python bench.py --workload cfg4 --steps 5 --warmup 1     (cfg 4: 1024 queries per step)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
@@ -35,6 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 N_USERS = 1632803
 TOPK = 10
+CFG4_QUERIES = 1024  # cfg 4 = 1024 query uids (seed 3)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "FAS candidates scored/sec over 1.6M users, top-k=10; 1/2/4/8 GPU + %HBM peak"
 
@@ -89,6 +93,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
+    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default="cfg2",
+                    help="cfg2: N queries per step (1 per GPU, weak scaling; the default); "
+                         "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
                     help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
@@ -124,10 +131,11 @@ def main():
     log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t2 - t1:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
         f"alg {lay.alg_bytes / 1e9:.3f} GB, packed={lay.packed_tokens}")
 
-    Q = world * args.queries_per_gpu
+    cfg4 = args.workload == "cfg4"
+    Q = CFG4_QUERIES if cfg4 else world * args.queries_per_gpu
     k = TOPK
     steps, warm = args.steps, args.warmup
-    rng = np.random.default_rng(2)  # same query stream on every rank
+    rng = np.random.default_rng(3 if cfg4 else 2)  # same query stream on every rank (SURVEY D1 seeds)
     qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
     # a dedicated stream: the engine, the all-gather and the copies are all ordered on it
     stream = torch.cuda.Stream()
@@ -179,7 +187,14 @@ def main():
     shard_frac = 1.0 / world
     alg_bytes = lay.alg_bytes * shard_frac * Q
     achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
-    workload = f"cfg2_all_candidates_top{k}_{args.users}users_q{Q}_shard1of{world}"
+    workload = f"{args.workload}_all_candidates_top{k}_{args.users}users_q{Q}_shard1of{world}"
+    if cfg4:
+        wl_name = (f"cfg4: {Q}-query batch, interest FAS all-candidates top-10 over the full 1.6M-user corpus, "
+                   f"candidates sharded over {world} GPU(s)" + ("" if world == 1 else ", RCCL all-gather of per-shard top-10"))
+    else:
+        wl_name = ("cfg2: full 1.6M-user single-query interest FAS all-candidates top-10"
+                   + ("" if world == 1 else f"; {Q} queries/step, candidates sharded over {world} GPUs, "
+                                            "RCCL all-gather of per-shard top-10"))
     traffic = pmc_traffic(workload, kernel_name)
     rec = {
         "metric": METRIC,
@@ -190,13 +205,11 @@ def main():
         "warmup": warm,
         "ms_per_step": elapsed * 1e3 / steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg4 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
-        "config": {"workload": "cfg2: full 1.6M-user single-query interest FAS all-candidates top-10"
-                               + ("" if world == 1 else f"; {Q} queries/step, candidates sharded over {world} GPUs, "
-                                                        "RCCL all-gather of per-shard top-10"),
+        "config": {"workload": wl_name,
                    "workload_key": workload, "n_users": args.users, "queries_per_step": Q, "topk": k,
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

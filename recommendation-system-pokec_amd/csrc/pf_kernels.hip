@@ -790,18 +790,25 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 //   3. fixed terms (public .. friends) per owned candidate from its 32-B header;
 //   4. text, one active query column at a time in ascending order: the column's token
 //      lists (<= 8 tokens per pass) write each hit's tf byte at [candidate][token] and its
-//      (candidate, column) norm; each wave lists its hit candidates in its own segment
-//      (ballot + popcount, no atomics), and their dot (ascending tid: token order, only the
-//      hit bytes visited) and cosine -> sigmoid term are computed densely, one candidate per
-//      thread, so the FP64 divisions and exp never run on idle lanes; the owners then add
+//      (candidate, column) norm; each wave lists its own hit candidates (ballot + popcount,
+//      no atomics), and their dot (ascending tid: token order, only the hit bytes visited)
+//      and cosine -> sigmoid term are computed densely by the wave, one candidate per lane,
+//      so the FP64 divisions and exp never run on idle lanes; the owners then add
 //      the column's term, or the s = 0 term of a common column without hits, in the
 //      reference's order (recommender_similarity.cpp:38-113).
 // LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
-// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | per-wave hit counts u32[4] |
+// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | misc u32[4] |
 // PTok[n_tok] | ranges uint2[n_lists] | prefix u32[n_tok + 1].  The tail merge reuses the
 // tf-byte array.
 constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16;
-static_assert(kPostWaves == 4, "per-wave hit counts live in the 4 misc words");
+
+// Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
+// this keeps the compiler from moving accesses across the point).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // A query token in LDS: its weight and idf, and the products for tf = 1 and 2 (the common
 // cases), each computed as the reference does, wq * (tf * idf) (recommender.cpp:74-85).
@@ -908,7 +915,7 @@ __device__ __forceinline__ void walk_chunk(const PostStore& ps, const uint2* rng
     }
 }
 
-__global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
+__global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
@@ -1049,28 +1056,23 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                     }
                 });
                 __syncthreads();
-                {  // each wave lists its hit candidates in its own segment: no atomics
-                    uint16_t* wl = list + (tid >> 6) * (kBlockCands / kPostWaves);
-                    uint32_t nw = 0;
+                // each wave lists its own hit candidates (ballot + popcount) and scores them
+                // itself: no atomics, and no barrier between listing and scoring
+                uint16_t* wl = list + (tid >> 6) * (kBlockCands / kPostWaves);
+                uint32_t nw = 0;
 #pragma unroll
-                    for (int kk = 0; kk < kCandsPerThread; ++kk) {
-                        const int p = kk * kPostThreads + tid;
-                        if (tfv[p] != 0ull) colhit |= 1u << kk;
-                        if (dbg & 2048) { tfv[p] = 0ull; continue; }
-                        const bool h = (colhit >> kk) & 1u;
-                        const uint64_t m = __ballot(h);
-                        if (h) wl[nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-                        nw += (uint32_t)__popcll(m);
-                    }
-                    if (lane == 0) nlist[tid >> 6] = nw;
+                for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                    const int p = kk * kPostThreads + tid;
+                    if (tfv[p] != 0ull) colhit |= 1u << kk;
+                    if (dbg & 2048) { tfv[p] = 0ull; continue; }
+                    const bool h = (colhit >> kk) & 1u;
+                    const uint64_t m = __ballot(h);
+                    if (h) wl[nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
+                    nw += (uint32_t)__popcll(m);
                 }
-                __syncthreads();
-                const uint32_t n0 = nlist[0], n1 = nlist[1], n2 = nlist[2];
-                const uint32_t n = n0 + n1 + n2 + nlist[3];
-                for (uint32_t i = tid; i < n; i += kPostThreads) {
-                    uint32_t r = i, w = 0;  // item i -> (wave segment w, position r)
-                    if (r >= n0) { r -= n0; ++w; if (r >= n1) { r -= n1; ++w; if (r >= n2) { r -= n2; ++w; } } }
-                    const int p = list[w * (kBlockCands / kPostWaves) + r];
+                wave_sync();
+                for (uint32_t i = lane; i < nw; i += 64) {
+                    const int p = wl[i];
                     uint64_t v = tfv[p];
                     tfv[p] = 0ull;
                     if (dbg & 1024) { term[p] = (double)v; continue; }
@@ -1087,6 +1089,7 @@ __global__ __launch_bounds__(kPostThreads) void fas_post_kernel(PostStore ps, co
                     }
                     term[p] = (!last || (dbg & 2)) ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
+                wave_sync();
                 __syncthreads();
             }
 #pragma unroll

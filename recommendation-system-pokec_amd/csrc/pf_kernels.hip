@@ -797,10 +797,10 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 //      the column's term, or the s = 0 term of a common column without hits, in the
 //      reference's order (recommender_similarity.cpp:38-113).
 // LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
-// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | misc u32[4] |
+// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | misc u32[4] | QCol[48] |
 // PTok[n_tok] | ranges uint2[n_lists] | prefix u32[n_tok + 1].  The tail merge reuses the
 // tf-byte array.
-constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16;
+constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16 + 16 * kPostMaxCols;
 
 // Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
 // this keeps the compiler from moving accesses across the point).
@@ -878,40 +878,51 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
 
 // The entries of token lists js .. js + nj - 1 (nj <= 8) flattened over the workgroup, with
 // the block's token prefix gpre: a thread finds the list of a flat entry in 3 bisection
-// steps.  Two entries per thread and group of 512, loaded together, then f(list - js, entry, norm).
-template <class F>
-__device__ __forceinline__ void walk_chunk(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
-                                           uint32_t dbg, uint32_t c0, F f) {
+// steps.  One group of 512 flat entries: a thread's two (list - js or -1, entry, norm),
+// loaded together.
+struct Group {
+    int jj[2];
+    uint32_t ent[2];
+    double nv[2];
+};
+
+__device__ __forceinline__ void load_group(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
+                                           uint32_t f0, Group& g) {
     static_assert(kChunkToks <= 8, "3 bisection steps cover 8 lists");
     const uint32_t base = gpre[js], total = gpre[js + nj] - base;
-    for (uint32_t f0 = 0; f0 < total; f0 += 2 * kPostThreads) {
-        int jj[2];
-        uint32_t xs[2];
+    uint32_t xs[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
-            int j = js;  // last list starting at or before fl
-            if (j + 4 < js + nj && gpre[j + 4] - base <= fl) j += 4;
-            if (j + 2 < js + nj && gpre[j + 2] - base <= fl) j += 2;
-            if (j + 1 < js + nj && gpre[j + 1] - base <= fl) j += 1;
-            jj[u] = fl < total ? j : -1;
-            xs[u] = fl < total ? rng[j].x + (fl - (gpre[j] - base)) : 0u;
-        }
-        uint32_t ent[2];
-        double nv[2];
+    for (int u = 0; u < 2; ++u) {
+        const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
+        int j = js;  // last list starting at or before fl
+        if (j + 4 < js + nj && gpre[j + 4] - base <= fl) j += 4;
+        if (j + 2 < js + nj && gpre[j + 2] - base <= fl) j += 2;
+        if (j + 1 < js + nj && gpre[j + 1] - base <= fl) j += 1;
+        g.jj[u] = fl < total ? j - js : -1;
+        xs[u] = fl < total ? rng[j].x + (fl - (gpre[j] - base)) : 0u;
+    }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (dbg & 512) {  // no loads: a synthetic hit per flat entry
-                ent[u] = jj[u] >= 0 ? ((c0 + xs[u] % 1024u) << 8 | 1u) : 0u;
-                nv[u] = 1.0;
-            } else {
-                ent[u] = jj[u] >= 0 ? ps.post[xs[u]] : 0u;
-                nv[u] = jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
-            }
-        }
+    for (int u = 0; u < 2; ++u) {
+        g.ent[u] = g.jj[u] >= 0 ? ps.post[xs[u]] : 0u;
+        g.nv[u] = g.jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
+    }
+}
+
+// f(list - js, entry, norm) for every entry of group g, then for the groups of the pass
+// after the first (long lists only), loaded here
+template <class F>
+__device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
+                                          const Group& g, F f) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+        if (g.jj[u] >= 0) f(g.jj[u], g.ent[u], g.nv[u]);
+    const uint32_t total = gpre[js + nj] - gpre[js];
+    for (uint32_t f0 = 2 * kPostThreads; f0 < total; f0 += 2 * kPostThreads) {
+        Group r;
+        load_group(ps, rng, gpre, js, nj, f0, r);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-            if (jj[u] >= 0 && (!(dbg & 256) || (ent[u] == 0xFFFFFFFFu && nv[u] == -1.0))) f(jj[u] - js, ent[u], nv[u]);
+            if (r.jj[u] >= 0) f(r.jj[u], r.ent[u], r.nv[u]);
     }
 }
 
@@ -937,12 +948,14 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
     uint32_t* nlist = exb + kBlockCands / 32;
+    QCol* scol = reinterpret_cast<QCol*>(nlist + 4);  // the active columns (read at every pass)
     PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
     uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + sizeof(PTok) * H.n_tok);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
     const int nsets = H.n_club + H.n_friend;
     const int nl = H.n_tok + nsets;
     stage(smem, img, sizeof(QConst));
+    for (int j = tid; j < H.n_act; j += kPostThreads) scol[j] = cols[j];
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
         PTok v;
         v.wq = toks[j].wq;
@@ -1034,9 +1047,19 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
         }
         __syncthreads();  // the counters' LDS now holds the compacted lists
-        // 4. text columns, ascending
-        for (int ci = 0; ci < ((dbg & 8) ? 0 : H.n_act); ++ci) {
-            const QCol col = cols[ci];
+        // 4. text columns, ascending.  A pass is one column's tokens js .. js + nj - 1
+        // (nj <= kChunkToks); the first group of the next pass's entries is loaded while
+        // this pass is scored (software pipeline: the loads are the walk's latency).
+        const int n_act = (dbg & 8) ? 0 : H.n_act;
+        Group ahead;
+        {
+            int c = 0;  // the first column with tokens (columns without any have no passes)
+            while (c < n_act && scol[c].j1 == scol[c].j0) ++c;
+            load_group(ps, rng, gpre, c < n_act ? scol[c].j0 : 0, c < n_act ? min(kChunkToks, scol[c].j1 - scol[c].j0) : 0,
+                       0, ahead);
+        }
+        for (int ci = 0; ci < n_act; ++ci) {
+            const QCol col = scol[ci];
             const int t = col.t;
             uint32_t colhit = 0;  // bit kk: owned candidate kk has a hit in column t
             // a column of more than kChunkToks tokens carries its dot in term[] across passes
@@ -1048,13 +1071,28 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             for (int js = col.j0; js < col.j1; js += kChunkToks) {
                 const int nj = min(kChunkToks, col.j1 - js);
                 const bool last = js + kChunkToks >= col.j1;
-                if (!(dbg & 1)) walk_chunk(ps, rng, gpre, js, nj, dbg, c0, [&](int j, uint32_t e, double nv) {
+                if (!(dbg & 1)) walk_pass(ps, rng, gpre, js, nj, ahead, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
                     if (p < B) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
                         nrm[p] = nv;
                     }
                 });
+                {  // one load site (copies of in-flight registers at a join would wait for them)
+                    int njs = 0, nnj = 0;  // the next pass (none: 0 tokens)
+                    if (!last) {
+                        njs = js + kChunkToks;
+                        nnj = min(kChunkToks, col.j1 - njs);
+                    } else {
+                        int c = ci + 1;
+                        while (c < n_act && scol[c].j1 == scol[c].j0) ++c;
+                        if (c < n_act) {
+                            njs = scol[c].j0;
+                            nnj = min(kChunkToks, scol[c].j1 - njs);
+                        }
+                    }
+                    load_group(ps, rng, gpre, njs, nnj, 0, ahead);
+                }
                 __syncthreads();
                 // each wave lists its own hit candidates (ballot + popcount) and scores them
                 // itself: no atomics, and no barrier between listing and scoring
@@ -1092,30 +1130,16 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 wave_sync();
                 __syncthreads();
             }
+            // the image lists every non-empty query column, so the common columns are met
+            // here in ascending order (recommender_similarity.cpp:93-113)
 #pragma unroll
-            for (int kk = 0; kk < kCandsPerThread; ++kk) {
-                uint64_t below = pend[kk] & ((1ull << t) - 1ull);
-                pend[kk] &= ~below;
-                while (below) {
-                    const int c = __ffsll((unsigned long long)below) - 1;
-                    below &= below - 1;
-                    sum[kk] += q.sig0_col[c];
-                }
-                if ((pend[kk] >> t) & 1ull) {
-                    sum[kk] += ((colhit >> kk) & 1u) ? term[kk * kPostThreads + tid] : q.sig0_col[t];
-                    pend[kk] &= ~(1ull << t);
-                }
-            }
+            for (int kk = 0; kk < kCandsPerThread; ++kk)
+                if ((pend[kk] >> t) & 1ull) sum[kk] += ((colhit >> kk) & 1u) ? term[kk * kPostThreads + tid] : q.sig0_col[t];
         }
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
         uint64_t keys[kCandsPerThread];
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
-            while (pend[kk]) {
-                const int c = __ffsll((unsigned long long)pend[kk]) - 1;
-                pend[kk] &= pend[kk] - 1;
-                sum[kk] += q.sig0_col[c];
-            }
             uint64_t key = ~0ull;
             if (!((skip >> kk) & 1u)) {
                 float f = 0.0f;
@@ -1258,8 +1282,7 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 
 // PF_K5_DBG: bit mask that switches K5 phases off (profiling only; results are wrong then):
 // 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions, 32 fixed terms,
-// 64 top-k pushes, 128 header loads, 256 text scatter LDS writes (entries still loaded),
-// 512 text entry loads (synthetic hits instead), 1024 dense dots and terms, 2048 hit compaction
+// 64 top-k pushes, 128 header loads, 1024 dense dots and terms, 2048 hit compaction
 static uint32_t post_dbg() {
     static const uint32_t v = [] {
         const char* e = getenv("PF_K5_DBG");

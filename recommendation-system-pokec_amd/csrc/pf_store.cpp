@@ -705,7 +705,9 @@ void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const
             q.idf = idf;
             toks.push_back(q);
         }
-        if ((int32_t)toks.size() > j0) cols.push_back(QCol{t, j0, (int32_t)toks.size(), 0});
+        // every non-empty query column is listed (none of its tokens may carry weight: then
+        // it has no passes), so the kernel adds every common column's term at its column
+        if (hc.tok_off[r + 1] != hc.tok_off[r]) cols.push_back(QCol{t, j0, (int32_t)toks.size(), 0});
     }
     std::vector<PList> sets;
     auto add_sets = [&](const std::vector<int64_t>& o, const std::vector<uint32_t>& ids,

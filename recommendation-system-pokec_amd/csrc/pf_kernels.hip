@@ -926,6 +926,15 @@ __device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng,
     }
 }
 
+#ifdef PF_K5_TIMERS
+// profiling build only (make K5T=1): per-phase clock64() sums over every wave, printed by
+// launch_post every 10th launch
+__device__ unsigned long long g_k5t[16];
+#define K5T(slot) do { const uint64_t t_ = clock64(); tacc[slot] += t_ - tprev; tprev = t_; } while (0)
+#else
+#define K5T(slot) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
@@ -968,6 +977,11 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     for (int kk = 0; kk < kCandsPerThread; ++kk) tfv[kk * kPostThreads + tid] = 0ull;
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
+#ifdef PF_K5_TIMERS
+    uint64_t tacc[12] = {0};
+    uint64_t tprev = clock64();
+    const uint64_t tstart = tprev;
+#endif
     for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end; blk += (int)gridDim.x) {
         const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
@@ -985,7 +999,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             cnt[kk * kPostThreads + tid] = 0u;
         }
         if (tid < kBlockCands / 32) exb[tid] = 0u;
+        K5T(0);
         __syncthreads();
+        K5T(1);
         if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
         {
@@ -1010,7 +1026,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             const uint32_t p = (e >> 8) - c0;
             if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
+        K5T(2);
         __syncthreads();
+        K5T(1);
         // 3. fixed terms, recommender_similarity.cpp:38-91
         double sum[kCandsPerThread];
         uint32_t used = 0;  // byte kk: terms used by candidate kk (<= 7 + 48)
@@ -1046,7 +1064,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             sum[kk] = s;
             used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
         }
+        K5T(3);
         __syncthreads();  // the counters' LDS now holds the compacted lists
+        K5T(1);
         // 4. text columns, ascending.  A pass is one column's tokens js .. js + nj - 1
         // (nj <= kChunkToks); the first group of the next pass's entries is loaded while
         // this pass is scored (software pipeline: the loads are the walk's latency).
@@ -1093,7 +1113,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     }
                     load_group(ps, rng, gpre, njs, nnj, 0, ahead);
                 }
+                K5T(4);
                 __syncthreads();
+                K5T(5);
                 // each wave lists its own hit candidates (ballot + popcount) and scores them
                 // itself: no atomics, and no barrier between listing and scoring
                 uint16_t* wl = list + (tid >> 6) * (kBlockCands / kPostWaves);
@@ -1109,6 +1131,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     nw += (uint32_t)__popcll(m);
                 }
                 wave_sync();
+                K5T(6);
                 for (uint32_t i = lane; i < nw; i += 64) {
                     const int p = wl[i];
                     uint64_t v = tfv[p];
@@ -1128,7 +1151,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     term[p] = (!last || (dbg & 2)) ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
                 wave_sync();
+                K5T(7);
                 __syncthreads();
+                K5T(8);
             }
             // the image lists every non-empty query column, so the common columns are met
             // here in ascending order (recommender_similarity.cpp:93-113)
@@ -1136,6 +1161,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             for (int kk = 0; kk < kCandsPerThread; ++kk)
                 if ((pend[kk] >> t) & 1ull) sum[kk] += ((colhit >> kk) & 1u) ? term[kk * kPostThreads + tid] : q.sig0_col[t];
         }
+        K5T(9);
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
         uint64_t keys[kCandsPerThread];
 #pragma unroll
@@ -1167,7 +1193,15 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         }
+        K5T(10);
     }
+#ifdef PF_K5_TIMERS
+    tacc[11] = clock64() - tstart;
+    if (lane == 0) {
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_k5t[i], (unsigned long long)tacc[i]);
+        atomicAdd(&g_k5t[12], 1ull);
+    }
+#endif
     // idx -> uid in the wave's list (the same order: uid ascending == idx ascending)
     if (lane < k && best != ~0ull) {
         const uint32_t idx = (uint32_t)best ^ 0x80000000u;
@@ -1305,6 +1339,23 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
     if (nq <= 0) return hipSuccess;
     hipLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool, img_off,
                        blk_begin, blk_end, k, parts, sync, out, out_rows, post_dbg());
+#ifdef PF_K5_TIMERS
+    {
+        static int calls = 0;
+        unsigned long long t[16];
+        hipStreamSynchronize(s);
+        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k5t), sizeof(t));
+        static const char* nm[12] = {"ranges+hdr", "barriers", "excl+sets", "fixed", "walk", "walk-bar",
+                                     "compact", "dense", "pass-bar", "owner-add", "fas+topk", "total"};
+        if (++calls % 10 == 0) {
+            fprintf(stderr, "k5t per wave (clock64):");
+            for (int i = 0; i < 12; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[12]);
+            fprintf(stderr, "\n");
+        }
+        const unsigned long long z[16] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_k5t), z, sizeof(z));
+    }
+#endif
     return hipGetLastError();
 }
 

@@ -47,6 +47,27 @@ struct DBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Pinned host buffer that only grows (contents are not initialised)
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 using Ranked = std::vector<std::pair<int32_t, float>>;
 
 void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
@@ -76,6 +97,7 @@ struct pf_ctx {
     pf::DevStore ds{};
     // workspaces
     DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
+    PinBuf h_pool, h_slots, h_scores;  // pair batches: images, candidate slots, scores
     int32_t tile_begin = 0, tile_end = 0;
     // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
     pf::HostPost hp;
@@ -209,6 +231,42 @@ void add_image(Images& im, const pf::QImageHost& q) {
     im.refs.push_back(r);
 }
 
+// Many images at once: refs and offsets first (returns the pool bytes), then fill_images
+// copies them on threads into `dst` (pinned; a few thousand images per chunk).
+size_t plan_images(Images& im, const std::vector<pf::QImageHost>& qs) {
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    size_t o = 0;
+    for (const auto& q : qs) {
+        pf::QImageRef r{};
+        r.const_off = (uint32_t)o;
+        r.keys_off = (uint32_t)(o + sizeof(pf::QConst));
+        r.vals_off = (uint32_t)a16(r.keys_off + q.keys.size() * 8);
+        o = a16(r.vals_off + q.vals.size() * sizeof(pf::QVal));
+        const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
+        r.lds_bytes = kv <= stage_limit() ? (uint32_t)kv : 0u;
+        im.gtab = im.gtab || r.lds_bytes == 0;
+        const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads +
+                              4u * kBlockThreads + 2048u;
+        im.max_lds = std::max(im.max_lds, need);
+        im.refs.push_back(r);
+    }
+    return o;
+}
+
+void fill_images(const Images& im, const std::vector<pf::QImageHost>& qs, uint8_t* dst, size_t total) {
+    par_jobs(qs.size(), [&](size_t i) {
+        const pf::QImageHost& q = qs[i];
+        const pf::QImageRef& r = im.refs[i];
+        const size_t kend = r.keys_off + q.keys.size() * 8, vend = r.vals_off + q.vals.size() * sizeof(pf::QVal);
+        const size_t next = i + 1 < qs.size() ? im.refs[i + 1].const_off : total;
+        std::memcpy(dst + r.const_off, &q.c, sizeof(pf::QConst));
+        if (!q.keys.empty()) std::memcpy(dst + r.keys_off, q.keys.data(), q.keys.size() * 8);
+        std::memset(dst + kend, 0, r.vals_off - kend);
+        if (!q.vals.empty()) std::memcpy(dst + r.vals_off, q.vals.data(), q.vals.size() * sizeof(pf::QVal));
+        std::memset(dst + vend, 0, next - vend);
+    });
+}
+
 // recommender_graph.cpp:10-31 (friends + FoFs, first-seen order, limit after every push)
 std::vector<int32_t> gather_graph(const pf::AdjView& V, int32_t u, int32_t limit) {
     std::vector<int32_t> out;
@@ -281,6 +339,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
         if (pairs == 0) { g0 = g1; continue; }
         std::vector<pf::QImageHost> qi(uq.size());
         std::vector<uint8_t> ok(uq.size(), 1);
+        pf::HpLap hl;
         {
             const int th = (int)std::min<size_t>(16, std::max<size_t>(1, uq.size() / 16));
             std::vector<std::thread> ts;
@@ -293,34 +352,52 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
         }
         for (uint8_t x : ok)
             if (!x) return c->fail(PF_EUNSUPP, "query hash table too large");
+        hl.lap(pf::kHpImages);
         Images im;
-        for (auto& x : qi) add_image(im, x);
         std::vector<pf::PairBlock> blocks;
-        std::vector<int32_t> flat;
-        flat.reserve(pairs);
+        const size_t pool_bytes = plan_images(im, qi);
+        // per group: first block and first pair (serial, O(groups)); then the copies on threads
+        std::vector<size_t> gb(g1 - g0 + 1), gf(g1 - g0 + 1);
         for (size_t g = g0; g < g1; ++g) {
-            if (slots[g].empty()) continue;
-            const int32_t img = img_of.at(qidx[g]);
-            for (size_t b = 0; b < slots[g].size(); b += 256) {
-                pf::PairBlock pb{img, (int32_t)flat.size(), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
-                blocks.push_back(pb);
-                for (size_t j = b; j < b + (size_t)pb.count; ++j) flat.push_back(slots[g][j]);
-            }
+            gb[g - g0 + 1] = gb[g - g0] + (slots[g].size() + 255) / 256;
+            gf[g - g0 + 1] = gf[g - g0] + slots[g].size();
         }
-        HIPCHK(c, upload(c, c->d_pool, im.pool));
+        const size_t npairs = gf.back();
+        HIPCHK(c, c->h_pool.ensure(pool_bytes));
+        HIPCHK(c, c->h_slots.ensure(npairs * sizeof(int32_t)));
+        HIPCHK(c, c->h_scores.ensure(npairs * sizeof(float)));
+        fill_images(im, qi, c->h_pool.as<uint8_t>(), pool_bytes);
+        blocks.resize(gb.back());
+        int32_t* flat = c->h_slots.as<int32_t>();
+        par_jobs(g1 - g0, [&](size_t i) {
+            const size_t g = g0 + i;
+            if (slots[g].empty()) return;
+            const int32_t img = img_of.at(qidx[g]);
+            std::memcpy(flat + gf[i], slots[g].data(), slots[g].size() * sizeof(int32_t));
+            for (size_t b = 0, x = gb[i]; b < slots[g].size(); b += 256, ++x)
+                blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
+        });
+        hl.lap(pf::kHpPack);
+        // pinned buffers: async copies; they are reused only after this chunk's synchronize
+        HIPCHK(c, c->d_pool.ensure(std::max<size_t>(pool_bytes, 16)));
+        HIPCHK(c, hipMemcpyAsync(c->d_pool.p, c->h_pool.p, pool_bytes, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, upload(c, c->d_refs, im.refs));
         HIPCHK(c, upload(c, c->d_blocks, blocks));
-        HIPCHK(c, upload(c, c->d_slots, flat));
-        HIPCHK(c, c->d_scores.ensure(flat.size() * sizeof(float)));
+        HIPCHK(c, c->d_slots.ensure(npairs * sizeof(int32_t)));
+        HIPCHK(c, hipMemcpyAsync(c->d_slots.p, flat, npairs * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, c->d_scores.ensure(npairs * sizeof(float)));
         HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
                                    c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
                                    c->d_scores.as<float>(), c->stream));
-        std::vector<float> res(flat.size());
-        HIPCHK(c, hipMemcpyAsync(res.data(), c->d_scores.p, res.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        const float* res = c->h_scores.as<float>();
+        HIPCHK(c, hipMemcpyAsync(c->h_scores.p, c->d_scores.p, npairs * sizeof(float), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        size_t o = 0;
-        for (size_t g = g0; g < g1; ++g)
-            for (size_t j = 0; j < slots[g].size(); ++j) out[g][j] = res[o++];
+        hl.lap(pf::kHpGpu);
+        par_jobs(g1 - g0, [&](size_t i) {
+            const size_t g = g0 + i;
+            if (!slots[g].empty()) std::memcpy(out[g].data(), res + gf[i], slots[g].size() * sizeof(float));
+        });
+        hl.lap(pf::kHpUnpack);
         g0 = g1;
     }
     return PF_OK;
@@ -491,6 +568,23 @@ namespace pf {
 
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c) { return c->hc.adj; }
 
+HostProf::HostProf() {
+    const char* e = getenv("PF_HOST_PROF");
+    on = e && *e && *e != '0';
+    for (auto& x : ns) x = 0;
+}
+HostProf::~HostProf() {
+    if (!on) return;
+    static const char* nm[kHpStages] = {"plan", "prep", "images", "pack", "gpu", "unpack", "stage2", "collab", "finish"};
+    fprintf(stderr, "pokec_fas host stages (s):");
+    for (int i = 0; i < kHpStages; ++i) fprintf(stderr, " %s=%.3f", nm[i], (double)ns[i].load() * 1e-9);
+    fprintf(stderr, "\n");
+}
+HostProf& host_prof() {
+    static HostProf h;
+    return h;
+}
+
 // Every job's FAS pairs in two GPU stages (stage 2: the clubs recommender's friend-of-friend
 // pairs, which depend on stage 1's friend weights), the collaborative sums in one K4 launch,
 // then the reference's host arithmetic.  The per-job host work runs on threads.
@@ -509,6 +603,7 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
         int64_t coff = -1;                // collab: offset of its sums
     };
     std::vector<St> st(jobs.size());
+    HpLap hl;
     par_jobs(jobs.size(), [&](size_t i) {
         Job& J = jobs[i];
         St& S = st[i];
@@ -588,8 +683,10 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
         S.groups.clear();
     }
     std::vector<std::vector<float>> res;
+    hl.lap(kHpPrep);
     int rc = run_pairs(c, qidx, slots, res);
     if (rc != PF_OK) return rc;
+    hl.skip();
     // stage 2: FAS(f, fof) for every fof of every positive-weight friend (clubs)
     par_jobs(jobs.size(), [&](size_t i) {
         Job& J = jobs[i];
@@ -624,8 +721,10 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
         st[i].groups.clear();
     }
     std::vector<std::vector<float>> res2;
+    hl.lap(kHpStage2);
     rc = run_pairs(c, qidx2, slots2, res2);
     if (rc != PF_OK) return rc;
+    hl.skip();
     // collaborative sums (K4): every collab job of the batch in one launch
     {
         std::vector<CollabSum> cj;
@@ -664,6 +763,7 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
                                      c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
         }
+        hl.lap(kHpCollab);
         par_jobs(jobs.size(), [&](size_t i) {
             Job& J = jobs[i];
             St& S = st[i];
@@ -716,6 +816,7 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
             rank(r, J.topk);
             J.out = std::move(r);
         });
+        hl.lap(kHpFinish);
     }
     return PF_OK;
 }

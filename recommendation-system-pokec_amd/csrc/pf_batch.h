@@ -1,6 +1,8 @@
 // pf_batch.h — engine-internal batched recommenders (pf_api.cpp) for the C ABI entry points
 // and the batched hold-out drivers (pf_dataset.cpp).  Not part of the public ABI.
 #pragma once
+#include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstdint>
 #include <unordered_map>
@@ -43,6 +45,30 @@ struct Job {
     bool all_candidates = false;
     AdjView view;
     std::vector<std::pair<int32_t, float>> out;  // ranked (id, score), <= topk
+};
+
+// Host-side stage clocks of the batched drivers (PF_HOST_PROF=1: summed over the process and
+// printed to stderr at exit; profiling only).
+enum HostStage {
+    kHpPlan = 0, kHpPrep, kHpImages, kHpPack, kHpGpu, kHpUnpack, kHpStage2, kHpCollab, kHpFinish, kHpStages
+};
+struct HostProf {
+    bool on = false;
+    std::atomic<long long> ns[kHpStages];
+    HostProf();
+    ~HostProf();
+};
+HostProf& host_prof();
+// lap(st): the time since the last lap (or construction) goes to stage st; skip(): dropped
+struct HpLap {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int st) {
+        const auto n = std::chrono::steady_clock::now();
+        HostProf& h = host_prof();
+        if (h.on) h.ns[st] += std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count();
+        t = n;
+    }
+    void skip() { t = std::chrono::steady_clock::now(); }
 };
 
 // Runs every job; their FAS pairs go to the GPU together (one pair-kernel launch per stage

@@ -837,7 +837,9 @@ extern "C" {
 int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard, int32_t nshards,
                             int32_t batch, double* out_ratio, int32_t cap, int32_t* n_plan) {
     if (!ctx || !ds || !n_plan || (cap > 0 && !out_ratio) || bad_shard(shard, nshards, batch)) return PF_EINVAL;
+    pf::HpLap hl;
     const std::vector<PlanEntry> plan = plan_friends(ds, sample_size);
+    hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
     // one adj_mod for the whole run (test.cpp:35,73): user i sees the rows of users 0..i edited
     std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>> over;
@@ -878,7 +880,9 @@ int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t samp
                                  int32_t* n_plan) {
     if (!ctx || !ds || !n_plan || (cap > 0 && (!out_hits || !out_club)) || bad_shard(shard, nshards, batch))
         return PF_EINVAL;
+    pf::HpLap hl;
     const std::vector<PlanEntry> plan = plan_rec(ds, sample_size);
+    hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
     const auto& base = pf::base_adj(ctx);
     std::vector<int32_t> mine;

@@ -98,6 +98,7 @@ struct pf_ctx {
     // workspaces
     DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
     PinBuf h_pool, h_slots, h_scores;  // pair batches: images, candidate slots, scores
+    DBuf d_pairs1;                     // run_jobs stage-1 scores (the collaborative matrices)
     int32_t tile_begin = 0, tile_end = 0;
     // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
     pf::HostPost hp;
@@ -155,10 +156,11 @@ struct pf_ctx {
 
 namespace {
 
-// f(0 .. n-1) on up to 16 threads (4 items per thread at least)
+// f(0 .. n-1) on up to 16 threads, `grain` items per thread at least (a thread costs tens of
+// microseconds: the single-user calls of the sequential drivers stay on the caller's thread)
 template <class F>
-void par_jobs(size_t n, F f) {
-    const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / 4, std::thread::hardware_concurrency())));
+void par_jobs(size_t n, F f, size_t grain = 4) {
+    const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / grain, std::thread::hardware_concurrency())));
     if (th <= 1) {
         for (size_t i = 0; i < n; ++i) f(i);
         return;
@@ -264,7 +266,7 @@ void fill_images(const Images& im, const std::vector<pf::QImageHost>& qs, uint8_
         std::memset(dst + kend, 0, r.vals_off - kend);
         if (!q.vals.empty()) std::memcpy(dst + r.vals_off, q.vals.data(), q.vals.size() * sizeof(pf::QVal));
         std::memset(dst + vend, 0, next - vend);
-    });
+    }, 64);
 }
 
 // recommender_graph.cpp:10-31 (friends + FoFs, first-seen order, limit after every push)
@@ -316,9 +318,20 @@ pf::AdjView plain_view(const pf_ctx* c) {
 // FAS(A = qidx[g], B = slots[g][j]) for every group g, on the GPU.
 // Groups go to the GPU in chunks (<= 4096 distinct queries, <= 8M pairs per launch); each
 // distinct query's image is built once per chunk, on host threads.
+// keep (optional): every chunk's scores stay on the device in one buffer, group g at
+// (*goff)[g] (the collaborative sums read their matrix rows there)
 int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std::vector<int32_t>>& slots,
-              std::vector<std::vector<float>>& out) {
+              std::vector<std::vector<float>>& out, DBuf* keep = nullptr, std::vector<int64_t>* goff = nullptr) {
     out.assign(qidx.size(), {});
+    if (keep) {
+        size_t tot = 0;
+        goff->assign(qidx.size(), 0);
+        for (size_t g = 0; g < qidx.size(); ++g) {
+            (*goff)[g] = (int64_t)tot;
+            tot += slots[g].size();
+        }
+        HIPCHK(c, keep->ensure(std::max<size_t>(tot, 1) * sizeof(float)));
+    }
     for (size_t g = 0; g < qidx.size(); ++g) out[g].assign(slots[g].size(), 0.f);
     size_t g0 = 0;
     while (g0 < qidx.size()) {
@@ -376,7 +389,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
             std::memcpy(flat + gf[i], slots[g].data(), slots[g].size() * sizeof(int32_t));
             for (size_t b = 0, x = gb[i]; b < slots[g].size(); b += 256, ++x)
                 blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
-        });
+        }, 256);
         hl.lap(pf::kHpPack);
         // pinned buffers: async copies; they are reused only after this chunk's synchronize
         HIPCHK(c, c->d_pool.ensure(std::max<size_t>(pool_bytes, 16)));
@@ -385,18 +398,24 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
         HIPCHK(c, upload(c, c->d_blocks, blocks));
         HIPCHK(c, c->d_slots.ensure(npairs * sizeof(int32_t)));
         HIPCHK(c, hipMemcpyAsync(c->d_slots.p, flat, npairs * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, c->d_scores.ensure(npairs * sizeof(float)));
+        float* dsc = nullptr;
+        if (keep) {
+            dsc = keep->as<float>() + (*goff)[g0];  // groups are laid out in order, chunk after chunk
+        } else {
+            HIPCHK(c, c->d_scores.ensure(npairs * sizeof(float)));
+            dsc = c->d_scores.as<float>();
+        }
         HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
-                                   c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(),
-                                   c->d_scores.as<float>(), c->stream));
+                                   c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(), dsc,
+                                   c->stream));
         const float* res = c->h_scores.as<float>();
-        HIPCHK(c, hipMemcpyAsync(c->h_scores.p, c->d_scores.p, npairs * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_scores.p, dsc, npairs * sizeof(float), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         hl.lap(pf::kHpGpu);
         par_jobs(g1 - g0, [&](size_t i) {
             const size_t g = g0 + i;
             if (!slots[g].empty()) std::memcpy(out[g].data(), res + gf[i], slots[g].size() * sizeof(float));
-        });
+        }, 256);
         hl.lap(pf::kHpUnpack);
         g0 = g1;
     }
@@ -684,7 +703,8 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
     }
     std::vector<std::vector<float>> res;
     hl.lap(kHpPrep);
-    int rc = run_pairs(c, qidx, slots, res);
+    std::vector<int64_t> goff;  // stage-1 scores stay on the device for K4
+    int rc = run_pairs(c, qidx, slots, res, &c->d_pairs1, &goff);
     if (rc != PF_OK) return rc;
     hl.skip();
     // stage 2: FAS(f, fof) for every fof of every positive-weight friend (clubs)
@@ -728,7 +748,7 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
     // collaborative sums (K4): every collab job of the batch in one launch
     {
         std::vector<CollabSum> cj;
-        std::vector<float> M, w;
+        std::vector<float> w;
         std::vector<int32_t> wrow;
         int64_t ctot = 0;
         int max_nc = 0;
@@ -736,13 +756,13 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
             St& S = st[i];
             if (jobs[i].kind != kJobCollab || S.iq < 0 || jobs[i].topk <= 0 || S.cuid.empty()) continue;
             const int F = (int)S.friends.size(), nc = (int)S.cuid.size();
-            CollabSum js{(int64_t)M.size(), ctot, (int32_t)w.size(), F, nc, 0};
+            // the matrix rows M[f][c] are stage-1 groups g1 .. g1 + |fidx| - 1, consecutive on the device
+            CollabSum js{S.fidx.empty() ? 0 : goff[S.g1], ctot, (int32_t)w.size(), F, nc, 0};
             for (int j = 0; j < F; ++j) {
                 auto rt = S.fpos.find(S.friends[j]);
                 wrow.push_back(rt == S.fpos.end() ? -1 : rt->second);
                 w.push_back(rt == S.fpos.end() ? 0.f : res[S.g0][rt->second]);
             }
-            for (size_t rr = 0; rr < S.fidx.size(); ++rr) M.insert(M.end(), res[S.g1 + rr].begin(), res[S.g1 + rr].end());
             S.coff = ctot;
             ctot += nc;
             max_nc = std::max(max_nc, nc);
@@ -750,13 +770,12 @@ int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
         }
         std::vector<float> sums((size_t)ctot);
         if (!cj.empty()) {
-            HIPCHK(c, upload(c, c->d_scores, M));
             HIPCHK(c, upload(c, c->d_w, w));
             HIPCHK(c, upload(c, c->d_wrow, wrow));
             HIPCHK(c, upload(c, c->d_cjobs, cj));
             HIPCHK(c, c->d_csum.ensure((size_t)ctot * sizeof(float)));
             for (size_t b = 0; b < cj.size(); b += 65535)
-                HIPCHK(c, launch_collab_sum(c->d_scores.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(),
+                HIPCHK(c, launch_collab_sum(c->d_pairs1.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(),
                                             c->d_cjobs.as<CollabSum>() + b, (int)std::min<size_t>(65535, cj.size() - b),
                                             max_nc, c->d_csum.as<float>(), c->stream));
             HIPCHK(c, hipMemcpyAsync(sums.data(), c->d_csum.p, sums.size() * sizeof(float), hipMemcpyDeviceToHost,

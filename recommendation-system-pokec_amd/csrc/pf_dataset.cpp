@@ -6,12 +6,15 @@
 // reference exposes: the profiles map (hold-out drivers), adj_list, and each
 // token_cols map (profile JSON).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -129,98 +132,205 @@ bool load_columns(const std::string& path, std::vector<std::string>& out) {
     return true;
 }
 
+// ---------------------------------------------------------------- parallel text ingest (F2)
+// The reference reads both CSVs line by line with std::getline (graph_builder.cpp:44,
+// user_loader.cpp:38).  Here the file is read whole, cut into the same lines ('\n' only; a
+// '\r' stays in the line, a last line without '\n' still counts), the lines are parsed on
+// threads, and the parsed records are inserted into the hash containers on one thread in
+// file order, so every container sees the reference's insertion sequence.
+
+bool read_file(const std::string& path, std::string& buf) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    buf.clear();
+    char tmp[1 << 16];
+    if (fseek(f, 0, SEEK_END) == 0) {
+        const long sz = ftell(f);
+        if (sz > 0) buf.reserve((size_t)sz);
+        fseek(f, 0, SEEK_SET);
+    }
+    size_t got;
+    while ((got = fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, got);
+    const bool ok = !ferror(f);
+    fclose(f);
+    return ok;
+}
+
+// [begin, end) of each std::getline line of buf from offset `from`, at most max_lines (<= 0: all)
+void split_lines(const std::string& buf, size_t from, int64_t max_lines, std::vector<std::pair<size_t, size_t>>& out) {
+    out.clear();
+    const char* p = buf.data();
+    const size_t n = buf.size();
+    size_t b = from;
+    while (b < n && (max_lines <= 0 || (int64_t)out.size() < max_lines)) {
+        const void* q = memchr(p + b, '\n', n - b);
+        const size_t e = q ? (size_t)((const char*)q - p) : n;
+        out.emplace_back(b, e);
+        b = e + 1;
+    }
+}
+
+int ingest_threads() {
+    if (const char* e = getenv("PF_LOAD_THREADS")) {
+        const int v = atoi(e);
+        if (v > 0) return std::min(v, 256);
+    }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
+}
+
+// f(i) for i in [0, n) on ingest_threads() threads, contiguous chunks of `grain`
+template <class F>
+void parallel_for(size_t n, size_t grain, F f) {
+    const int nt = (int)std::min<size_t>((size_t)ingest_threads(), (n + grain - 1) / std::max<size_t>(grain, 1));
+    if (nt <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const size_t b = next.fetch_add(grain);
+            if (b >= n) return;
+            const size_t e = std::min(n, b + grain);
+            for (size_t i = b; i < e; ++i) f(i);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+}
+
 // GraphBuilder::load_serialized (graph_builder.cpp:39-59) + build_adj_list (utils.cpp:26-34)
 bool load_adjacency(const std::string& path, std::unordered_map<int, std::vector<int>>& adj_list) {
-    std::ifstream in(path);
-    if (!in.is_open()) return false;
-    std::unordered_map<int, std::vector<int>> adjacency;  // GraphBuilder::adjacency
-    std::string line;
-    while (std::getline(in, line)) {
-        if (line.empty()) continue;
+    std::string buf;
+    if (!read_file(path, buf)) return false;
+    std::vector<std::pair<size_t, size_t>> lines;
+    split_lines(buf, 0, 0, lines);
+    // one line "uid,n1,n2,..." -> (uid, neighbours); tokens trimmed (trim_copy_g), empty skipped
+    std::vector<int> uid(lines.size(), -1);
+    std::vector<std::vector<int>> nb(lines.size());
+    parallel_for(lines.size(), 4096, [&](size_t i) {
+        const size_t lb = lines[i].first, le = lines[i].second;
         bool first = true;
-        int uid = -1;
-        for_each_token(line, ',', [&](size_t b, size_t e) {
-            while (b < e && is_space((unsigned char)line[b])) ++b;  // trim_copy_g
-            if (b == e) return;
-            if (first) { uid = atoi_at(line, b); first = false; return; }
-            adjacency[uid].push_back(atoi_at(line, b));
-        });
+        size_t b = lb;
+        while (b < le) {
+            const void* q = memchr(buf.data() + b, ',', le - b);
+            const size_t e = q ? (size_t)((const char*)q - buf.data()) : le;
+            size_t s = b;
+            while (s < e && is_space((unsigned char)buf[s])) ++s;
+            if (s < e) {
+                const int v = atoi(buf.c_str() + s);  // stops at ',' like atoi on the token copy
+                if (first) { uid[i] = v; first = false; }
+                else nb[i].push_back(v);
+            }
+            b = e + 1;
+        }
+    });
+    std::unordered_map<int, std::vector<int>> adjacency;  // GraphBuilder::adjacency
+    for (size_t i = 0; i < lines.size(); ++i) {
+        if (nb[i].empty()) continue;  // adjacency[uid] is touched only by a push_back
+        std::vector<int>& a = adjacency[uid[i]];
+        if (a.empty()) a = std::move(nb[i]);  // a repeated uid line appends
+        else a.insert(a.end(), nb[i].begin(), nb[i].end());
     }
     for (auto& kv : adjacency) {  // build_adj_list: out[u].push_back in adjacency order
         std::vector<int>& o = adj_list[kv.first];
-        o.insert(o.end(), kv.second.begin(), kv.second.end());
+        if (o.empty()) o = std::move(kv.second);
+        else o.insert(o.end(), kv.second.begin(), kv.second.end());
     }
+    return true;
+}
+
+// One users_encoded data line -> r (user_loader.cpp:40-88); false for an empty line or uid 0
+bool parse_user(const std::string& line, size_t T, std::vector<std::string>& parts, Row& r) {
+    if (line.empty()) return false;
+    size_t np = 0;
+    split_csv(line, parts, np);
+    const int uid = atoi(parts[0].c_str());
+    if (uid == 0) return false;
+    auto has = [&](size_t i) { return i < np && !parts[i].empty(); };
+    r.uid = uid;
+    r.pub = has(1) ? atoi(parts[1].c_str()) : -1;
+    r.comp = has(2) ? atoi(parts[2].c_str()) : -1;
+    r.gen = has(3) ? atoi(parts[3].c_str()) : -1;
+    r.age = has(5) ? atoi(parts[5].c_str()) : 0;
+    if (has(6))
+        for_each_token(parts[6], ';', [&](size_t b, size_t e) {
+            if (b < e) r.clubs.push_back((uint32_t)atoi_at(parts[6], b));
+        });
+    if (has(7))
+        for_each_token(parts[7], ';', [&](size_t b, size_t e) {
+            if (b < e) r.friends.push_back((uint32_t)atoi_at(parts[7], b));
+        });
+    r.reg[0] = r.reg[1] = r.reg[2] = -1;
+    if (has(4)) {
+        std::string rf = parts[4];
+        if (rf.size() >= 2 && rf.front() == '"' && rf.back() == '"') rf = rf.substr(1, rf.size() - 2);
+        int pi = 0;
+        for_each_token(rf, ';', [&](size_t b, size_t e) {
+            if (pi >= 3) return;
+            if (b < e) r.reg[pi] = atoi_at(rf, b);
+            ++pi;
+        });
+    }
+    r.col_off.resize(T + 1);
+    for (size_t t = 0; t < T; ++t) {
+        r.col_off[t] = (int32_t)r.tok.size();
+        const size_t idx = 8 + t;
+        if (!has(idx)) continue;
+        std::string s = parts[idx];  // parse_tok_field (utils.cpp:52-68)
+        if (s.size() >= 2 && s.front() == '"' && s.back() == '"') s = s.substr(1, s.size() - 2);
+        const size_t base = r.tok.size();
+        for_each_token(s, ';', [&](size_t b, size_t e) {
+            if (b == e) return;
+            const size_t p = s.find(':', b);
+            if (p == std::string::npos || p >= e) return;
+            const int tid = atoi_at(s, b), cnt = atoi_at(s, p + 1);
+            // token_cols[t][tid] = cnt: a repeated tid keeps its first position, takes the last count
+            for (size_t k = base; k < r.tok.size(); ++k)
+                if (r.tok[k].first == tid) { r.tok[k].second = cnt; return; }
+            r.tok.emplace_back(tid, cnt);
+        });
+    }
+    r.col_off[T] = (int32_t)r.tok.size();
     return true;
 }
 
 // load_users_encoded (user_loader.cpp:10-96)
 bool load_users(const std::string& path, int64_t max_lines, pf_dataset& d) {
-    std::ifstream in(path);
-    if (!in.is_open()) return false;
-    std::string line;
-    if (!std::getline(in, line)) return false;  // header
+    std::string buf;
+    if (!read_file(path, buf)) return false;
+    const void* h = memchr(buf.data(), '\n', buf.size());
+    if (buf.empty()) return false;  // no header line
+    const size_t from = h ? (size_t)((const char*)h - buf.data()) + 1 : buf.size();
+    std::vector<std::pair<size_t, size_t>> lines;
+    split_lines(buf, from, max_lines, lines);
     const size_t T = d.cols.size();
-    std::vector<std::string> parts;
-    size_t np = 0;
-    int64_t c = 0;
-    while (std::getline(in, line) && (max_lines <= 0 || c < max_lines)) {
-        ++c;
-        if (line.empty()) continue;
-        split_csv(line, parts, np);
-        const int uid = atoi(parts[0].c_str());
-        if (uid == 0) continue;
-        auto has = [&](size_t i) { return i < np && !parts[i].empty(); };
-        Row r;
-        r.uid = uid;
-        r.pub = has(1) ? atoi(parts[1].c_str()) : -1;
-        r.comp = has(2) ? atoi(parts[2].c_str()) : -1;
-        r.gen = has(3) ? atoi(parts[3].c_str()) : -1;
-        r.age = has(5) ? atoi(parts[5].c_str()) : 0;
-        if (has(6))
-            for_each_token(parts[6], ';', [&](size_t b, size_t e) {
-                if (b < e) r.clubs.push_back((uint32_t)atoi_at(parts[6], b));
-            });
-        if (has(7))
-            for_each_token(parts[7], ';', [&](size_t b, size_t e) {
-                if (b < e) r.friends.push_back((uint32_t)atoi_at(parts[7], b));
-            });
-        r.reg[0] = r.reg[1] = r.reg[2] = -1;
-        if (has(4)) {
-            std::string rf = parts[4];
-            if (rf.size() >= 2 && rf.front() == '"' && rf.back() == '"') rf = rf.substr(1, rf.size() - 2);
-            int pi = 0;
-            for_each_token(rf, ';', [&](size_t b, size_t e) {
-                if (pi >= 3) return;
-                if (b < e) r.reg[pi] = atoi_at(rf, b);
-                ++pi;
-            });
+    std::vector<Row> parsed(lines.size());
+    std::vector<uint8_t> ok(lines.size(), 0);
+    const size_t grain = 2048;
+    parallel_for((lines.size() + grain - 1) / grain, 1, [&](size_t g) {
+        std::vector<std::string> parts;
+        std::string line;
+        const size_t e = std::min(lines.size(), (g + 1) * grain);
+        for (size_t i = g * grain; i < e; ++i) {
+            line.assign(buf, lines[i].first, lines[i].second - lines[i].first);
+            ok[i] = parse_user(line, T, parts, parsed[i]) ? 1 : 0;
         }
-        r.col_off.resize(T + 1);
-        for (size_t t = 0; t < T; ++t) {
-            r.col_off[t] = (int32_t)r.tok.size();
-            const size_t idx = 8 + t;
-            if (!has(idx)) continue;
-            std::string s = parts[idx];  // parse_tok_field (utils.cpp:52-68)
-            if (s.size() >= 2 && s.front() == '"' && s.back() == '"') s = s.substr(1, s.size() - 2);
-            const size_t base = r.tok.size();
-            for_each_token(s, ';', [&](size_t b, size_t e) {
-                if (b == e) return;
-                const size_t p = s.find(':', b);
-                if (p == std::string::npos || p >= e) return;
-                const int tid = atoi_at(s, b), cnt = atoi_at(s, p + 1);
-                // token_cols[t][tid] = cnt: a repeated tid keeps its first position, takes the last count
-                for (size_t k = base; k < r.tok.size(); ++k)
-                    if (r.tok[k].first == tid) { r.tok[k].second = cnt; return; }
-                r.tok.emplace_back(tid, cnt);
-            });
-        }
-        r.col_off[T] = (int32_t)r.tok.size();
+    });
+    std::string().swap(buf);
+    d.rows.reserve(lines.size());  // (the profiles map is not reserved: its bucket sequence, and
+                                   // so its iteration order, stays the reference's)
+    for (size_t i = 0; i < lines.size(); ++i) {
+        if (!ok[i]) continue;
         // out_profiles[p.user_id] = std::move(p): a repeated uid replaces the profile in place
-        auto ins = d.profiles.emplace(uid, (int32_t)d.rows.size());
-        if (ins.second) d.rows.push_back(std::move(r));
-        else d.rows[ins.first->second] = std::move(r);
+        auto ins = d.profiles.emplace(parsed[i].uid, (int32_t)d.rows.size());
+        if (ins.second) d.rows.push_back(std::move(parsed[i]));
+        else d.rows[ins.first->second] = std::move(parsed[i]);
     }
-    d.info.lines_read = c;
+    d.info.lines_read = (int64_t)lines.size();
     return true;
 }
 
@@ -273,33 +383,47 @@ void build_desc(pf_dataset& d) {
     const int32_t n = (int32_t)d.rows.size(), T = (int32_t)d.cols.size();
     d.uid.resize(n); d.pub.resize(n); d.comp.resize(n); d.gen.resize(n); d.age.resize(n);
     d.reg.resize((size_t)3 * n);
-    d.club_off.assign(1, 0); d.friend_off.assign(1, 0); d.tok_off.assign(1, 0);
-    d.club_off.reserve(n + 1); d.friend_off.reserve(n + 1); d.tok_off.reserve((size_t)n * T + 1);
-    size_t nc = 0, nf = 0, nt = 0;
-    for (const Row& r : d.rows) { nc += r.clubs.size(); nf += r.friends.size(); nt += r.tok.size(); }
-    d.club_ids.reserve(nc); d.friend_ids.reserve(nf); d.tok_tid.reserve(nt); d.tok_tf.reserve(nt);
+    // row i's lists go to offsets fixed by a prefix pass, then rows are copied on threads
+    d.club_off.assign((size_t)n + 1, 0); d.friend_off.assign((size_t)n + 1, 0);
+    d.tok_off.assign((size_t)n * T + 1, 0);
+    std::vector<int64_t> tbase((size_t)n + 1, 0);
     for (int32_t i = 0; i < n; ++i) {
+        const Row& r = d.rows[i];
+        d.club_off[i + 1] = d.club_off[i] + (int64_t)r.clubs.size();
+        d.friend_off[i + 1] = d.friend_off[i] + (int64_t)r.friends.size();
+        tbase[i + 1] = tbase[i] + (int64_t)r.tok.size();
+    }
+    d.club_ids.resize((size_t)d.club_off[n]); d.friend_ids.resize((size_t)d.friend_off[n]);
+    d.tok_tid.resize((size_t)tbase[n]); d.tok_tf.resize((size_t)tbase[n]);
+    parallel_for((size_t)n, 8192, [&](size_t i) {
         const Row& r = d.rows[i];
         d.uid[i] = r.uid; d.pub[i] = r.pub; d.comp[i] = r.comp; d.gen[i] = r.gen; d.age[i] = r.age;
         for (int k = 0; k < 3; ++k) d.reg[(size_t)3 * i + k] = r.reg[k];
-        d.club_ids.insert(d.club_ids.end(), r.clubs.begin(), r.clubs.end());
-        d.club_off.push_back((int64_t)d.club_ids.size());
-        d.friend_ids.insert(d.friend_ids.end(), r.friends.begin(), r.friends.end());
-        d.friend_off.push_back((int64_t)d.friend_ids.size());
-        for (int32_t t = 0; t < T; ++t) {
-            for (int32_t k = r.col_off[t]; k < r.col_off[t + 1]; ++k) {
-                d.tok_tid.push_back(r.tok[k].first);
-                d.tok_tf.push_back(r.tok[k].second);
-            }
-            d.tok_off.push_back((int64_t)d.tok_tid.size());
+        std::copy(r.clubs.begin(), r.clubs.end(), d.club_ids.begin() + d.club_off[i]);
+        std::copy(r.friends.begin(), r.friends.end(), d.friend_ids.begin() + d.friend_off[i]);
+        const int64_t tb = tbase[i];
+        for (size_t k = 0; k < r.tok.size(); ++k) {
+            d.tok_tid[(size_t)tb + k] = r.tok[k].first;
+            d.tok_tf[(size_t)tb + k] = r.tok[k].second;
         }
-    }
-    d.adj_uid.clear(); d.adj_off.assign(1, 0); d.adj_nbr.clear();
+        for (int32_t t = 0; t < T; ++t) d.tok_off[(size_t)i * T + t + 1] = tb + r.col_off[t + 1];
+    });
+    // adjacency rows in adj_list's iteration order
+    std::vector<const std::vector<int>*> arow;
+    arow.reserve(d.adj_list.size());
+    d.adj_uid.clear();
+    d.adj_uid.reserve(d.adj_list.size());
+    d.adj_off.assign(1, 0);
+    d.adj_off.reserve(d.adj_list.size() + 1);
     for (auto& kv : d.adj_list) {
         d.adj_uid.push_back(kv.first);
-        d.adj_nbr.insert(d.adj_nbr.end(), kv.second.begin(), kv.second.end());
-        d.adj_off.push_back((int64_t)d.adj_nbr.size());
+        arow.push_back(&kv.second);
+        d.adj_off.push_back(d.adj_off.back() + (int64_t)kv.second.size());
     }
+    d.adj_nbr.resize((size_t)d.adj_off.back());
+    parallel_for(arow.size(), 8192, [&](size_t j) {
+        std::copy(arow[j]->begin(), arow[j]->end(), d.adj_nbr.begin() + d.adj_off[j]);
+    });
     // one map feeds both normaliser sets (api_cli.cpp:163-165)
     const int K = kFixed + T;
     d.npres.assign(K, 0); d.nmean.assign(K, 0.f); d.nsd.assign(K, 0.f);
@@ -344,8 +468,17 @@ int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out) {
     auto bail = [&](const std::string& m) { delete d; return fail(m); };
     if (!load_columns(r + "/config/text_columns.txt", d->cols)) return bail("cannot read config/text_columns.txt");
     if (d->cols.size() > PF_MAX_COLS) return bail("more than PF_MAX_COLS text columns");
+    const bool prof = getenv("PF_HOST_PROF") && atoi(getenv("PF_HOST_PROF")) > 0;
+    auto t0 = std::chrono::steady_clock::now();
+    auto stage = [&](const char* what) {  // PF_HOST_PROF=1: loader stage clocks on stderr
+        const auto t1 = std::chrono::steady_clock::now();
+        if (prof) fprintf(stderr, "[pf_dataset_load] %s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+        t0 = t1;
+    };
     if (!load_adjacency(data + "/adjacency.csv", d->adj_list)) return bail("cannot read data/adjacency.csv");
+    stage("adjacency");
     if (!load_users(data + "/users_encoded.csv", max_lines, *d)) return bail("cannot load users_encoded.csv");
+    stage("users");
     // median age (api_cli.cpp:139-153, user_loader.cpp:98-140)
     int median = 0;
     bool loaded = false;
@@ -370,6 +503,7 @@ int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out) {
     load_norms(data + "/column_normalizers.csv", d->norms);
     d->info.vocab_loaded = load_club_names(data, d->club_names) ? 1 : 0;
     build_desc(*d);
+    stage("ages, normalisers, club names, corpus arrays");
     d->info.n_profiles = (int32_t)d->rows.size();
     d->info.n_cols = (int32_t)d->cols.size();
     d->info.n_adj = (int32_t)d->adj_list.size();

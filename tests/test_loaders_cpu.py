@@ -175,3 +175,56 @@ def test_compute_normalizers_matches_reference(name):
     got = {keys[k]: (int(mean[k].view(np.uint32)), int(sd[k].view(np.uint32))) for k in range(len(keys))}
     assert got == ref_bits
     assert got_csv == ref_csv
+
+
+def test_parallel_ingest_equals_one_thread():
+    """F2: the threaded loaders (line split, parse on threads, ordered insert) give the
+    same corpus arrays and the same hash-container iteration orders as one thread, on a
+    corpus large enough for many parse chunks (edge-case rows included)."""
+    pf = tl.product()
+    c = tl.synth.Corpus(n_users=30000, seed=11, edge_cases=1)
+    with tempfile.TemporaryDirectory() as d:
+        c.write_reference_files(d)
+        c.close()
+        out = {}
+        old = os.environ.get("PF_LOAD_THREADS")
+        try:
+            for th in ("1", "7"):
+                os.environ["PF_LOAD_THREADS"] = th
+                ds = pf.Dataset(d, -1)
+                out[th] = (desc_arrays(ds.desc_ptr()), list(ds.profile_order()), list(ds.adj_order()))
+                ds.close()
+        finally:
+            if old is None:
+                os.environ.pop("PF_LOAD_THREADS", None)
+            else:
+                os.environ["PF_LOAD_THREADS"] = old
+    a1, p1, j1 = out["1"]
+    a7, p7, j7 = out["7"]
+    assert a1["n"] == a7["n"] > 20000
+    for k in a1:
+        assert np.array_equal(np.asarray(a1[k]), np.asarray(a7[k])), k
+    assert p1 == p7 and j1 == j7
+
+
+def test_ingest_last_line_without_newline_and_cr():
+    """std::getline semantics: a last line without '\\n' is a line; a '\\r' stays in the line
+    and stops atoi like any other non-digit."""
+    pf = tl.product()
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "config"))
+        os.makedirs(os.path.join(d, "data"))
+        with open(os.path.join(d, "config", "text_columns.txt"), "w") as f:
+            f.write("about\n")
+        with open(os.path.join(d, "data", "users_encoded.csv"), "w", newline="") as f:
+            f.write("uid,pub,comp,gen,region,age,clubs,friends,about\r\n"
+                    "3,1,40,0,1;2;3,30,7,9,2:1\r\n"
+                    "4,0,50,1,,25,,3,5:2")
+        with open(os.path.join(d, "data", "adjacency.csv"), "w", newline="") as f:
+            f.write("3,4\r\n4,3")
+        ds = pf.Dataset(d)
+        a = desc_arrays(ds.desc_ptr())
+        assert list(a["user_id"]) == [3, 4] and ds.info().lines_read == 2
+        assert list(a["tok_tid"]) == [2, 5] and list(a["tok_tf"]) == [1, 2]
+        mine = {int(u): list(a["adj_nbr"][a["adj_off"][i]:a["adj_off"][i + 1]]) for i, u in enumerate(a["adj_uid"])}
+        assert mine == {3: [4], 4: [3]}

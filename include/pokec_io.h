@@ -67,6 +67,15 @@ typedef struct pf_dataset_info {
  * PF_EINVAL when config/text_columns.txt, data/users_encoded.csv or
  * data/adjacency.csv cannot be read. */
 int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out);
+/* F2 (no reference symbol; the reference re-parses the CSVs at every start, user_loader.cpp:
+ * 10-96, graph_builder.cpp:39-59): pf_dataset_load with a binary cache of the parse at
+ * cache_path.  A cache whose key (the sizes and mtimes of users_encoded.csv and
+ * adjacency.csv, max_lines, the text columns) matches is read instead of the CSVs; otherwise
+ * the CSVs are parsed and the cache is (re)written, best effort (a failed write is not an
+ * error).  *from_cache (may be NULL) gets 1 when the cache served.  The result, its
+ * iteration orders included, equals pf_dataset_load's.  cache_path NULL = pf_dataset_load. */
+int pf_dataset_load_cached(const char* root, int64_t max_lines, const char* cache_path, int32_t* from_cache,
+                           pf_dataset** out);
 void pf_dataset_free(pf_dataset* ds);
 /* Engine input view (valid while ds lives): IDF from profiles, normalisers as loaded. */
 const pf_corpus_desc* pf_dataset_desc(const pf_dataset* ds);

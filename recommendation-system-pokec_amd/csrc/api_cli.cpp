@@ -3,7 +3,7 @@
 // loader progress lines, READY, then one JSON line per input line.  The four
 // recommenders run through the C ABI (pokec_fas.h); start-up uses pokec_io.h.
 //
-//   pokec_api_cli [load_users] [--root DIR] [--device N] [--no-cap]
+//   pokec_api_cli [load_users] [--root DIR] [--device N] [--no-cap] [--cache PATH]
 //
 // load_users is parsed and ignored exactly like the reference (the loader's cap is
 // fixed at 100000 lines, user_loader.cpp:34); --no-cap lifts it for full corpora.
@@ -78,17 +78,19 @@ int main(int argc, char** argv) {
     std::string root = ".";
     int device = 0;
     int64_t cap = PF_LOAD_REFERENCE_CAP;
+    std::string cache;  // --cache PATH: binary cache of the CSV parse (F2), off by default
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--root" && i + 1 < argc) root = argv[++i];
         else if (a == "--device" && i + 1 < argc) device = atoi(argv[++i]);
         else if (a == "--no-cap") cap = 0;
+        else if (a == "--cache" && i + 1 < argc) cache = argv[++i];
         else {
             try { (void)std::stoi(a); } catch (...) {}  // load_users: no effect, as in the reference
         }
     }
     pf_dataset* ds = nullptr;
-    if (pf_dataset_load(root.c_str(), cap, &ds) != PF_OK) {
+    if (pf_dataset_load_cached(root.c_str(), cap, cache.empty() ? nullptr : cache.c_str(), nullptr, &ds) != PF_OK) {
         std::cerr << "[api_cli] " << pf_last_error(nullptr) << "\n";
         return 1;
     }

@@ -871,11 +871,21 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
             return bail(PF_ENODEV);
         }
     }
+    const bool prof = pf::host_prof().on;
+    auto t0 = std::chrono::steady_clock::now();
+    auto stage = [&](const char* what) {  // PF_HOST_PROF=1: pf_open stage clocks on stderr
+        const auto t1 = std::chrono::steady_clock::now();
+        if (prof) fprintf(stderr, "[pf_open] %s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+        t0 = t1;
+    };
     int rc = pf::build_host_corpus(desc, c->hc, c->err);
     if (rc != PF_OK) return bail(rc);
+    stage("host corpus (sorted rows, idf, norms)");
     rc = pf::build_store(c->hc, c->hs, c->err);
     if (rc != PF_OK) return bail(rc);
+    stage("tile store");
     pf::build_postings(c->hc, c->hp);  // hp.ok = false: the stream scan serves every query
+    stage("postings store");
     // PF_SCAN=stream|postings sets the context's initial scan kernel (tests force variants
     // per process with it); pf_set_scan_kernel changes it later
     if (const char* sk = getenv("PF_SCAN")) {
@@ -908,6 +918,7 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         if (e == hipSuccess) e = upload(c, c->d_cells, hp.cells);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    stage("upload");
     if (e != hipSuccess) {
         c->hip_fail(e, "corpus upload");
         return bail(e == hipErrorOutOfMemory ? PF_ENOMEM : PF_ENODEV);

@@ -5,6 +5,11 @@
 // (same key types, same insertion sequence), which fix every iteration order the
 // reference exposes: the profiles map (hold-out drivers), adj_list, and each
 // token_cols map (profile JSON).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -103,6 +108,7 @@ struct pf_dataset {
     std::vector<Row> rows;                             // slot = first appearance of the uid
     std::unordered_map<int, int32_t> profiles;         // uid -> slot, built like out_profiles
     std::unordered_map<int, std::vector<int>> adj_list;// built like build_adj_list(gb.adjacency)
+    std::vector<int32_t> adj_seq;                      // adj_list's key insertion sequence (binary cache)
     std::unordered_map<std::string, std::pair<float, float>> norms;
     std::unordered_map<int, std::string> club_names;
     pf_dataset_info info{};
@@ -203,7 +209,8 @@ void parallel_for(size_t n, size_t grain, F f) {
 }
 
 // GraphBuilder::load_serialized (graph_builder.cpp:39-59) + build_adj_list (utils.cpp:26-34)
-bool load_adjacency(const std::string& path, std::unordered_map<int, std::vector<int>>& adj_list) {
+bool load_adjacency(const std::string& path, std::unordered_map<int, std::vector<int>>& adj_list,
+                    std::vector<int32_t>& adj_seq) {
     std::string buf;
     if (!read_file(path, buf)) return false;
     std::vector<std::pair<size_t, size_t>> lines;
@@ -235,7 +242,10 @@ bool load_adjacency(const std::string& path, std::unordered_map<int, std::vector
         if (a.empty()) a = std::move(nb[i]);  // a repeated uid line appends
         else a.insert(a.end(), nb[i].begin(), nb[i].end());
     }
+    adj_seq.clear();
+    adj_seq.reserve(adjacency.size());
     for (auto& kv : adjacency) {  // build_adj_list: out[u].push_back in adjacency order
+        adj_seq.push_back(kv.first);
         std::vector<int>& o = adj_list[kv.first];
         if (o.empty()) o = std::move(kv.second);
         else o.insert(o.end(), kv.second.begin(), kv.second.end());
@@ -449,6 +459,192 @@ void build_desc(pf_dataset& d) {
     c.norm_present = d.npres.data(); c.norm_mean = d.nmean.data(); c.norm_sd = d.nsd.data();
 }
 
+// ---------------------------------------------------------------- binary cache (F2)
+// The parse phase's output (the rows in slot order, the user loader's line count, the
+// adjacency rows in adj_list's insertion sequence) as flat little-endian arrays, keyed by
+// the two CSVs' sizes and mtimes, the line cap and the text columns.  Re-inserting the
+// uids and adjacency keys in the recorded sequences rebuilds both hash containers with
+// the reference's iteration orders; everything after the parse (median, normalisers,
+// club names, corpus arrays) runs as without the cache.
+constexpr char kCacheMagic[8] = {'P', 'F', 'D', 'S', 'C', 'A', 'C', '1'};
+
+struct CacheKey {
+    bool ok = false;
+    int64_t max_lines = 0, u_size = 0, u_mtime = 0, a_size = 0, a_mtime = 0;
+    std::string cols;  // names joined by '\n'
+};
+
+CacheKey cache_key(const std::string& data, int64_t max_lines, const std::vector<std::string>& cols) {
+    CacheKey k;
+    struct stat su, sa;
+    if (stat((data + "/users_encoded.csv").c_str(), &su) != 0 || stat((data + "/adjacency.csv").c_str(), &sa) != 0)
+        return k;
+    k.max_lines = max_lines <= 0 ? 0 : max_lines;
+    k.u_size = (int64_t)su.st_size;
+    k.u_mtime = (int64_t)su.st_mtim.tv_sec * 1000000000LL + su.st_mtim.tv_nsec;
+    k.a_size = (int64_t)sa.st_size;
+    k.a_mtime = (int64_t)sa.st_mtim.tv_sec * 1000000000LL + sa.st_mtim.tv_nsec;
+    for (auto& c : cols) { k.cols += c; k.cols += '\n'; }
+    k.ok = true;
+    return k;
+}
+
+// Arrays are written straight to the file as (int64 count, raw elements).
+struct Writer {
+    FILE* f;
+    bool ok = true;
+    void raw(const void* p, size_t n) { if (ok && n) ok = fwrite(p, 1, n, f) == n; }
+    template <class T> void put(const T& v) { raw(&v, sizeof(T)); }
+    template <class T> void arr(const std::vector<T>& v) {
+        put((int64_t)v.size());
+        raw(v.data(), sizeof(T) * v.size());
+    }
+};
+
+// The cache file mapped read-only; arrays are used in place.
+struct Reader {
+    const char* p;
+    const char* e;
+    bool ok = true;
+    template <class T> T get() {
+        T v{};
+        if ((size_t)(e - p) < sizeof(T)) { ok = false; return v; }
+        std::memcpy(&v, p, sizeof(T));
+        p += sizeof(T);
+        return v;
+    }
+    template <class T> const T* arr(size_t& n) {  // elements are 4- or 8-byte aligned (see write_cache)
+        const int64_t k = get<int64_t>();
+        if (!ok || k < 0 || (uint64_t)k > (uint64_t)(e - p) / sizeof(T)) { ok = false; n = 0; return nullptr; }
+        const T* v = reinterpret_cast<const T*>(p);
+        n = (size_t)k;
+        p += sizeof(T) * n;
+        return v;
+    }
+};
+
+std::string key_bytes(const CacheKey& k) {
+    std::string b(kCacheMagic, 8);
+    auto put = [&](int64_t v) { b.append(reinterpret_cast<const char*>(&v), 8); };
+    put(k.max_lines); put(k.u_size); put(k.u_mtime); put(k.a_size); put(k.a_mtime);
+    put((int64_t)k.cols.size());
+    b += k.cols;
+    b.append((8 - b.size() % 8) % 8, '\0');  // keep the arrays 8-byte aligned
+    return b;
+}
+
+void write_cache(const std::string& path, const CacheKey& key, const pf_dataset& d) {
+    const size_t n = d.rows.size(), T = d.cols.size();
+    std::vector<int32_t> fixed(n * 8);
+    std::vector<int64_t> coff(n + 1, 0), foff(n + 1, 0), toff(n + 1, 0);
+    std::vector<uint16_t> cnt(n * T + (4 - (n * T) % 4) % 4);  // padded to 8 bytes
+    for (size_t i = 0; i < n; ++i) {
+        const Row& r = d.rows[i];
+        int32_t* f = &fixed[i * 8];
+        f[0] = r.uid; f[1] = r.pub; f[2] = r.comp; f[3] = r.gen; f[4] = r.age;
+        f[5] = r.reg[0]; f[6] = r.reg[1]; f[7] = r.reg[2];
+        coff[i + 1] = coff[i] + (int64_t)r.clubs.size();
+        foff[i + 1] = foff[i] + (int64_t)r.friends.size();
+        toff[i + 1] = toff[i] + (int64_t)r.tok.size();
+        for (size_t t = 0; t < T; ++t) {
+            const int32_t k = r.col_off[t + 1] - r.col_off[t];
+            if (k > 65535) return;  // not cacheable (16-bit per-column counts)
+            cnt[i * T + t] = (uint16_t)k;
+        }
+    }
+    std::vector<uint32_t> clubs((size_t)coff[n] + (coff[n] & 1)), friends((size_t)foff[n] + (foff[n] & 1));
+    std::vector<std::pair<int32_t, int32_t>> tok((size_t)toff[n]);
+    parallel_for(n, 8192, [&](size_t i) {
+        const Row& r = d.rows[i];
+        std::copy(r.clubs.begin(), r.clubs.end(), clubs.begin() + coff[i]);
+        std::copy(r.friends.begin(), r.friends.end(), friends.begin() + foff[i]);
+        std::copy(r.tok.begin(), r.tok.end(), tok.begin() + toff[i]);
+    });
+    std::vector<int64_t> aoff(1, 0);
+    std::vector<int32_t> aseq(d.adj_seq), anbr;
+    for (int32_t u : d.adj_seq) {
+        const std::vector<int>& v = d.adj_list.at(u);
+        anbr.insert(anbr.end(), v.begin(), v.end());
+        aoff.push_back((int64_t)anbr.size());
+    }
+    if (aseq.size() & 1) aseq.push_back(0);  // padding (the real count is aoff.size() - 1)
+    if (anbr.size() & 1) anbr.push_back(0);
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+    Writer w{fopen(tmp.c_str(), "wb")};
+    if (!w.f) return;
+    const std::string kb = key_bytes(key);
+    w.raw(kb.data(), kb.size());
+    w.put(d.info.lines_read);
+    w.put((int64_t)n);
+    w.put((int64_t)coff[n]); w.put((int64_t)foff[n]); w.put((int64_t)aoff.back());
+    w.arr(fixed); w.arr(coff); w.arr(clubs); w.arr(foff); w.arr(friends); w.arr(toff); w.arr(cnt); w.arr(tok);
+    w.arr(aseq); w.arr(aoff); w.arr(anbr);
+    const bool ok = w.ok;
+    if (fclose(w.f) != 0 || !ok || rename(tmp.c_str(), path.c_str()) != 0) remove(tmp.c_str());
+}
+
+bool read_cache(const std::string& path, const CacheKey& key, pf_dataset& d) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || st.st_size <= 0) { close(fd); return false; }
+    const size_t len = (size_t)st.st_size;
+    void* m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return false;
+    struct Unmap { void* m; size_t len; ~Unmap() { munmap(m, len); } } unmap{m, len};
+    const char* base = static_cast<const char*>(m);
+    const std::string kb = key_bytes(key);
+    if (len < kb.size() || std::memcmp(base, kb.data(), kb.size()) != 0) return false;  // stale or foreign
+    Reader rd{base + kb.size(), base + len};
+    const size_t T = d.cols.size();
+    const int64_t lines = rd.get<int64_t>();
+    const size_t n = (size_t)rd.get<int64_t>();
+    const int64_t nclub = rd.get<int64_t>(), nfr = rd.get<int64_t>(), nadj = rd.get<int64_t>();
+    size_t nfixed, ncoff, nclubs, nfoff, nfriends, ntoff, ncnt, ntok, naseq, naoff, nanbr;
+    const int32_t* fixed = rd.arr<int32_t>(nfixed);
+    const int64_t* coff = rd.arr<int64_t>(ncoff);
+    const uint32_t* clubs = rd.arr<uint32_t>(nclubs);
+    const int64_t* foff = rd.arr<int64_t>(nfoff);
+    const uint32_t* friends = rd.arr<uint32_t>(nfriends);
+    const int64_t* toff = rd.arr<int64_t>(ntoff);
+    const uint16_t* cnt = rd.arr<uint16_t>(ncnt);
+    const std::pair<int32_t, int32_t>* tok = rd.arr<std::pair<int32_t, int32_t>>(ntok);
+    const int32_t* aseq = rd.arr<int32_t>(naseq);
+    const int64_t* aoff = rd.arr<int64_t>(naoff);
+    const int32_t* anbr = rd.arr<int32_t>(nanbr);
+    if (!rd.ok || rd.p != rd.e || nfixed != n * 8 || ncoff != n + 1 || nfoff != n + 1 || ntoff != n + 1 ||
+        ncnt < n * T || coff[n] != nclub || foff[n] != nfr || nclubs < (size_t)nclub || nfriends < (size_t)nfr ||
+        toff[n] != (int64_t)ntok || naoff < 1 || naseq < naoff - 1 || aoff[naoff - 1] != nadj || nanbr < (size_t)nadj)
+        return false;
+    for (size_t i = 0; i < n; ++i)  // offsets must be monotone before rows index through them
+        if (coff[i + 1] < coff[i] || foff[i + 1] < foff[i] || toff[i + 1] < toff[i]) return false;
+    for (size_t j = 0; j + 1 < naoff; ++j)
+        if (aoff[j + 1] < aoff[j]) return false;
+    d.rows.clear();
+    d.rows.resize(n);
+    std::atomic<bool> bad{false};
+    parallel_for(n, 8192, [&](size_t i) {
+        Row& r = d.rows[i];
+        const int32_t* f = &fixed[i * 8];
+        r.uid = f[0]; r.pub = f[1]; r.comp = f[2]; r.gen = f[3]; r.age = f[4];
+        r.reg[0] = f[5]; r.reg[1] = f[6]; r.reg[2] = f[7];
+        r.clubs.assign(clubs + coff[i], clubs + coff[i + 1]);
+        r.friends.assign(friends + foff[i], friends + foff[i + 1]);
+        r.tok.assign(tok + toff[i], tok + toff[i + 1]);
+        r.col_off.resize(T + 1);
+        r.col_off[0] = 0;
+        for (size_t t = 0; t < T; ++t) r.col_off[t + 1] = r.col_off[t] + cnt[i * T + t];
+        if ((int64_t)r.col_off[T] != toff[i + 1] - toff[i]) bad = true;
+    });
+    if (bad) { d.rows.clear(); return false; }
+    for (size_t i = 0; i < n; ++i) d.profiles.emplace(d.rows[i].uid, (int32_t)i);  // slot order = first appearance
+    d.adj_seq.assign(aseq, aseq + (naoff - 1));
+    for (size_t j = 0; j + 1 < naoff; ++j) d.adj_list[aseq[j]].assign(anbr + aoff[j], anbr + aoff[j + 1]);
+    d.info.lines_read = lines;
+    return true;
+}
+
 void write_int_list(std::string& o, const std::vector<uint32_t>& v) {
     for (size_t i = 0; i < v.size(); ++i) {
         if (i) o += ',';
@@ -461,8 +657,14 @@ void write_int_list(std::string& o, const std::vector<uint32_t>& v) {
 extern "C" {
 
 int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out) {
+    return pf_dataset_load_cached(root, max_lines, nullptr, nullptr, out);
+}
+
+int pf_dataset_load_cached(const char* root, int64_t max_lines, const char* cache_path, int32_t* from_cache,
+                           pf_dataset** out) {
     if (!root || !out) return fail("null argument");
     *out = nullptr;
+    if (from_cache) *from_cache = 0;
     auto d = new pf_dataset();
     const std::string r(root), data = r + "/data";
     auto bail = [&](const std::string& m) { delete d; return fail(m); };
@@ -475,10 +677,20 @@ int pf_dataset_load(const char* root, int64_t max_lines, pf_dataset** out) {
         if (prof) fprintf(stderr, "[pf_dataset_load] %s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
         t0 = t1;
     };
-    if (!load_adjacency(data + "/adjacency.csv", d->adj_list)) return bail("cannot read data/adjacency.csv");
-    stage("adjacency");
-    if (!load_users(data + "/users_encoded.csv", max_lines, *d)) return bail("cannot load users_encoded.csv");
-    stage("users");
+    const CacheKey key = cache_key(data, max_lines, d->cols);
+    if (cache_path && key.ok && read_cache(cache_path, key, *d)) {
+        if (from_cache) *from_cache = 1;
+        stage("binary cache");
+    } else {
+        if (!load_adjacency(data + "/adjacency.csv", d->adj_list, d->adj_seq)) return bail("cannot read data/adjacency.csv");
+        stage("adjacency");
+        if (!load_users(data + "/users_encoded.csv", max_lines, *d)) return bail("cannot load users_encoded.csv");
+        stage("users");
+        if (cache_path && key.ok) {
+            write_cache(cache_path, key, *d);  // best effort: a failed write leaves no file behind
+            stage("cache write");
+        }
+    }
     // median age (api_cli.cpp:139-153, user_loader.cpp:98-140)
     int median = 0;
     bool loaded = false;

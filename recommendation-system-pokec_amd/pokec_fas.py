@@ -28,7 +28,7 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
            "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_set_scan_kernel"]
 # include/pokec_io.h: loaders and hold-out drivers
-IO_EXPORTS = ["pf_dataset_load", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
+IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
               "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests",
               "pf_eval_holdout_friends", "pf_eval_recommendation_tests"]
@@ -90,6 +90,7 @@ def lib():
         L.pf_profile_reset.argtypes = [V]
         L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
         L.pf_dataset_load.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(V)]
+        L.pf_dataset_load_cached.argtypes = [ctypes.c_char_p, I64, ctypes.c_char_p, ctypes.POINTER(I32), ctypes.POINTER(V)]
         L.pf_dataset_free.argtypes = [V]
         L.pf_dataset_free.restype = None
         L.pf_dataset_desc.argtypes = [V]
@@ -255,11 +256,16 @@ class Dataset:
     """The reference's start-up loaders over a data directory (pf_dataset_load): the
     corpus the engine opens on, plus the reference's own iteration orders.  Host only."""
 
-    def __init__(self, root, max_lines=PF_LOAD_REFERENCE_CAP):
+    def __init__(self, root, max_lines=PF_LOAD_REFERENCE_CAP, cache=None):
+        """cache: path of a binary cache of the parse (pf_dataset_load_cached); None = none.
+        self.from_cache tells whether the cache served."""
         L = lib()
         self._L = L
         self.h = ctypes.c_void_p()
-        rc = L.pf_dataset_load(os.fsencode(root), max_lines, ctypes.byref(self.h))
+        fc = ctypes.c_int32(0)
+        rc = L.pf_dataset_load_cached(os.fsencode(root), max_lines, os.fsencode(cache) if cache else None,
+                                      ctypes.byref(fc), ctypes.byref(self.h))
+        self.from_cache = bool(fc.value)
         if rc != PF_OK:
             raise FasError(f"pf_dataset_load failed ({rc}): {L.pf_last_error(None).decode()}")
 

@@ -220,15 +220,18 @@ def test_api_cli_transcript_matches_reference():
         stdin = f.read()
     with gzip.open(os.path.join(tl.GOLDEN, "api", "transcript_stdout.txt.gz"), "rb") as f:
         ref = f.read()
+    want = ref.decode().splitlines()
     with tempfile.TemporaryDirectory() as d:
         tl.regen_reference_dir("api", d)
-        r = subprocess.run([exe, m["load_users"]], cwd=d, input=stdin, capture_output=True, timeout=600)
-    assert r.returncode == 0, r.stderr.decode()
-    got = r.stdout.decode().splitlines()
-    want = ref.decode().splitlines()
-    assert len(got) == len(want)
-    for i, (g, w) in enumerate(zip(got, want)):
-        assert g == w, f"line {i}: {g[:200]} != {w[:200]}"
+        # plain, then with the F2 binary cache (the first run writes it, the second reads it)
+        for extra in ([], ["--cache", "parse.bin"], ["--cache", "parse.bin"]):
+            r = subprocess.run([exe, m["load_users"]] + extra, cwd=d, input=stdin, capture_output=True, timeout=600)
+            assert r.returncode == 0, r.stderr.decode()
+            got = r.stdout.decode().splitlines()
+            assert len(got) == len(want), extra
+            for i, (g, w) in enumerate(zip(got, want)):
+                assert g == w, f"{extra} line {i}: {g[:200]} != {w[:200]}"
+        assert os.path.exists(os.path.join(d, "parse.bin"))
 
 
 def test_holdout_drivers_match_reference():

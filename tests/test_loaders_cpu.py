@@ -228,3 +228,64 @@ def test_ingest_last_line_without_newline_and_cr():
         assert list(a["tok_tid"]) == [2, 5] and list(a["tok_tf"]) == [1, 2]
         mine = {int(u): list(a["adj_nbr"][a["adj_off"][i]:a["adj_off"][i + 1]]) for i, u in enumerate(a["adj_uid"])}
         assert mine == {3: [4], 4: [3]}
+
+
+def _snapshot(ds):
+    uids = list(ds.profile_order())
+    js = []
+    for u in uids[:50] + uids[-50:]:
+        js.append(ds.profile_json(u))
+    info = ds.info()
+    return (desc_arrays(ds.desc_ptr()), uids, list(ds.adj_order()), js,
+            (info.lines_read, info.n_profiles, info.n_adj, info.median_age, info.ages_replaced))
+
+
+def _same(x, y):
+    a, b = x[0], y[0]
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    assert x[1:] == y[1:]
+
+
+def test_binary_cache_equals_csv_parse():
+    """F2 cache: a load served by the binary cache equals the CSV parse (corpus arrays,
+    profiles / adj_list iteration orders, profile JSON, info); a changed CSV or a damaged
+    cache file falls back to the parse and rewrites the cache."""
+    pf = tl.product()
+    c = tl.synth.Corpus(n_users=6000, seed=12, edge_cases=1)
+    with tempfile.TemporaryDirectory() as d:
+        c.write_reference_files(d)
+        c.close()
+        cache = os.path.join(d, "parse.bin")
+        for cap in (-1, 2500):
+            if os.path.exists(cache):
+                os.remove(cache)
+            plain = pf.Dataset(d, cap)
+            ref = _snapshot(plain)
+            plain.close()
+            first = pf.Dataset(d, cap, cache=cache)
+            assert not first.from_cache and os.path.exists(cache)
+            _same(_snapshot(first), ref)
+            first.close()
+            hit = pf.Dataset(d, cap, cache=cache)
+            assert hit.from_cache
+            _same(_snapshot(hit), ref)
+            hit.close()
+        # the key holds the line cap: another cap re-parses
+        other = pf.Dataset(d, 100, cache=cache)
+        assert not other.from_cache and other.info().lines_read == 100
+        other.close()
+        # damaged cache: truncated -> parse again, then served again
+        with open(cache, "r+b") as f:
+            f.truncate(os.path.getsize(cache) // 2)
+        again = pf.Dataset(d, 100, cache=cache)
+        assert not again.from_cache
+        again.close()
+        assert pf.Dataset(d, 100, cache=cache).from_cache
+        # a changed adjacency file (size / mtime) is a stale key
+        with open(os.path.join(d, "data", "adjacency.csv"), "a") as f:
+            f.write("1,2\n")
+        stale = pf.Dataset(d, 100, cache=cache)
+        assert not stale.from_cache
+        fresh = pf.Dataset(d, 100)
+        _same(_snapshot(stale), _snapshot(fresh))

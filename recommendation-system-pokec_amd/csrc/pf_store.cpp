@@ -5,10 +5,12 @@
 #include "pf_store.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <mutex>
 #include <thread>
 
 namespace pf {
@@ -584,19 +586,35 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     // ---- set lists: entries idx << 8 | multiplicity (recommender.cpp:119-128 counts B's
     // duplicates); one list per distinct club / friend id
     std::vector<uint64_t> ckeys, fkeys;
-    std::vector<uint32_t> tmp;
+    // keys (id, idx, multiplicity) are collected per row range on threads; each (id, idx) pair
+    // occurs once, so the radix sort below fixes their order whatever the concatenation order
     auto collect = [&](const std::vector<int64_t>& o, const std::vector<uint32_t>& ids, std::vector<uint64_t>& keys) -> bool {
-        for (int32_t i = 0; i < n; ++i) {
-            tmp.assign(ids.begin() + o[i], ids.begin() + o[i + 1]);
-            std::sort(tmp.begin(), tmp.end());
-            for (size_t a = 0; a < tmp.size();) {
-                size_t b = a;
-                while (b < tmp.size() && tmp[b] == tmp[a]) ++b;
-                if (b - a > 255) return false;
-                keys.push_back(((uint64_t)tmp[a] << 32) | ((uint64_t)i << 8) | (uint64_t)(b - a));
-                a = b;
+        std::mutex mu;
+        std::vector<std::pair<int64_t, std::vector<uint64_t>>> parts;
+        std::atomic<bool> ok{true};
+        par_for(n, [&](int64_t lo, int64_t hi) {
+            std::vector<uint64_t> mine;
+            std::vector<uint32_t> tmp;
+            for (int64_t i = lo; i < hi && ok; ++i) {
+                tmp.assign(ids.begin() + o[i], ids.begin() + o[i + 1]);
+                std::sort(tmp.begin(), tmp.end());
+                for (size_t a = 0; a < tmp.size();) {
+                    size_t b = a;
+                    while (b < tmp.size() && tmp[b] == tmp[a]) ++b;
+                    if (b - a > 255) { ok = false; break; }
+                    mine.push_back(((uint64_t)tmp[a] << 32) | ((uint64_t)i << 8) | (uint64_t)(b - a));
+                    a = b;
+                }
             }
-        }
+            std::lock_guard<std::mutex> g(mu);
+            parts.emplace_back(lo, std::move(mine));
+        });
+        if (!ok) return false;
+        std::sort(parts.begin(), parts.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        size_t tot = 0;
+        for (auto& pr : parts) tot += pr.second.size();
+        keys.reserve(tot);
+        for (auto& pr : parts) keys.insert(keys.end(), pr.second.begin(), pr.second.end());
         return true;
     };
     if (!collect(hc.club_off, hc.clubs, ckeys) || !collect(hc.friend_off, hc.friends, fkeys))

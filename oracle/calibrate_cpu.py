@@ -1,0 +1,84 @@
+"""calibrate the CPU baseline bench.py reports (oracle/refcpu.cpp, the
+clean-room restatement, `cpu_baseline.kind` "port") against the REAL reference compiled from
+its own sources (oracle/_ref/ref_timing, built by `make -C oracle ref`).
+
+TEST INFRASTRUCTURE ONLY; runs in the build container (it needs oracle/_ref and so
+/root/reference at build time).  Both sides run single-threaded on the same synthetic corpus
+(written in the reference's formats, 100,000 users = the reference loader's line cap), the
+same query uids, all-candidates interest top-10, timing scoring + top-k only.
+It also checks that both return the same top-10 ids and score bits.
+
+    python oracle/calibrate_cpu.py [--users 100000] [--queries 12] [--out profiles/cpu_calibration.json]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "recommendation-system-pokec_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=100000)
+    ap.add_argument("--queries", type=int, default=12)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    exe = os.path.join(HERE, "_ref", "ref_timing")
+    if not os.path.exists(exe):
+        sys.exit("build the reference first: make -C oracle ref")
+    import pokec_testlib as tl
+    import synth
+    pf = tl.product()
+    rng = np.random.default_rng(7)
+    q = [int(x) for x in rng.choice(np.arange(1, args.users + 1), args.queries, replace=False)]
+    with tempfile.TemporaryDirectory() as d:
+        c = synth.Corpus(n_users=args.users, seed=5, edge_cases=0, threads=8)
+        c.write_reference_files(d)
+        c.close()
+        # the real reference, one process, one thread
+        r = subprocess.run(["taskset", "-c", "0", exe, d] + [str(u) for u in q], capture_output=True, text=True,
+                           check=True)
+        ref_rows = [ln.split() for ln in r.stdout.splitlines() if ln and ln[0].isdigit()]
+        ref_total = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("total")][0]
+        ref_n, ref_s = int(ref_total[1]), float(ref_total[2])
+        # the port (oracle/refcpu.cpp) on the same files, loaded by the product's loader
+        ds = pf.Dataset(d, pf.PF_LOAD_REFERENCE_CAP)
+        orc = tl.Oracle(None, desc_ptr=ds.desc_ptr())
+        port_s, same = 0.0, True
+        os.sched_setaffinity(0, {0})
+        for u, row in zip(q, ref_rows):
+            t = time.perf_counter()
+            got = orc.interest([u], 10, tl.PF_MODE_ALL, 0)[0]
+            port_s += time.perf_counter() - t
+            ref_ids = [int(x.split(":")[0]) for x in row[3:]]
+            ref_bits = [int(x.split(":")[1], 16) for x in row[3:]]
+            same &= list(got[0]) == ref_ids and [int(b) for b in got[1].view(np.uint32)] == ref_bits
+        orc.close()
+        ds.close()
+    out = {"what": "all-candidates interest top-10, single thread, scoring + top-k timed",
+           "users": args.users, "queries": len(q), "candidates_scored": ref_n,
+           "reference": {"seconds": round(ref_s, 3), "candidates_per_s": ref_n / ref_s,
+                         "binary": "oracle/_ref/ref_timing (reference sources, g++ -O3)"},
+           "port": {"seconds": round(port_s, 3), "candidates_per_s": ref_n / port_s,
+                    "binary": "oracle/librefcpu.so (oracle/refcpu.cpp, g++ -O2)"},
+           "port_over_reference": (ref_n / port_s) / (ref_n / ref_s),
+           "top10_identical": bool(same)}
+    s = json.dumps(out)
+    print(s)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()

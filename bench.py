@@ -97,6 +97,8 @@ def main():
                     help="cfg2: N queries per step (1 per GPU, weak scaling; the default); "
                          "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--time-every", type=int, default=1,
+                    help="HIP-event timing on every n-th scan launch of the timed region (1 = all)")
     ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
                     help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
     args = ap.parse_args()
@@ -159,6 +161,11 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # HIP events on every scan launch of the timed region by default.  They cost ~9 us of
+    # stream time per single-query step; --time-every 3 times launches 0, 3, 6, ... only
+    # (r1p: +2 % candidates/s, but 17 sampled queries averaged 235 us against rocprof's 209 us
+    # over all launches, so the default keeps every launch timed)
+    eng.profile_sample(args.time_every)
     eng.profile_reset()
     t_start = time.perf_counter()
     for i in range(warm, warm + steps):
@@ -215,6 +222,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
+                     "timed_launches": launches, "timed_every": args.time_every,
                      "alg_bytes_per_launch": alg_bytes,
                      # what the kernel really moves: PMC FETCH_SIZE bytes over the same launch time
                      "dram_gbs": None if traffic is None else traffic / (avg_launch_ms * 1e-3) / 1e9,

@@ -231,6 +231,9 @@ float pf_last_scan_ms(const pf_ctx* ctx);
  * summed device time of every scan launch since the reset (synchronises). */
 int pf_profile_reset(pf_ctx* ctx);
 int pf_profile_read(pf_ctx* ctx, double* total_ms, int64_t* launches);
+/* Time only scan launches 0, every, 2*every, ... after a reset (default 1 = all); the
+ * others run without timing events.  *launches in pf_profile_read counts timed launches. */
+int pf_profile_sample(pf_ctx* ctx, int32_t every);
 
 #ifdef __cplusplus
 }

@@ -143,6 +143,8 @@ struct pf_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
     size_t prof_used = 0;
     bool prof_on = false;
+    int64_t prof_seen = 0;   // scan launches since the reset
+    int32_t prof_every = 1;  // time launches 0, every, 2 every, ... (pf_profile_sample)
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -438,6 +440,12 @@ int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
     e0 = c->ev0;
     e1 = c->ev1;
     if (c->prof_on) {
+        // a timed launch costs ~9 us of stream time (two timestamped events, measured at
+        // 231 vs 222 us per single-query step): sampled launches only when asked
+        if (c->prof_seen++ % c->prof_every != 0) {
+            timed = false;
+            return PF_OK;
+        }
         if (c->prof_used == c->prof_ev.size()) {
             hipEvent_t a, b;
             HIPCHK(c, hipEventCreate(&a));
@@ -1201,6 +1209,13 @@ int pf_profile_reset(pf_ctx* c) {
     if (!c) return PF_EINVAL;
     c->prof_on = true;
     c->prof_used = 0;
+    c->prof_seen = 0;
+    return PF_OK;
+}
+
+int pf_profile_sample(pf_ctx* c, int32_t every) {
+    if (!c || every < 1) return PF_EINVAL;
+    c->prof_every = every;
     return PF_OK;
 }
 

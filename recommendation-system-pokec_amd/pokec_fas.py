@@ -26,7 +26,7 @@ MAX_TOPK_DEVICE = 64
 EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_users", "pf_idf", "pf_fas_pairs",
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
-           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_set_scan_kernel"]
+           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -88,6 +88,7 @@ def lib():
         L.pf_last_scan_ms.argtypes = [V]
         L.pf_last_scan_ms.restype = ctypes.c_float
         L.pf_profile_reset.argtypes = [V]
+        L.pf_profile_sample.argtypes = [V, I32]
         L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
         L.pf_dataset_load.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(V)]
         L.pf_dataset_load_cached.argtypes = [ctypes.c_char_p, I64, ctypes.c_char_p, ctypes.POINTER(I32), ctypes.POINTER(V)]
@@ -234,6 +235,10 @@ class FasEngine:
 
     def profile_reset(self):
         self._check(self._L.pf_profile_reset(self.h), "pf_profile_reset")
+
+    def profile_sample(self, every):
+        """Time only every `every`-th scan launch after profile_reset() (1 = all)."""
+        self._check(self._L.pf_profile_sample(self.h, int(every)), "pf_profile_sample")
 
     def profile_read(self):
         """(summed scan-kernel device ms, launches) since profile_reset()."""

@@ -296,6 +296,27 @@ def test_cpp_facade_matches_reference():
     assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))
 
 
+def test_profile_sampling_counts_and_results(big):
+    """pf_profile_sample: with every = 3, launches 0, 3, 6 of nine are timed (positive device
+    time), the untimed ones return the same keys as timed ones; every = 1 times all."""
+    import torch
+    c, eng, orc = big
+    s = torch.cuda.Stream()
+    q = np.array([5], np.int32)
+    outs = [torch.empty((1, 10), dtype=torch.int64, device="cuda") for _ in range(9)]
+    for every, want in ((3, 3), (1, 9)):
+        eng.profile_sample(every)
+        eng.profile_reset()
+        for o in outs:
+            eng.scan_keys_async(q, 10, o.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        ms, n = eng.profile_read()
+        assert n == want and ms > 0.0, (every, n, ms)
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0])
+    eng.profile_sample(1)
+
+
 def test_sharded_scan_merges_to_single_gpu_result(big):
     """The multi-GPU path on one device: each candidate shard's top-k keys (pf_set_shard +
     pf_scan_keys_async), concatenated as the all-gather would, merged by

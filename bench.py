@@ -2,25 +2,36 @@
 """FAS all-candidates scan benchmark (BASELINE.json metric: "FAS candidates scored/sec
 over 1.6M users, top-k=10; 1/2/4/8 GPU + %HBM peak").
 
-Workload (BASELINE.json configs[1]): synthetic Pokec-shaped corpus of
-1,632,803 users (seeded generator tools/pokec_synth.cpp, resident in HBM), interest FAS
-top-10 over every candidate (A13).  One step = one all-candidates pass for a batch of
-queries: at N GPUs the batch holds N distinct query users (1 at N=1, i.e. exactly
-config 2), every rank scores its candidate shard (1/N of the corpus, split by stream
-bytes) for the whole batch, the per-shard top-10 keys are exchanged with one RCCL
-all-gather over xGMI and merged on device.  Per-GPU work is fixed (1.6M pairs/step):
-weak scaling.  value = candidates scored / s over the whole job.  With --workload cfg4 a
-step is a fixed batch of 1024 queries (SURVEY D1 cfg 4, seed 3) over the sharded candidates:
-strong scaling.
+Workload: synthetic Pokec-shaped corpus of 1,632,803 users (seeded
+generator tools/pokec_synth.cpp, resident in HBM), interest FAS top-10 over every candidate
+(A13).  Default by N:
+  N = 1  cfg 2 (BASELINE.json configs[1], the metric's configuration): one query per step,
+         every candidate scored.
+  N > 1  cfg 4 (configs[3]): a fixed batch of 1024 queries per step (seed 3), candidates
+         sharded over the N ranks by posting weight, each rank's per-shard top-10 keys
+         exchanged with one RCCL all-gather over xGMI and merged on device.  Total work is
+         fixed: strong scaling (the north-star ">= 6x at 8 GPUs" is defined on cfg 4).
+--workload cfg2|cfg4 overrides the default (cfg2 at N > 1: N queries per step, one per GPU,
+weak scaling).  value = candidates scored / s over the whole job.
 
-Also reports the roofline of the dominant kernel (fas_post_kernel, the postings scan, by
-default; fas_scan_kernel, the record-stream scan, with --scan-kernel stream; HIP events
-around every launch) with both the algorithmic rate and the measured DRAM share, and the
-CPU baseline (oracle/refcpu.cpp, the reference algorithm with its unordered_map data
-structures, single thread, bounded sample of the same corpus).
+Roofline of the dominant kernel (fas_post_kernel, the postings scan, by default;
+fas_scan_kernel, the record-stream scan, with --scan-kernel stream), HIP events around every
+launch on the kernel's stream:
+  achieved  = the bytes the kernel reads by its access pattern (pf_scan_bytes: headers, cell
+              words, the list entries of the query's lists, their norms)
+              summed over the timed queries / the summed launch time;
+  traffic   = HBM bytes per launch measured in this run by a rocprofv3 --pmc FETCH_SIZE pass
+              of the same command (a child process started before this one touches the GPU;
+              FETCH_SIZE KiB x 1024 x the gfx950 factor calibrated for the kernel's load widths,
+              profiles/fetch_calib_*.json), null when rocprofv3 is absent or --no-pmc;
+  alg_effective_* = SURVEY D3's per-candidate record bytes (b_c, the metric's definition)
+              over the same time, an *effective* rate a postings scan can exceed the peak with.
+CPU baseline: oracle/refcpu.cpp (the reference algorithm with its unordered_map data
+structures), one core, bounded sample of the same corpus, median per query; plus an
+all-cores context figure (one oracle per core).
 
-    python bench.py [--gpus N --steps K --warmup W]        (cfg 2, the headline)
-    python bench.py --workload cfg4 --steps 5 --warmup 1     (cfg 4: 1024 queries per step)
+    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py --workload cfg4 --steps 5 --warmup 1     (cfg 4 at N = 1)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
@@ -47,43 +58,132 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(desc_ptr, seconds_budget=12.0):
-    """Oracle (reference algorithm, unordered_map per profile/column) on one core over a
-    bounded prefix of the same corpus: all-candidates interest top-10 per query."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+SAMPLE_USERS = 150000
+
+
+_DESC = None  # the parent's corpus descriptor, inherited by the forked oracle workers
+
+
+def _oracle_worker(args):
+    """One core's share of the all-cores context figure: queries for `seconds` on its own oracle
+    (forked before any GPU use, so it shares the parent's corpus arrays copy-on-write)."""
+    seed, seconds = args
     import pokec_testlib as tl
-    sample_users = 150000
+    orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=_DESC)
+    rng = np.random.default_rng(seed)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.interest([int(rng.integers(1, SAMPLE_USERS + 1))], TOPK, tl.PF_MODE_ALL, 0)
+        done += 1
+    el = time.perf_counter() - t0
+    cands = (orc.L.ro_num_users(orc.h) - 1) * done
+    orc.close()
+    return cands, el
+
+
+def cpu_baseline(desc_ptr, seconds_budget=12.0, all_cores_seconds=6.0):
+    """Oracle (reference algorithm, unordered_map per profile/column) over a bounded prefix of
+    the same corpus: all-candidates interest top-10 per query.  value = candidates per query /
+    the median single-core query time; all_cores = one oracle per host core
+    (context only, not the x100 denominator)."""
+    import pokec_testlib as tl
     t0 = time.time()
-    orc = tl.Oracle(None, max_users=sample_users, desc_ptr=desc_ptr)
+    orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=desc_ptr)
     build_s = time.time() - t0
     rng = np.random.default_rng(123)
-    done, cands, el = 0, 0, 0.0
-    while el < seconds_budget and done < 64:
-        q = int(rng.integers(1, sample_users + 1))
+    per, el = [], 0.0
+    while el < seconds_budget and len(per) < 64:
+        q = int(rng.integers(1, SAMPLE_USERS + 1))
         t = time.perf_counter()
         orc.interest([q], TOPK, tl.PF_MODE_ALL, 0)
-        el += time.perf_counter() - t
-        cands += orc.L.ro_num_users(orc.h) - 1
-        done += 1
+        dt = time.perf_counter() - t
+        per.append(dt)
+        el += dt
+    n_cand = orc.L.ro_num_users(orc.h) - 1
     orc.close()
-    return {"value": cands / el, "unit": "candidates/s", "cores": 1, "kind": "port",
-            "sample": f"{done} all-candidates interest top-10 queries over the first {sample_users} users of the "
-                      f"same synthetic corpus (oracle/refcpu.cpp, single thread, {el:.1f}s timed, "
-                      f"{build_s:.1f}s map build untimed)"}
-
-
-def pmc_traffic(workload, kernel):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC pass (profiles/pmc_traffic.json,
-    written by tools/profile_round.sh), keyed by workload and kernel."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
+    med = float(np.median(per))
+    out = {"value": n_cand / med, "unit": "candidates/s", "cores": 1, "kind": "port",
+           "cpu_model": cpu_model(), "median_query_s": med, "queries": len(per),
+           "mean_rate": n_cand * len(per) / el,
+           "sample": f"{len(per)} all-candidates interest top-10 queries over the first {SAMPLE_USERS} users of the "
+                     f"same synthetic corpus (oracle/refcpu.cpp -O3, single thread, median of the per-query times, "
+                     f"{el:.1f}s timed, {build_s:.1f}s map build untimed)"}
+    # all-cores context: one oracle process per core (the box's CPU share is 16)
+    global _DESC
+    _DESC = desc_ptr
     try:
-        with open(p) as f:
-            d = json.load(f)
-        e = d.get(f"{workload}:{kernel}")
-        return None if e is None else float(e["bytes_per_launch"])
-    except Exception:
-        return None
+        import multiprocessing as mp
+        ncores = min(16, len(os.sched_getaffinity(0)))
+        ctx = mp.get_context("fork")
+        with ctx.Pool(ncores) as pool:
+            res = pool.map(_oracle_worker, [(1000 + i, all_cores_seconds) for i in range(ncores)])
+        out["all_cores"] = {"value": sum(c for c, _ in res) / max(e for _, e in res), "cores": ncores,
+                            "note": "one oracle process per core, each on the same 150k-user prefix; context only"}
+    except Exception as e:  # context figure only
+        out["all_cores"] = {"value": None, "error": str(e)[:200]}
+    return out
+
+
+def pmc_pass(args, kernel_name):
+    """HBM bytes per timed launch of the scan kernel from a rocprofv3 --pmc FETCH_SIZE pass of
+    this same command, run as a child before this process touches the GPU.  FETCH_SIZE (KiB)
+    x 1024 x the gfx950 factor (profiles/fetch_calib_r2.json: the factor measured on known
+    byte counts of the kernel's load widths; MI355X_MICROARCH.md HBM section)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    factor, fsrc = 2.0, "MI355X_MICROARCH.md (16-B/lane streams)"
+    cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
+    if os.path.exists(cal):
+        try:
+            with open(cal) as f:
+                c = json.load(f)
+            factor, fsrc = float(c["k5_factor"]), "profiles/fetch_calib_r2.json"
+        except Exception:
+            pass
+    d = tempfile.mkdtemp(prefix="pf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [prof, "--pmc", "FETCH_SIZE", "--kernel-include-regex", kernel_name, "-T", "--output-format", "csv",
+           "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--gpus", "1",
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-pmc",
+           "--workload", args.workload, "--scan-kernel", args.scan_kernel, "--users", str(args.users)]
+    try:
+        r = subprocess.run(["timeout", "-s", "KILL", "240"] + cmd, capture_output=True, text=True,
+                           env={**os.environ, "TMPDIR": os.environ.get("TMPDIR", "/tmp")})
+        if r.returncode != 0:
+            return None, f"rocprofv3 pass rc={r.returncode}: {r.stderr[-300:]}"
+        vals = []
+        for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(p) as f:
+                for row in csv.DictReader(f):
+                    if row.get("Counter_Name") == "FETCH_SIZE" and kernel_name in row.get("Kernel_Name", ""):
+                        vals.append((int(row.get("Dispatch_Id", len(vals))), float(row["Counter_Value"])))
+        vals.sort()
+        vals = [v for _, v in vals][-args.steps:]  # the timed launches (the warmup ones come first)
+        if not vals:
+            return None, "no FETCH_SIZE rows"
+        mean = sum(vals) / len(vals)
+        return {"bytes_per_launch": mean * 1024 * factor, "fetch_size_kib_mean": mean, "launches": len(vals),
+                "factor": factor, "factor_source": fsrc}, None
+    except Exception as e:
+        return None, str(e)[:300]
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def main():
@@ -93,10 +193,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
-    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default="cfg2",
-                    help="cfg2: N queries per step (1 per GPU, weak scaling; the default); "
-                         "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong scaling)")
+    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default=None,
+                    help="cfg2: N queries per step (1 per GPU, weak scaling; the default at N = 1); "
+                         "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong "
+                         "scaling; the default at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass (traffic = null)")
     ap.add_argument("--time-every", type=int, default=1,
                     help="HIP-event timing on every n-th scan launch of the timed region (1 = all)")
     ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
@@ -108,6 +210,26 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    if args.workload is None:
+        args.workload = "cfg2" if world == 1 else "cfg4"
+    import synth
+
+    t0 = time.time()
+    corpus = synth.Corpus(n_users=args.users, seed=1, edge_cases=0, threads=16)
+    desc = corpus.desc_ptr()
+    t1 = time.time()
+    # rank 0 at N = 1, before this process touches the GPU: the CPU baseline (its all-cores part
+    # forks oracle workers) and the rocprofv3 PMC pass (a child running this same command)
+    want_kernel = "fas_scan_kernel" if args.scan_kernel == "stream" else "fas_post_kernel"
+    base, pmc, pmc_err = None, None, "not run (N > 1 or --no-pmc)"
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            base = cpu_baseline(desc)
+        if not args.no_pmc:
+            pmc, pmc_err = pmc_pass(args, want_kernel)
+            if pmc_err:
+                log(f"pmc pass: {pmc_err}")
+
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -115,22 +237,19 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    import synth
     import pokec_fas as pf
 
-    t0 = time.time()
-    corpus = synth.Corpus(n_users=args.users, seed=1, edge_cases=0, threads=16)
-    desc = corpus.desc_ptr()
-    t1 = time.time()
-    eng = pf.FasEngine(desc, local)
     t2 = time.time()
+    eng = pf.FasEngine(desc, local)
+    t3 = time.time()
     eng.set_shard(rank, world)
     eng.set_scan_kernel({"auto": pf.PF_SCAN_AUTO, "stream": pf.PF_SCAN_STREAM, "postings": pf.PF_SCAN_POSTINGS}
                         [args.scan_kernel])
     lay = eng.layout()
     kernel_name = "fas_post_kernel" if lay.scan_kernel == pf.PF_SCAN_POSTINGS else "fas_scan_kernel"
-    log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t2 - t1:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
+    if kernel_name != want_kernel:
+        pmc, pmc_err = None, f"the pass profiled {want_kernel}, the engine runs {kernel_name}"
+    log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t3 - t2:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
         f"alg {lay.alg_bytes / 1e9:.3f} GB, packed={lay.packed_tokens}")
 
     cfg4 = args.workload == "cfg4"
@@ -176,6 +295,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     scan_ms, launches = eng.profile_read()
+    eng.profile_sample(0)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -189,11 +309,23 @@ def main():
 
     n_cand = eng.num_users - 1  # candidates per query: every profile but the query (minus adj[q])
     value = Q * n_cand * steps / elapsed
-    avg_launch_ms = scan_ms / max(launches, 1)
-    # algorithmic bytes per launch: SURVEY 8(d) D3 b_c summed over this rank's shard, x queries per launch
+    # bytes per launch by the kernel's access pattern, over the queries timed (this rank's shard)
+    timed_q = qstream[warm:warm + steps].reshape(-1)
+    phys = eng.scan_bytes(timed_q)
+    timed_steps = list(range(0, steps, max(args.time_every, 1)))[:launches] if launches else []
+    phys_per_launch = (float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in timed_steps]))
+                       if timed_steps else None)
+    avg_launch_ms = scan_ms / launches if launches else None
+    # SURVEY 8(d) D3 record bytes of this rank's shard x queries per launch (the metric's definition)
     shard_frac = 1.0 / world
     alg_bytes = lay.alg_bytes * shard_frac * Q
-    achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
+
+    def rate(b):  # GB/s over the average launch
+        return None if (b is None or not avg_launch_ms) else b / (avg_launch_ms * 1e-3) / 1e9
+
+    achieved = rate(phys_per_launch)
+    alg_eff = rate(alg_bytes)
+    traffic = pmc["bytes_per_launch"] if pmc else None
     workload = f"{args.workload}_all_candidates_top{k}_{args.users}users_q{Q}_shard1of{world}"
     if cfg4:
         wl_name = (f"cfg4: {Q}-query batch, interest FAS all-candidates top-10 over the full 1.6M-user corpus, "
@@ -202,7 +334,6 @@ def main():
         wl_name = ("cfg2: full 1.6M-user single-query interest FAS all-candidates top-10"
                    + ("" if world == 1 else f"; {Q} queries/step, candidates sharded over {world} GPUs, "
                                             "RCCL all-gather of per-shard top-10"))
-    traffic = pmc_traffic(workload, kernel_name)
     rec = {
         "metric": METRIC,
         "value": value,
@@ -220,22 +351,26 @@ def main():
                    "workload_key": workload, "n_users": args.users, "queries_per_step": Q, "topk": k,
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
                      "timed_launches": launches, "timed_every": args.time_every,
+                     "bytes_per_launch": phys_per_launch,
+                     "bytes_model": ("pf_scan_bytes: per block 32-B headers, 2 cell words per query list, each list's "
+                                     "cell-range entries (4 B; token entries + 8-B norm), exclusions; staged image "
+                                     "per workgroup" if kernel_name == "fas_post_kernel" else
+                                     "pf_scan_bytes: the shard's record stream + 48-B headers"),
+                     "dram_gbs": rate(traffic),
+                     "dram_frac": None if traffic is None or not avg_launch_ms else rate(traffic) / HBM_PEAK_GBS,
+                     "traffic_source": pmc if pmc else pmc_err,
+                     "alg_effective_gbs": alg_eff,
+                     "alg_effective_frac": None if alg_eff is None else alg_eff / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_bytes,
-                     # what the kernel really moves: PMC FETCH_SIZE bytes over the same launch time
-                     "dram_gbs": None if traffic is None else traffic / (avg_launch_ms * 1e-3) / 1e9,
-                     "dram_frac": None if traffic is None else traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "note": ("postings scan: reads only the query's candidate lists (~0.2 GB), so the "
-                              "algorithmic rate of a full record pass exceeds the HBM peak; dram_frac is the "
-                              "measured HBM share" if kernel_name == "fas_post_kernel" else
-                              "record-stream scan: one pass over every candidate's record"),
-                     "stream_bytes_per_launch": (lay.stream_bytes + lay.header_bytes) * shard_frac * Q},
+                     "note": ("achieved/frac: the bytes this kernel reads by its access pattern; "
+                              "alg_effective_*: SURVEY D3 record bytes b_c of every candidate over the same time (the "
+                              "postings scan reads only the query's lists, so that effective rate can pass the peak)")},
         "topk_selfcheck": consistent,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(desc)
+    if rank == 0 and world == 1 and base is not None:
         rec["cpu_baseline"] = base
         rec["speedup_vs_cpu"] = value / base["value"]
     elif rank == 0:

@@ -176,8 +176,10 @@ int pf_fof_candidates(pf_ctx* ctx, int32_t uid, int32_t limit, int32_t flavour,
  * row (uid absent from adj_list). */
 int pf_set_adj(pf_ctx* ctx, int32_t uid, const int32_t* nbrs, int32_t n);
 
-/* Restrict the all-candidates scan to shard `shard` of `nshards` (candidate
- * slots split by stream bytes); the multi-GPU path merges the per-shard top-k. */
+/* Restrict the all-candidates scan to shard `shard` of `nshards`: contiguous
+ * candidate ranges of equal stream bytes (K1 tiles) and of equal posting weight
+ * (K5 blocks: a fixed share per candidate plus its tokens, clubs and friends);
+ * the multi-GPU path merges the per-shard top-k. */
 int pf_set_shard(pf_ctx* ctx, int32_t shard, int32_t nshards);
 
 /* All-candidates scan kernel.  PF_SCAN_AUTO (default) takes the postings scan
@@ -196,9 +198,14 @@ int pf_set_scan_kernel(pf_ctx* ctx, int32_t kind);
  * 64-bit keys to DEVICE memory d_keys[nq*topk] on `stream` (a hipStream_t;
  * NULL = the context's stream).  Key = (~orderable(score) << 32) | (uid ^
  * 0x80000000): ascending key = (score desc, uid asc); unused slots are
- * UINT64_MAX.  `stream` is used as given (NULL = the HIP null stream), so the
- * caller's collectives on that stream are ordered after the scan.  No host
- * synchronisation.
+ * UINT64_MAX.  `stream` is used as given (NULL = the HIP null stream, not the
+ * context's stream), so the caller's collectives on that stream are ordered
+ * after the scan.  No host synchronisation.
+ * The context's device workspaces (query images, partial keys, rendezvous
+ * tickets) are shared by every call on it: all calls on one context must be
+ * serialised on ONE stream (the context's own calls use its internal stream and
+ * synchronise before returning, so mixing them with this call is safe only after
+ * the caller has synchronised `stream`).
  */
 int pf_scan_keys_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq,
                        int32_t topk, uint64_t* d_keys, void* stream);
@@ -224,6 +231,16 @@ typedef struct pf_layout_stats {
 } pf_layout_stats;
 int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
 
+/* Bytes the all-candidates scan kernel reads from device memory for each query
+ * over this context's shard, by the kernel's access pattern (the physical byte
+ * model of DESIGN.md section 4): K5 = per candidate block, the 32-B headers, two
+ * cell words per query list and every entry of each list's cell range (4 B;
+ * token entries also their 8-B norm), the exclusion list, and the staged query
+ * image per workgroup; K1 = the shard's record stream and headers.  0 for an
+ * unknown uid.  (A query alone in its launch is assumed; in a batch each
+ * workgroup stages its query's image once per block.) */
+int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* out_bytes);
+
 /* Device time (ms) of the last all-candidates scan kernel (HIP events on the
  * stream it was launched on). */
 float pf_last_scan_ms(const pf_ctx* ctx);
@@ -232,7 +249,9 @@ float pf_last_scan_ms(const pf_ctx* ctx);
 int pf_profile_reset(pf_ctx* ctx);
 int pf_profile_read(pf_ctx* ctx, double* total_ms, int64_t* launches);
 /* Time only scan launches 0, every, 2*every, ... after a reset (default 1 = all); the
- * others run without timing events.  *launches in pf_profile_read counts timed launches. */
+ * others run without timing events.  *launches in pf_profile_read counts timed launches.
+ * every = 0 turns profiling off (until the next pf_profile_reset).  At most 65536 launches
+ * are timed per reset; later ones run untimed. */
 int pf_profile_sample(pf_ctx* ctx, int32_t every);
 
 #ifdef __cplusplus

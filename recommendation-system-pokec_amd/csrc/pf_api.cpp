@@ -25,6 +25,8 @@ namespace {
 thread_local std::string g_open_error;
 
 constexpr uint32_t kLdsLimit = 64 * 1024;  // query images above this probe from global memory
+constexpr uint32_t kK5LdsCap = 160u * 1024u;  // one K5 workgroup's LDS (gfx950: 160 KB per CU)
+constexpr size_t kProfCap = 1u << 16;      // profiling event pairs kept (pf_profile_*)
 
 struct DBuf {
     void* p = nullptr;
@@ -433,20 +435,30 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
     oc[i] = n;
 }
 
-// All-candidates scan for `idx` (valid query indices) into d_keys rows `rows`.
-// One pinned staging buffer [refs | rows | image pool] goes up in a single async copy.
-// Timing events of one scan launch (the profiling pool when pf_profile_reset is on)
+// Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
+// launch the caller passes timed = false, or that sampling skips, records nothing and clears
+// last_ev0/last_ev1, so pf_last_scan_ms never reports another launch's time.
 int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
     e0 = c->ev0;
     e1 = c->ev1;
+    if (!timed) {
+        c->last_ev0 = c->last_ev1 = nullptr;
+        return PF_OK;
+    }
     if (c->prof_on) {
         // a timed launch costs ~9 us of stream time (two timestamped events, measured at
         // 231 vs 222 us per single-query step): sampled launches only when asked
         if (c->prof_seen++ % c->prof_every != 0) {
             timed = false;
+            c->last_ev0 = c->last_ev1 = nullptr;
             return PF_OK;
         }
         if (c->prof_used == c->prof_ev.size()) {
+            if (c->prof_ev.size() >= kProfCap) {  // pool full: the launch runs untimed
+                timed = false;
+                c->last_ev0 = c->last_ev1 = nullptr;
+                return PF_OK;
+            }
             hipEvent_t a, b;
             HIPCHK(c, hipEventCreate(&a));
             HIPCHK(c, hipEventCreate(&b));
@@ -455,37 +467,27 @@ int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
         e0 = c->prof_ev[c->prof_used].first;
         e1 = c->prof_ev[c->prof_used].second;
         ++c->prof_used;
-        timed = true;
     }
     return PF_OK;
 }
 
-// K5: the postings scan.  Staging: [image offsets | rows | sync | images].
-int scan_post(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
-              hipStream_t s, bool timed) {
-    const int nq = (int)idx.size();
-    std::vector<uint8_t> pool;
+// K5: the postings scan of prebuilt images (pf_types.h QPostHead layout) into d_keys rows
+// `rows`.  Staging: [image offsets | rows | sync | images], one async copy.
+int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, const std::vector<int32_t>& rows, int k,
+              uint64_t* d_keys, hipStream_t s, bool timed) {
+    const int nq = (int)imgs.size();
+    if (nq == 0) return PF_OK;
     std::vector<uint32_t> offs;
     int max_lists = 0, max_tok = 0;
-    // the query images (host, ~35 us each) on threads for a batch
-    std::vector<std::vector<uint8_t>> imgs(idx.size());
-    par_jobs(idx.size(), [&](size_t q) {
-        const int32_t i = idx[q], u = c->hc.uid[i];
-        std::vector<int32_t> ex;
-        auto it = c->hc.adj.find(u);
-        if (it != c->hc.adj.end()) ex = it->second;
-        ex.push_back(u);
-        pf::build_query_post(c->hc, c->hp, i, ex, imgs[q]);
-    });
-    for (const auto& im : imgs) {
-        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(im.data() + sizeof(pf::QConst));
+    size_t pool_b = 0;
+    for (const auto* im : imgs) {
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(im->data() + sizeof(pf::QConst));
         max_lists = std::max(max_lists, h->n_tok + h->n_club + h->n_friend);
         max_tok = std::max(max_tok, h->n_tok);
-        offs.push_back((uint32_t)pool.size());
-        pool.insert(pool.end(), im.begin(), im.end());
+        offs.push_back((uint32_t)pool_b);
+        pool_b += im->size();
     }
     const uint32_t wave_lds = pf::post_var_lds(max_tok, max_lists);
-    if (pf::post_lds(wave_lds) > 160u * 1024u) return c->fail(PF_EUNSUPP, "query names too many lists for one workgroup's LDS");
     const int nwb = c->wb_end - c->wb_begin;
     const int per_cu = pf::post_blocks_per_cu(wave_lds);
     // One query: one resident round of workgroups loops over the blocks.  A batch: one block
@@ -497,13 +499,13 @@ int scan_post(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int3
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
-    const size_t total = offs_b + rows_b + sync_b + pool.size();
+    const size_t total = offs_b + rows_b + sync_b + pool_b;
     uint8_t* h = c->stage_acquire(total);
     if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
     std::memcpy(h, offs.data(), (size_t)nq * 4);
     std::memcpy(h + offs_b, rows.data(), (size_t)nq * 4);
     std::memset(h + offs_b + rows_b, 0, sync_b);
-    std::memcpy(h + offs_b + rows_b + sync_b, pool.data(), pool.size());
+    for (int q = 0; q < nq; ++q) std::memcpy(h + offs_b + rows_b + sync_b + offs[q], imgs[q]->data(), imgs[q]->size());
     HIPCHK(c, c->d_pool.ensure(total));
     HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
     HIPCHK(c, c->stage_release(s));
@@ -525,10 +527,11 @@ int scan_post(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int3
     return PF_OK;
 }
 
-int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
-             hipStream_t s, bool timed) {
+// K1: the record-stream scan for `idx` (valid query indices) into d_keys rows `rows`.
+// One pinned staging buffer [refs | rows | sync | image pool] goes up in a single async copy.
+int scan_stream(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
+                hipStream_t s, bool timed) {
     if (idx.empty()) return PF_OK;
-    if (c->use_post()) return scan_post(c, idx, rows, k, d_keys, s, timed);
     Images im;
     pf::QImageHost qi;
     std::vector<int32_t> excl;
@@ -578,6 +581,67 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         c->last_ev1 = e1;
     }
     return PF_OK;
+}
+
+// All-candidates scan for `idx` (valid query indices) into d_keys rows `rows`.  The postings
+// scan (K5) serves every query whose lists fit one workgroup's LDS; a query naming more lists
+// (a user with ~15k friends or thousands of tokens) goes to the record-stream scan (K1) in a
+// launch of its own, so one heavy user never fails the batch.
+int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32_t>& rows, int k, uint64_t* d_keys,
+             hipStream_t s, bool timed) {
+    if (idx.empty()) return PF_OK;
+    if (!c->use_post()) return scan_stream(c, idx, rows, k, d_keys, s, timed);
+    // the query images (host, ~35 us each) on threads for a batch
+    std::vector<std::vector<uint8_t>> imgs(idx.size());
+    std::vector<uint8_t> fits(idx.size(), 1);
+    par_jobs(idx.size(), [&](size_t q) {
+        const int32_t i = idx[q], u = c->hc.uid[i];
+        std::vector<int32_t> ex;
+        auto it = c->hc.adj.find(u);
+        if (it != c->hc.adj.end()) ex = it->second;
+        ex.push_back(u);
+        pf::build_query_post(c->hc, c->hp, i, ex, imgs[q]);
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[q].data() + sizeof(pf::QConst));
+        fits[q] = pf::post_lds(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend)) <= kK5LdsCap;
+    });
+    std::vector<const std::vector<uint8_t>*> pi;
+    std::vector<int32_t> prow, sidx, srow;
+    for (size_t q = 0; q < idx.size(); ++q) {
+        if (fits[q]) { pi.push_back(&imgs[q]); prow.push_back(rows[q]); }
+        else { sidx.push_back(idx[q]); srow.push_back(rows[q]); }
+    }
+    int rc = scan_post(c, pi, prow, k, d_keys, s, timed);
+    if (rc != PF_OK) return rc;
+    return scan_stream(c, sidx, srow, k, d_keys, s, timed && pi.empty());
+}
+
+// Bytes the postings scan (K5) reads for one query image over this context's blocks, by the
+// kernel's own access pattern (fas_post_kernel): per block, 32 B of header per candidate, two
+// cell words per list, and every entry of the list's cell-rounded range (4 B; token entries
+// also their 8-B norm); per block the exclusion list (whole when <= 256 entries); per
+// workgroup the staged image.
+int64_t post_query_bytes(const pf_ctx* c, const std::vector<uint8_t>& img, int wgs) {
+    const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(img.data() + sizeof(pf::QConst));
+    const pf::QTok* toks = reinterpret_cast<const pf::QTok*>(img.data() + h->tok_off);
+    const pf::PList* sets = reinterpret_cast<const pf::PList*>(img.data() + h->set_off);
+    const uint32_t B = (uint32_t)c->ps.bsize, n = (uint32_t)c->ps.n;
+    const uint32_t* cells = c->hp.cells.data();
+    int64_t bytes = 0;
+    auto list_bytes = [&](const pf::PList& L, int per) {
+        for (int32_t blk = c->wb_begin; blk < c->wb_end; ++blk) {
+            const uint32_t c0 = (uint32_t)blk * B, c1 = std::min(c0 + B, n) - 1;
+            const uint32_t lo = cells[L.cell_off + (c0 >> L.shift)], hi = cells[L.cell_off + (c1 >> L.shift) + 1];
+            bytes += (int64_t)(hi - lo) * per + 8;
+        }
+    };
+    for (int j = 0; j < h->n_tok; ++j) list_bytes(toks[j].l, 12);
+    for (int j = 0; j < h->n_club + h->n_friend; ++j) list_bytes(sets[j], 4);
+    const int64_t nb = c->wb_end - c->wb_begin;
+    const int64_t cands = std::max<int64_t>(0, std::min<int64_t>((int64_t)c->wb_end * B, n) - (int64_t)c->wb_begin * B);
+    bytes += cands * 32;
+    bytes += nb * 4 * (int64_t)std::min(h->n_excl, (int32_t)pf::kPostThreads);
+    bytes += (int64_t)std::min<int64_t>(nb, wgs) * (int64_t)img.size();
+    return bytes;
 }
 
 int emit_jobs(pf_ctx* c, std::vector<pf::Job>& jobs, int topk, int32_t* ou, float* os, int32_t* oc) {
@@ -959,7 +1023,7 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         std::vector<uint4>().swap(hp.hdr);
         std::vector<uint32_t>().swap(hp.post);
         std::vector<double>().swap(hp.pnorm);
-        std::vector<uint32_t>().swap(hp.cells);
+        // hp.cells stays on the host too: pf_scan_bytes reads the lists' cell ranges
         c->ps.hdr = c->d_phdr.as<uint4>();
         c->ps.post = c->d_post.as<uint32_t>();
         c->ps.pnorm = c->d_pnorm.as<double>();
@@ -1135,10 +1199,31 @@ int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {
     };
     c->tile_begin = bound(shard);
     c->tile_end = bound(shard + 1);
-    // postings scan: contiguous block ranges of equal candidate count
+    // postings scan: contiguous block ranges of equal posting weight.  A block's cost is a
+    // fixed part (headers, ranges, top-k: ~60 of ~210 us at cfg 2) plus
+    // its share of the lists a query names, i.e. of the postings entries (tokens, clubs,
+    // friends) its candidates hold: weight = kBlockFixedWords * candidates + entries.
     const int64_t nwb = c->ps.n_blocks;
-    c->wb_begin = (int32_t)(nwb * shard / nshards);
-    c->wb_end = (int32_t)(nwb * (shard + 1) / nshards);
+    if (nwb > 0) {
+        const auto& hc = c->hc;
+        const int64_t bs = c->ps.bsize;
+        constexpr int64_t kBlockFixedWords = 64;
+        std::vector<uint64_t> wpre(nwb + 1, 0);
+        for (int64_t b = 0; b < nwb; ++b) {
+            const int64_t i0 = b * bs, i1 = std::min<int64_t>(hc.n, i0 + bs);
+            const int64_t ent = (hc.tok_off[(size_t)i1 * hc.T] - hc.tok_off[(size_t)i0 * hc.T]) +
+                                (hc.club_off[i1] - hc.club_off[i0]) + (hc.friend_off[i1] - hc.friend_off[i0]);
+            wpre[b + 1] = wpre[b] + (uint64_t)(kBlockFixedWords * (i1 - i0) + ent);
+        }
+        auto wbound = [&](int s) -> int32_t {
+            if (s <= 0) return 0;
+            if (s >= nshards) return (int32_t)nwb;
+            const uint64_t target = wpre[nwb] * (uint64_t)s / (uint64_t)nshards;
+            return (int32_t)(std::lower_bound(wpre.begin(), wpre.end(), target) - wpre.begin());
+        };
+        c->wb_begin = wbound(shard);
+        c->wb_end = wbound(shard + 1);
+    }
     return PF_OK;
 }
 
@@ -1169,6 +1254,34 @@ int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int3
     (void)hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(c, pf::launch_merge(d_parts, nparts, (int64_t)nq * topk, topk, nq, topk, d_out, s));
+    return PF_OK;
+}
+
+int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
+    if (!c || nq < 0 || (nq && (!q || !out))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (!c->use_post()) {  // K1: one pass over the shard's tiles and headers, whatever the query
+        const int64_t tiles = c->tile_end - c->tile_begin;
+        int64_t sb = 0;
+        for (int32_t t = c->tile_begin; t < c->tile_end; ++t) sb += (int64_t)c->hs.tile_steps[t] * pf::kTileSlots * 16;
+        const int64_t hdr = tiles * pf::kTileSlots * 48;
+        for (int i = 0; i < nq; ++i) out[i] = c->hc.idx_of(q[i]) < 0 ? 0 : sb + hdr;
+        return PF_OK;
+    }
+    par_jobs((size_t)nq, [&](size_t i) {
+        const int32_t x = c->hc.idx_of(q[i]);
+        if (x < 0) { out[i] = 0; return; }
+        std::vector<int32_t> ex;
+        auto it = c->hc.adj.find(q[i]);
+        if (it != c->hc.adj.end()) ex = it->second;
+        ex.push_back(q[i]);
+        std::vector<uint8_t> img;
+        pf::build_query_post(c->hc, c->hp, x, ex, img);
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(img.data() + sizeof(pf::QConst));
+        const uint32_t wl = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
+        const int wgs = nq == 1 ? c->num_cus * pf::post_blocks_per_cu(wl) : 1;
+        out[i] = post_query_bytes(c, img, wgs);
+    }, 1);
     return PF_OK;
 }
 
@@ -1210,11 +1323,18 @@ int pf_profile_reset(pf_ctx* c) {
     c->prof_on = true;
     c->prof_used = 0;
     c->prof_seen = 0;
+    c->last_ev0 = c->last_ev1 = nullptr;  // pool events are re-recorded from here on
     return PF_OK;
 }
 
 int pf_profile_sample(pf_ctx* c, int32_t every) {
-    if (!c || every < 1) return PF_EINVAL;
+    if (!c || every < 0) return PF_EINVAL;
+    if (every == 0) {  // profiling off: launches use the context's own event pair again
+        c->prof_on = false;
+        c->prof_used = 0;
+        c->last_ev0 = c->last_ev1 = nullptr;
+        return PF_OK;
+    }
     c->prof_every = every;
     return PF_OK;
 }

@@ -26,7 +26,8 @@ MAX_TOPK_DEVICE = 64
 EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_users", "pf_idf", "pf_fas_pairs",
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
-           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel"]
+           "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel",
+           "pf_scan_bytes"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -90,6 +91,7 @@ def lib():
         L.pf_profile_reset.argtypes = [V]
         L.pf_profile_sample.argtypes = [V, I32]
         L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
+        L.pf_scan_bytes.argtypes = [V, V, I32, V]
         L.pf_dataset_load.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(V)]
         L.pf_dataset_load_cached.argtypes = [ctypes.c_char_p, I64, ctypes.c_char_p, ctypes.POINTER(I32), ctypes.POINTER(V)]
         L.pf_dataset_free.argtypes = [V]
@@ -245,6 +247,13 @@ class FasEngine:
         ms, n = ctypes.c_double(), ctypes.c_int64()
         self._check(self._L.pf_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)), "pf_profile_read")
         return ms.value, n.value
+
+    def scan_bytes(self, uids):
+        """Bytes the all-candidates scan kernel reads per query over this shard (pf_scan_bytes)."""
+        q = np.ascontiguousarray(np.atleast_1d(uids), np.int32)
+        out = np.zeros(len(q), np.int64)
+        self._check(self._L.pf_scan_bytes(self.h, q.ctypes.data, len(q), out.ctypes.data), "pf_scan_bytes")
+        return out
 
 
 def decode_keys(keys):

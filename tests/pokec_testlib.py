@@ -91,6 +91,56 @@ class Corpus:
         return {int(u): i for i, u in enumerate(self.uid)}
 
 
+def corpus_from_desc(ptr):
+    """numpy Corpus copied out of a pf_corpus_desc (e.g. a synth corpus), so tests can edit it."""
+    d = PfCorpusDesc.from_address(ptr)
+    n, T = d.n_users, d.n_cols
+
+    def arr(p, ct, count):
+        if count == 0:
+            return np.zeros(0, np.dtype(ct))
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ct)), shape=(count,)).copy()
+    i32, i64, u32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
+    club_off = arr(d.club_off, i64, n + 1)
+    friend_off = arr(d.friend_off, i64, n + 1)
+    tok_off = arr(d.tok_off, i64, n * T + 1)
+    adj_off = arr(d.adj_off, i64, d.n_adj + 1)
+    K = NUM_FIXED + T
+    return Corpus(arr(d.user_id, i32, n), arr(d.public_flag, i32, n), arr(d.completion, i32, n),
+                  arr(d.gender, i32, n), arr(d.age, i32, n), arr(d.region, i32, 3 * n),
+                  club_off, arr(d.club_ids, u32, int(club_off[-1])), friend_off,
+                  arr(d.friend_ids, u32, int(friend_off[-1])), tok_off, arr(d.tok_tid, i32, int(tok_off[-1])),
+                  arr(d.tok_tf, i32, int(tok_off[-1])), arr(d.adj_uid, i32, d.n_adj), adj_off,
+                  arr(d.adj_nbr, i32, int(adj_off[-1])), T, arr(d.norm_present, ctypes.c_uint8, K),
+                  arr(d.norm_mean, ctypes.c_float, K), arr(d.norm_sd, ctypes.c_float, K))
+
+
+def with_rows(c, user=None, friends=None, adj=None):
+    """Copy of numpy Corpus c with uid `user`'s profile friends column and/or adj_list row replaced
+    (adj maps uid -> new row; a uid absent from adj_list gets a new row)."""
+    n = c.n_users
+    fo, fr = c.friend_off, c.friends
+    if user is not None and friends is not None:
+        i = int(np.nonzero(c.uid == user)[0][0])
+        rows = [fr[fo[j]:fo[j + 1]] for j in range(n)]
+        rows[i] = np.asarray(friends, np.uint32)
+        fo = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+        fr = np.concatenate(rows).astype(np.uint32)
+    au, ao, an = c.adj_uid, c.adj_off, c.adj_nbr
+    if adj:
+        rows = {int(u): an[ao[j]:ao[j + 1]] for j, u in enumerate(au)}
+        order = [int(u) for u in au]
+        for u, r in adj.items():
+            if u not in rows:
+                order.append(u)
+            rows[u] = np.asarray(r, np.int32)
+        au = np.array(order, np.int32)
+        ao = np.concatenate([[0], np.cumsum([len(rows[u]) for u in order])]).astype(np.int64)
+        an = np.concatenate([rows[u] for u in order]).astype(np.int32)
+    return Corpus(c.uid, c.pub, c.comp, c.gen, c.age, c.region, c.club_off, c.clubs, fo, fr, c.tok_off, c.tok_tid,
+                  c.tok_tf, au, ao, an, c.n_cols, c.norm_present, c.norm_mean, c.norm_sd, c.median, c.col_names)
+
+
 # ------------------------------------------------------------- reference formats
 def _atoi(s):
     """C atoi: optional whitespace, sign, digits; stops at the first non-digit."""

@@ -148,6 +148,31 @@ def test_postings_scan_every_user_small_corpus():
         assert np.array_equal(p[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
+@pytest.fixture(scope="module")
+def hub():
+    """The 20k-user edge-case corpus with one heavy user: uid 4242's profile names 22,000
+    friends (every user plus 2,000 unknown ids), so its postings query needs ~20k friend lists,
+    beyond one K5 workgroup's LDS; its adj_list row stays small, so little is excluded."""
+    base = tl.synth.Corpus(n_users=20000, seed=77, edge_cases=1)
+    c = tl.corpus_from_desc(base.desc_ptr())
+    c = tl.with_rows(c, user=4242, friends=np.arange(1, 22001, dtype=np.uint32))
+    return c, tl.engine(c), tl.Oracle(c)
+
+
+def test_heavy_query_routes_to_stream_scan(hub):
+    """a query whose lists exceed K5's LDS is scored by K1 in its own launch, in the
+    same call as ordinary queries (which stay on K5), and matches the oracle bit for bit."""
+    c, eng, orc = hub
+    q = [4242, 3, 15000, 4242, 777]
+    assert eng.layout().scan_kernel == 2
+    got = eng.recommend_interest_all(q, 10)
+    ref = orc.interest(q, 10, tl.PF_MODE_ALL, 0)
+    for u, g, r in zip(q, got, ref):
+        assert len(g[0]) == 10, u
+        assert list(g[0]) == list(r[0]), u
+        assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
 def test_big_pairs_vs_oracle(big):
     c, eng, orc = big
     rng = np.random.default_rng(9)

@@ -16,9 +16,16 @@
 #include <vector>
 
 #include "pf_batch.h"
+#include "pf_ctx.h"
 #include "pf_kernels.h"
 #include "pf_store.h"
 #include "pokec_fas.h"
+
+using pf::DBuf;
+using pf::PinBuf;
+using pf::Ranked;
+using pf::par_jobs;
+using pf::rank;
 
 namespace {
 
@@ -28,169 +35,13 @@ constexpr uint32_t kLdsLimit = 64 * 1024;  // query images above this probe from
 constexpr uint32_t kK5LdsCap = 160u * 1024u;  // one K5 workgroup's LDS (gfx950: 160 KB per CU)
 constexpr size_t kProfCap = 1u << 16;      // profiling event pairs kept (pf_profile_*)
 
-struct DBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(bytes, 4096);
-        want = want + want / 4;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    ~DBuf() {
-        if (p) (void)hipFree(p);
-    }
-    template <class T>
-    T* as() const { return reinterpret_cast<T*>(p); }
-};
-
-// Pinned host buffer that only grows (contents are not initialised)
-struct PinBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        const size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    ~PinBuf() {
-        if (p) (void)hipHostFree(p);
-    }
-    template <class T>
-    T* as() const { return reinterpret_cast<T*>(p); }
-};
-
-using Ranked = std::vector<std::pair<int32_t, float>>;
-
-void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
-    std::sort(v.begin(), v.end(), [](const std::pair<int32_t, float>& a, const std::pair<int32_t, float>& b) {
-        return a.second == b.second ? a.first < b.first : a.second > b.second;
-    });
-    if ((int)v.size() > topk) v.resize(std::max(topk, 0));
-}
-
 }  // namespace
 
 namespace pf {
 void set_open_error(const std::string& m) { g_open_error = m; }
 }  // namespace pf
 
-struct pf_ctx {
-    int device = 0;
-    int num_cus = 256;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, last_ev0 = nullptr, last_ev1 = nullptr;
-    float last_scan_ms = 0.f;
-    std::string err;
-    pf::HostCorpus hc;
-    pf::HostStore hs;       // metadata only after upload (stream freed)
-    int64_t stream_bytes = 0, norm_bytes = 0;
-    DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
-    pf::DevStore ds{};
-    // workspaces
-    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
-    PinBuf h_pool, h_slots, h_scores;  // pair batches: images, candidate slots, scores
-    DBuf d_pairs1;                     // run_jobs stage-1 scores (the collaborative matrices)
-    int32_t tile_begin = 0, tile_end = 0;
-    // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
-    pf::HostPost hp;
-    DBuf d_phdr, d_post, d_pnorm, d_cells;
-    pf::PostStore ps{};
-    int64_t post_bytes = 0;
-    int32_t wb_begin = 0, wb_end = 0;
-    int32_t scan_kind = PF_SCAN_AUTO;
-    bool use_post() const { return hp.ok && scan_kind != PF_SCAN_STREAM; }
-    // pinned staging ring for the per-call query upload (a slot is reused only after
-    // the copy that read it has completed)
-    struct Stage {
-        uint8_t* p = nullptr;
-        size_t cap = 0;
-        hipEvent_t done = nullptr;
-    };
-    Stage stage[4];
-    int stage_cur = 0;
-    uint8_t* stage_acquire(size_t bytes) {
-        Stage& st = stage[stage_cur];
-        if (st.done) (void)hipEventSynchronize(st.done);
-        if (st.cap < bytes) {
-            if (st.p) (void)hipHostFree(st.p);
-            st.p = nullptr;
-            st.cap = 0;
-            size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 16);
-            if (hipHostMalloc((void**)&st.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-            st.cap = want;
-        }
-        return st.p;
-    }
-    hipError_t stage_release(hipStream_t s) {
-        Stage& st = stage[stage_cur];
-        stage_cur = (stage_cur + 1) % 4;
-        if (!st.done) {
-            hipError_t e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
-        return hipEventRecord(st.done, s);
-    }
-    // scan-kernel timing pool (pf_profile_*)
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
-    size_t prof_used = 0;
-    bool prof_on = false;
-    int64_t prof_seen = 0;   // scan launches since the reset
-    int32_t prof_every = 1;  // time launches 0, every, 2 every, ... (pf_profile_sample)
-
-    int fail(int code, const std::string& m) {
-        err = m;
-        return code;
-    }
-    int hip_fail(hipError_t e, const char* what) {
-        err = std::string(what) + ": " + hipGetErrorString(e);
-        return PF_ENODEV;
-    }
-};
-
 namespace {
-
-// f(0 .. n-1) on up to 16 threads, `grain` items per thread at least (a thread costs tens of
-// microseconds: the single-user calls of the sequential drivers stay on the caller's thread)
-template <class F>
-void par_jobs(size_t n, F f, size_t grain = 4) {
-    const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / grain, std::thread::hardware_concurrency())));
-    if (th <= 1) {
-        for (size_t i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::vector<std::thread> ts;
-    for (size_t w = 0; w < th; ++w)
-        ts.emplace_back([&, w]() {
-            for (size_t i = w; i < n; i += th) f(i);
-        });
-    for (auto& t : ts) t.join();
-}
-
-
-#define HIPCHK(ctx, expr)                                   \
-    do {                                                    \
-        hipError_t _e = (expr);                             \
-        if (_e != hipSuccess) return (ctx)->hip_fail(_e, #expr); \
-    } while (0)
-
-template <class T>
-hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
-    hipError_t e = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
-    if (e != hipSuccess) return e;
-    if (v.empty()) return hipSuccess;
-    return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream);
-}
 
 // Query images -> one byte pool + refs.
 struct Images {
@@ -273,46 +124,6 @@ void fill_images(const Images& im, const std::vector<pf::QImageHost>& qs, uint8_
     }, 64);
 }
 
-// recommender_graph.cpp:10-31 (friends + FoFs, first-seen order, limit after every push)
-std::vector<int32_t> gather_graph(const pf::AdjView& V, int32_t u, int32_t limit) {
-    std::vector<int32_t> out;
-    const std::vector<int32_t>* ru = V.row(u);
-    if (!ru) return out;
-    std::unordered_set<int32_t> seen;
-    for (int32_t f : *ru) {
-        if (f == u) continue;
-        if (seen.insert(f).second) out.push_back(f);
-        if ((int32_t)out.size() >= limit) return out;
-        const std::vector<int32_t>* rf = V.row(f);
-        if (!rf) continue;
-        for (int32_t x : *rf) {
-            if (x == u || !seen.insert(x).second) continue;
-            out.push_back(x);
-            if ((int32_t)out.size() >= limit) return out;
-        }
-    }
-    return out;
-}
-
-// recommender_graph.cpp:114-125 (FoFs only; inner loop breaks at the limit)
-std::vector<int32_t> gather_collab(const pf::AdjView& V, int32_t u, int32_t limit) {
-    std::vector<int32_t> out;
-    const std::vector<int32_t>* ru = V.row(u);
-    if (!ru) return out;
-    std::unordered_set<int32_t> seen;
-    for (int32_t f : *ru) {
-        const std::vector<int32_t>* rf = V.row(f);
-        if (!rf) continue;  // skips the limit check too (recommender_graph.cpp:117-118)
-        for (int32_t x : *rf) {
-            if (x == u) continue;
-            if (seen.insert(x).second) out.push_back(x);
-            if ((int32_t)out.size() >= limit) break;
-        }
-        if ((int32_t)out.size() >= limit) break;
-    }
-    return out;
-}
-
 pf::AdjView plain_view(const pf_ctx* c) {
     pf::AdjView v;
     v.base = &c->hc.adj;
@@ -392,7 +203,8 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
             const int32_t img = img_of.at(qidx[g]);
             std::memcpy(flat + gf[i], slots[g].data(), slots[g].size() * sizeof(int32_t));
             for (size_t b = 0, x = gb[i]; b < slots[g].size(); b += 256, ++x)
-                blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(256, slots[g].size() - b), 0};
+                blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(256, slots[g].size() - b),
+                                           (int32_t)(gf[i] + b)};
         }, 256);
         hl.lap(pf::kHpPack);
         // pinned buffers: async copies; they are reused only after this chunk's synchronize
@@ -676,242 +488,6 @@ HostProf& host_prof() {
     return h;
 }
 
-// Every job's FAS pairs in two GPU stages (stage 2: the clubs recommender's friend-of-friend
-// pairs, which depend on stage 1's friend weights), the collaborative sums in one K4 launch,
-// then the reference's host arithmetic.  The per-job host work runs on threads.
-int run_jobs(pf_ctx* c, std::vector<Job>& jobs) {
-    const auto& hc = c->hc;
-    const auto& slot_of = c->hs.slot_of_idx;
-    struct St {
-        int32_t iq = -1;
-        int g0 = -1, g1 = -1;             // stage-1 groups
-        std::vector<std::pair<int32_t, std::vector<int32_t>>> groups;  // (query idx, candidate slots)
-        std::vector<int32_t> cuid;        // interest / collab: candidate uids of the scored pairs
-        std::vector<int32_t> friends;     // collab / clubs: the query's adjacency row
-        std::vector<int32_t> fidx, fuid;  // distinct friends with a profile
-        std::unordered_map<int32_t, int32_t> fpos;
-        std::vector<int32_t> grp;         // clubs: stage-2 group per friend
-        int64_t coff = -1;                // collab: offset of its sums
-    };
-    std::vector<St> st(jobs.size());
-    HpLap hl;
-    par_jobs(jobs.size(), [&](size_t i) {
-        Job& J = jobs[i];
-        St& S = st[i];
-        J.out.clear();
-        const int32_t u = J.uid;
-        if (J.topk <= 0) return;
-        if (J.kind == kJobInterest) {
-            S.iq = hc.idx_of(u);
-            if (S.iq < 0) return;  // recommender_graph.cpp:39-40
-            std::unordered_set<int32_t> skip;
-            if (const std::vector<int32_t>* r = J.view.row(u)) skip.insert(r->begin(), r->end());
-            skip.insert(u);
-            std::vector<int32_t> sl;
-            if (J.all_candidates) {
-                for (int32_t j = 0; j < hc.n; ++j)
-                    if (!skip.count(hc.uid[j])) { sl.push_back(slot_of[j]); S.cuid.push_back(hc.uid[j]); }
-            } else {
-                for (int32_t x : gather_graph(J.view, u, J.limit)) {
-                    if (skip.count(x)) continue;
-                    const int32_t ix = hc.idx_of(x);
-                    if (ix < 0) continue;
-                    sl.push_back(slot_of[ix]);
-                    S.cuid.push_back(x);
-                }
-            }
-            S.groups.emplace_back(S.iq, std::move(sl));
-        } else if (J.kind == kJobCollab) {
-            if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
-            std::vector<int32_t> cand = gather_collab(J.view, u, J.limit);
-            S.iq = hc.idx_of(u);
-            if (S.iq < 0) return;  // recommender_graph.cpp:130
-            for (int32_t f : S.friends) {  // distinct friends with a profile -> matrix rows
-                const int32_t ix = hc.idx_of(f);
-                if (ix < 0 || S.fpos.count(f)) continue;
-                S.fpos.emplace(f, (int32_t)S.fidx.size());
-                S.fidx.push_back(ix);
-            }
-            std::vector<int32_t> cs;
-            for (int32_t x : cand) {
-                if (x == u) continue;
-                const int32_t ix = hc.idx_of(x);
-                if (ix < 0) continue;
-                cs.push_back(slot_of[ix]);
-                S.cuid.push_back(x);
-            }
-            // sim_u_f (float, recommender_graph.cpp:132-136), then M[f][c]
-            std::vector<int32_t> fs;
-            for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
-            S.groups.emplace_back(S.iq, std::move(fs));
-            for (int32_t ix : S.fidx) S.groups.emplace_back(ix, cs);
-        } else {
-            S.iq = hc.idx_of(u);
-            if (S.iq < 0) return;  // recommender_clubs.cpp:13-16
-            if (const std::vector<int32_t>* r = J.view.row(u)) S.friends = *r;
-            for (int32_t f : S.friends) {  // pass 1: w_f = FAS(q, f) for distinct friends with a profile
-                const int32_t ix = hc.idx_of(f);
-                if (ix < 0 || S.fpos.count(f)) continue;
-                S.fpos.emplace(f, (int32_t)S.fidx.size());
-                S.fidx.push_back(ix);
-                S.fuid.push_back(f);
-            }
-            std::vector<int32_t> fs;
-            for (int32_t ix : S.fidx) fs.push_back(slot_of[ix]);
-            S.groups.emplace_back(S.iq, std::move(fs));
-        }
-    });
-    std::vector<int32_t> qidx;
-    std::vector<std::vector<int32_t>> slots;
-    for (St& S : st) {
-        if (S.groups.empty()) continue;
-        S.g0 = (int)qidx.size();
-        S.g1 = S.g0 + 1;
-        for (auto& g : S.groups) {
-            qidx.push_back(g.first);
-            slots.push_back(std::move(g.second));
-        }
-        S.groups.clear();
-    }
-    std::vector<std::vector<float>> res;
-    hl.lap(kHpPrep);
-    std::vector<int64_t> goff;  // stage-1 scores stay on the device for K4
-    int rc = run_pairs(c, qidx, slots, res, &c->d_pairs1, &goff);
-    if (rc != PF_OK) return rc;
-    hl.skip();
-    // stage 2: FAS(f, fof) for every fof of every positive-weight friend (clubs)
-    par_jobs(jobs.size(), [&](size_t i) {
-        Job& J = jobs[i];
-        St& S = st[i];
-        if (J.kind != kJobClubs || S.iq < 0 || J.topk <= 0) return;
-        const std::vector<float>& w = res[S.g0];
-        S.grp.assign(S.fidx.size(), -1);
-        for (size_t r = 0; r < S.fidx.size(); ++r) {
-            if ((double)w[r] <= 0.0) continue;
-            const std::vector<int32_t>* rf = J.view.row(S.fuid[r]);
-            if (!rf) continue;
-            std::vector<int32_t> sl;
-            for (int32_t x : *rf) {
-                if (x == J.uid) continue;
-                const int32_t ix = hc.idx_of(x);
-                if (ix < 0) continue;
-                sl.push_back(slot_of[ix]);
-            }
-            S.grp[r] = (int32_t)S.groups.size();
-            S.groups.emplace_back(S.fidx[r], std::move(sl));
-        }
-    });
-    std::vector<int32_t> qidx2;
-    std::vector<std::vector<int32_t>> slots2;
-    std::vector<int32_t> gbase(jobs.size(), 0);
-    for (size_t i = 0; i < jobs.size(); ++i) {
-        gbase[i] = (int32_t)qidx2.size();
-        for (auto& g : st[i].groups) {
-            qidx2.push_back(g.first);
-            slots2.push_back(std::move(g.second));
-        }
-        st[i].groups.clear();
-    }
-    std::vector<std::vector<float>> res2;
-    hl.lap(kHpStage2);
-    rc = run_pairs(c, qidx2, slots2, res2);
-    if (rc != PF_OK) return rc;
-    hl.skip();
-    // collaborative sums (K4): every collab job of the batch in one launch
-    {
-        std::vector<CollabSum> cj;
-        std::vector<float> w;
-        std::vector<int32_t> wrow;
-        int64_t ctot = 0;
-        int max_nc = 0;
-        for (size_t i = 0; i < jobs.size(); ++i) {
-            St& S = st[i];
-            if (jobs[i].kind != kJobCollab || S.iq < 0 || jobs[i].topk <= 0 || S.cuid.empty()) continue;
-            const int F = (int)S.friends.size(), nc = (int)S.cuid.size();
-            // the matrix rows M[f][c] are stage-1 groups g1 .. g1 + |fidx| - 1, consecutive on the device
-            CollabSum js{S.fidx.empty() ? 0 : goff[S.g1], ctot, (int32_t)w.size(), F, nc, 0};
-            for (int j = 0; j < F; ++j) {
-                auto rt = S.fpos.find(S.friends[j]);
-                wrow.push_back(rt == S.fpos.end() ? -1 : rt->second);
-                w.push_back(rt == S.fpos.end() ? 0.f : res[S.g0][rt->second]);
-            }
-            S.coff = ctot;
-            ctot += nc;
-            max_nc = std::max(max_nc, nc);
-            cj.push_back(js);
-        }
-        std::vector<float> sums((size_t)ctot);
-        if (!cj.empty()) {
-            HIPCHK(c, upload(c, c->d_w, w));
-            HIPCHK(c, upload(c, c->d_wrow, wrow));
-            HIPCHK(c, upload(c, c->d_cjobs, cj));
-            HIPCHK(c, c->d_csum.ensure((size_t)ctot * sizeof(float)));
-            for (size_t b = 0; b < cj.size(); b += 65535)
-                HIPCHK(c, launch_collab_sum(c->d_pairs1.as<float>(), c->d_w.as<float>(), c->d_wrow.as<int32_t>(),
-                                            c->d_cjobs.as<CollabSum>() + b, (int)std::min<size_t>(65535, cj.size() - b),
-                                            max_nc, c->d_csum.as<float>(), c->stream));
-            HIPCHK(c, hipMemcpyAsync(sums.data(), c->d_csum.p, sums.size() * sizeof(float), hipMemcpyDeviceToHost,
-                                     c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-        }
-        hl.lap(kHpCollab);
-        par_jobs(jobs.size(), [&](size_t i) {
-            Job& J = jobs[i];
-            St& S = st[i];
-            if (J.topk <= 0 || S.iq < 0) return;
-            Ranked r;
-            if (J.kind == kJobInterest) {
-                const std::vector<float>& sc = res[S.g0];
-                r.reserve(sc.size());
-                for (size_t j = 0; j < sc.size(); ++j) r.emplace_back(S.cuid[j], sc[j]);
-            } else if (J.kind == kJobCollab) {
-                if (S.coff < 0) return;
-                for (size_t j = 0; j < S.cuid.size(); ++j) r.emplace_back(S.cuid[j], sums[S.coff + j]);
-            } else {
-                // club accumulation in the reference's exact loop order (double sums)
-                const std::vector<float>& wv = res[S.g0];
-                std::unordered_set<int32_t> own;
-                for (int64_t k = hc.club_off[S.iq]; k < hc.club_off[S.iq + 1]; ++k) own.insert((int32_t)hc.clubs[k]);
-                std::unordered_map<int32_t, double> score;
-                for (int32_t f : S.friends) {
-                    auto pt = S.fpos.find(f);
-                    if (pt == S.fpos.end()) continue;
-                    const double wf = wv[pt->second];
-                    if (wf <= 0.0) continue;
-                    const int32_t ix = S.fidx[pt->second];
-                    for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                        if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += wf;
-                }
-                for (int32_t f : S.friends) {
-                    auto pt = S.fpos.find(f);
-                    if (pt == S.fpos.end()) continue;
-                    const int32_t g = S.grp[pt->second];
-                    const double wf = wv[pt->second];
-                    if (wf <= 0.0 || g < 0) continue;
-                    const std::vector<float>& sf = res2[gbase[i] + g];
-                    const std::vector<int32_t>* rf = J.view.row(f);
-                    size_t j = 0;
-                    for (int32_t x : *rf) {
-                        if (x == J.uid) continue;
-                        const int32_t ix = hc.idx_of(x);
-                        if (ix < 0) continue;
-                        const double sv = sf[j++];
-                        if (sv <= 0.0) continue;
-                        const double addv = wf * sv;
-                        for (int64_t k = hc.club_off[ix]; k < hc.club_off[ix + 1]; ++k)
-                            if (!own.count((int32_t)hc.clubs[k])) score[(int32_t)hc.clubs[k]] += addv;
-                    }
-                }
-                for (auto& kv : score) r.emplace_back(kv.first, (float)kv.second);
-            }
-            rank(r, J.topk);
-            J.out = std::move(r);
-        });
-        hl.lap(kHpFinish);
-    }
-    return PF_OK;
-}
-
 }  // namespace pf
 
 extern "C" {
@@ -1041,6 +617,9 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         c->wb_begin = 0;
         c->wb_end = c->ps.n_blocks;
     }
+    rc = pf::jobs_open(c);  // device graph + image-builder tables (the recommenders' pipeline)
+    if (rc != PF_OK) return bail(rc);
+    stage("job pipeline (graph, image tables)");
     *out = c;
     return PF_OK;
 }
@@ -1171,8 +750,10 @@ int pf_recommend_clubs(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, in
 
 int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {
     if (!c || !n || (cap > 0 && !out)) return PF_EINVAL;
-    const pf::AdjView V = plain_view(c);
-    std::vector<int32_t> v = flavour == PF_FOF_COLLAB ? gather_collab(V, uid, limit) : gather_graph(V, uid, limit);
+    if (flavour != PF_FOF_GRAPH && flavour != PF_FOF_COLLAB) return PF_EINVAL;
+    std::vector<int32_t> v;  // K3 on the device (pf_jobs.hip gather_kernel)
+    const int rc = pf::fof_device(c, uid, limit, flavour, v);
+    if (rc != PF_OK) return rc;
     for (int32_t i = 0; i < (int32_t)v.size() && i < cap; ++i) out[i] = v[i];
     *n = (int32_t)v.size();
     return PF_OK;
@@ -1182,6 +763,7 @@ int pf_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
     if (!c || (n > 0 && !nbrs)) return PF_EINVAL;
     if (n < 0) c->hc.adj.erase(uid);
     else c->hc.adj[uid].assign(nbrs, nbrs + n);
+    pf::jobs_note_edit(c, uid);  // the device graph sees the edit at the next job batch
     return PF_OK;
 }
 

@@ -42,6 +42,7 @@ enum JobKind { kJobInterest = 0, kJobCollab = 1, kJobClubs = 2 };
 struct Job {
     int kind = kJobInterest;
     int32_t uid = 0, topk = 0, limit = 0;
+    int32_t limit_flavour = 0;  // pf_fof_candidates only: PF_FOF_GRAPH / PF_FOF_COLLAB
     bool all_candidates = false;
     AdjView view;
     std::vector<std::pair<int32_t, float>> out;  // ranked (id, score), <= topk
@@ -71,8 +72,8 @@ struct HpLap {
     void skip() { t = std::chrono::steady_clock::now(); }
 };
 
-// Runs every job; their FAS pairs go to the GPU together (one pair-kernel launch per stage
-// and chunk).  0 = OK, else a PF_* status.
+// Runs every job on the device job pipeline (pf_jobs_plan.cpp): one chain of device stages per
+// chunk of jobs.  0 = OK, else a PF_* status.
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs);
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c);
 

@@ -1,0 +1,218 @@
+// pf_ctx.h — the engine context behind the C ABI (pf_api.cpp) and the device job pipeline
+// (pf_jobs.cpp): device buffers, host corpus and stores, workspaces.  Engine-internal.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <utility>
+#include <vector>
+
+#include "pf_jobs.h"
+#include "pf_store.h"
+#include "pokec_fas.h"
+
+namespace pf {
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        want = want + want / 4;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Pinned host buffer that only grows (contents are not initialised)
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+using Ranked = std::vector<std::pair<int32_t, float>>;
+
+inline void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
+    std::sort(v.begin(), v.end(), [](const std::pair<int32_t, float>& a, const std::pair<int32_t, float>& b) {
+        return a.second == b.second ? a.first < b.first : a.second > b.second;
+    });
+    if ((int)v.size() > topk) v.resize(std::max(topk, 0));
+}
+
+
+// The device job pipeline's state (pf_jobs.cpp): the graph and image-builder inputs on the
+// device, their host mirrors, and the per-call workspaces.
+struct JobsState {
+    bool ok = false;
+    std::string why;
+    DevJobsStore js{};
+    DBuf d_tmpl, d_sigreg, d_comp_vals, d_comp_rows, d_age_vals, d_age_rows, d_idf_off, d_idf_tid, d_idf_val,
+        d_has_idf, d_slot_of, d_goff, d_glen, d_gnbr, d_guid, d_club_off, d_club_dense, d_club_id;
+    std::unordered_map<int32_t, int32_t> xnode;  // uid -> node for adj_list uids without a profile
+    std::vector<int32_t> g_uid, g_len;           // host mirrors (new uids from pf_set_adj append nodes)
+    bool nodes_dirty = false;
+    std::vector<uint8_t> img_lg;                 // per idx: query-table log2 (0 = outside the device limits)
+    std::vector<int32_t> img_nset;               // per idx: clubs + friends words of the record
+    std::unordered_set<int32_t> edited;          // uids whose adj_list row pf_set_adj changed
+    uint64_t edit_gen = 1, view_gen = 0;         // the uploaded edit table is current when equal
+    const void* view_over = nullptr;             // the batched drivers' versioned edits last uploaded
+    size_t view_over_n = 0;
+    DevView view{};
+    DBuf d_view_node, d_view_ver, d_view_off, d_view_len, d_view_nbr;
+    DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr, d_ncand, d_keys, d_acc, d_touched, d_fail;
+    PinBuf h_plan, h_out;
+    int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
+};
+
+}  // namespace pf
+
+using pf::DBuf;
+using pf::PinBuf;
+
+struct pf_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, last_ev0 = nullptr, last_ev1 = nullptr;
+    float last_scan_ms = 0.f;
+    std::string err;
+    pf::HostCorpus hc;
+    pf::HostStore hs;       // metadata only after upload (stream freed)
+    int64_t stream_bytes = 0, norm_bytes = 0;
+    DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
+    pf::DevStore ds{};
+    // workspaces
+    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
+    PinBuf h_pool, h_slots, h_scores;  // pair batches: images, candidate slots, scores
+    DBuf d_pairs1;                     // run_jobs stage-1 scores (the collaborative matrices)
+    int32_t tile_begin = 0, tile_end = 0;
+    // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
+    pf::HostPost hp;
+    DBuf d_phdr, d_post, d_pnorm, d_cells;
+    pf::PostStore ps{};
+    int64_t post_bytes = 0;
+    int32_t wb_begin = 0, wb_end = 0;
+    int32_t scan_kind = PF_SCAN_AUTO;
+    bool use_post() const { return hp.ok && scan_kind != PF_SCAN_STREAM; }
+    // pinned staging ring for the per-call query upload (a slot is reused only after
+    // the copy that read it has completed)
+    struct Stage {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    };
+    Stage stage[4];
+    int stage_cur = 0;
+    uint8_t* stage_acquire(size_t bytes) {
+        Stage& st = stage[stage_cur];
+        if (st.done) (void)hipEventSynchronize(st.done);
+        if (st.cap < bytes) {
+            if (st.p) (void)hipHostFree(st.p);
+            st.p = nullptr;
+            st.cap = 0;
+            size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 16);
+            if (hipHostMalloc((void**)&st.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+            st.cap = want;
+        }
+        return st.p;
+    }
+    hipError_t stage_release(hipStream_t s) {
+        Stage& st = stage[stage_cur];
+        stage_cur = (stage_cur + 1) % 4;
+        if (!st.done) {
+            hipError_t e = hipEventCreateWithFlags(&st.done, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(st.done, s);
+    }
+    // scan-kernel timing pool (pf_profile_*)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+    size_t prof_used = 0;
+    bool prof_on = false;
+    int64_t prof_seen = 0;   // scan launches since the reset
+    int32_t prof_every = 1;  // time launches 0, every, 2 every, ... (pf_profile_sample)
+
+    pf::JobsState jb;  // device job pipeline (pf_jobs.cpp)
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hip_fail(hipError_t e, const char* what) {
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return PF_ENODEV;
+    }
+};
+
+
+namespace pf {
+
+// f(0 .. n-1) on up to 16 threads, `grain` items per thread at least (a thread costs tens of
+// microseconds: the single-user calls of the sequential drivers stay on the caller's thread)
+template <class F>
+inline void par_jobs(size_t n, F f, size_t grain = 4) {
+    const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / grain, std::thread::hardware_concurrency())));
+    if (th <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (size_t w = 0; w < th; ++w)
+        ts.emplace_back([&, w]() {
+            for (size_t i = w; i < n; i += th) f(i);
+        });
+    for (auto& t : ts) t.join();
+}
+
+
+#define HIPCHK(ctx, expr)                                   \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return (ctx)->hip_fail(_e, #expr); \
+    } while (0)
+
+template <class T>
+inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
+    hipError_t e = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+    if (e != hipSuccess) return e;
+    if (v.empty()) return hipSuccess;
+    return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream);
+}
+
+
+// the device job pipeline (pf_jobs.cpp)
+int jobs_open(pf_ctx* c);                            // after the tile store is on the device
+void jobs_note_edit(pf_ctx* c, int32_t uid);         // pf_set_adj changed uid's row
+int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out);
+
+}  // namespace pf

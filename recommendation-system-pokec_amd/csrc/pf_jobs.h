@@ -1,0 +1,31 @@
+// pf_jobs.h — launchers of the device job pipeline (pf_jobs.hip) and its per-image plan.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pf_types.h"
+
+namespace pf {
+
+// One query image K6 builds (layout of pf_api.cpp plan_images): byte offsets into the image
+// pool; lg = table log2 (load <= 0.4), lge = exclusion table log2, dlg = log2 of the set
+// de-duplication table in scratch (u32 words from scr_off; the item list follows it).
+struct ImgJob {
+    int32_t idx, lg, lge, dlg;
+    uint32_t const_off, keys_off, vals_off, pad;
+    int64_t scr_off;
+};
+
+hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
+                         const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
+                         int32_t* ncand, hipStream_t s);
+hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n, uint8_t* pool,
+                          uint32_t* scratch, int32_t* fail, hipStream_t s);
+hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
+                         const float* pout, const int32_t* cand_slot, float* score, hipStream_t s);
+hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
+                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, int32_t* touched,
+                        float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);
+hipError_t launch_job_topk(const DevJob* jobs, const int32_t* jix, int njobs, const float* score, const int32_t* ids,
+                           const int32_t* slots, const int32_t* ncand, uint64_t* out, int k, hipStream_t s);
+
+}  // namespace pf

@@ -1,0 +1,659 @@
+// pf_jobs.hip — gfx950 kernels of the device job pipeline (pf_types.h DevJob): the reference's
+// graph / collaborative / clubs recommenders with the 2-hop work on the device.
+//
+//   gather_kernel   K3  per job: the ordered, de-duplicated, limit-truncated 2-hop candidate
+//                       list over the CSR adjacency (recommender_graph.cpp:10-31 / :114-125),
+//                       filtered like the recommender (no profile; row(u) + {u} for interest),
+//                       as tile-store slots for the pair kernel; clubs: each friend's row
+//   qimage_kernel   K6  per user: the query image the pair kernel stages (pf_store.cpp
+//                       build_query's layout): QConst from host-built tables + a 2-choice cuckoo
+//                       table of the user's distinct clubs, friends and (column, token) words
+//   collab_kernel   K4' score(c) = sum over row(u) positions of (double)FAS(u,f) * FAS(f,c)
+//                       (recommender_graph.cpp:167-180), in the reference's order
+//   clubs_kernel    K7  club scores in recommender_clubs.cpp:34-66's loop order (per club the
+//                       double sum is taken in exactly the reference's sequence)
+//   topk_kernel     K8  per job top-k of (score desc, id asc) (recommender_graph.cpp:97-101)
+//
+// Order-preserving de-duplication (K3): the sequence the reference walks (friend f, then f's
+// row, for each friend in order) is processed in 256-element chunks; each element claims its
+// node in a per-job open-addressing table and atomicMin's its position there, so after a
+// barrier an element is a first occurrence iff the table holds its own position (earlier
+// chunks hold smaller positions).  A block prefix sum over the first occurrences places them,
+// and the walk stops once `limit` have been found: exactly the reference's truncation.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "pf_device.h"
+#include "pf_jobs.h"
+
+namespace pf {
+
+constexpr int kJobThreads = 256;
+constexpr int kJobWaves = kJobThreads / 64;
+
+// ---------------------------------------------------------------- block helpers
+// exclusive rank of `flag` among the block's threads and the block total (ballots + LDS)
+__device__ __forceinline__ int block_rank(bool flag, int* wsum, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m = __ballot(flag);
+    const int r = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kJobWaves; ++w) {
+        const int x = wsum[w];
+        if (w < wave) before += x;
+        total += x;
+    }
+    __syncthreads();
+    return before + r;
+}
+
+// inclusive prefix of v over the block; total in `total`
+__device__ __forceinline__ int block_scan_incl(int v, int* wsum, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kJobWaves; ++w) {
+        const int t = wsum[w];
+        if (w < wave) before += t;
+        total += t;
+    }
+    __syncthreads();
+    return before + x;
+}
+
+// ---------------------------------------------------------------- adjacency under a view
+// Row of node x for job J: the job's own row, then the newest visible override, then the
+// base CSR.  Returns a pointer to the row's nodes, len = -1 when x has no adj_list row.
+__device__ __forceinline__ const int32_t* row_of(const DevJobsStore& g, const DevView& v, const DevJob& J,
+                                                 const int32_t* pool, int32_t x, int32_t& len) {
+    if (x == J.own) {  // the job's own row lives in the plan pool
+        len = J.own_len;
+        return pool + J.own_off;
+    }
+    if (v.n > 0) {
+        int lo = 0, hi = v.n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (v.node[mid] < x) lo = mid + 1; else hi = mid;
+        }
+        for (int i = lo; i < v.n && v.node[i] == x; ++i)
+            if (v.ver[i] <= J.version) {
+                len = v.len[i];
+                return v.nbr + v.off[i];
+            }
+    }
+    if (x < 0 || x >= g.M) {
+        len = -1;
+        return g.g_nbr;
+    }
+    len = g.g_len[x];
+    return g.g_nbr + g.g_off[x];
+}
+
+// ---------------------------------------------------------------- K3: gather
+__device__ __forceinline__ uint32_t node_hash(int32_t x) { return (uint32_t)x * 0x9E3779B1u; }
+
+// slot of node x in the job's table (claimed if absent); keys hold node + 1, 0 = empty
+__device__ __forceinline__ uint32_t ht_claim(int32_t* keys, uint32_t mask, int32_t x) {
+    uint32_t h = (node_hash(x) >> 7) & mask;
+    for (;;) {
+        const int32_t old = atomicCAS(&keys[h], 0, x + 1);
+        if (old == 0 || old == x + 1) return h;
+        h = (h + 1) & mask;
+    }
+}
+
+// one workgroup per job
+__global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
+                                                             const int32_t* __restrict__ pool, int32_t* __restrict__ ht,
+                                                             int32_t* __restrict__ seq, int32_t* __restrict__ cand_slot,
+                                                             int32_t* __restrict__ cand_id, int32_t* __restrict__ ncand,
+                                                             const int64_t* __restrict__ pool64) {
+    __shared__ int wsum[kJobWaves];
+    __shared__ int s_count, s_keep, s_done;
+    const DevJob J = jobs[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int32_t u = J.u;
+    const int32_t* frow = pool + J.f_off;
+    int32_t* slots = cand_slot + J.cand_off;
+    int32_t* ids = cand_id + J.cand_off;
+
+    if (J.kind == kDjCollab || J.kind == kDjClubs) {  // the pairs (u, f) of sim_u_f
+        const int32_t* fd = pool + J.fd_off;
+        for (int r = tid; r < J.nfd; r += kJobThreads) cand_slot[J.sim_off + r] = g.slot_of[fd[r]];
+    }
+    if (J.kind == kDjClubs) {
+        // recommender_clubs.cpp:47-58: each distinct friend's row, fof != u with a profile
+        const int32_t* fd = pool + J.fd_off;
+        const int64_t* sreg = pool64 + J.sreg_off;
+        for (int r = 0; r < J.nfd; ++r) {
+            int32_t len;
+            const int32_t* row = row_of(g, vw, J, pool, fd[r], len);
+            for (int k = tid; k < len; k += kJobThreads) {
+                const int32_t x = row[k];
+                cand_slot[sreg[r] + k] = (x != u && x >= 0 && x < g.n) ? g.slot_of[x] : -1;
+            }
+        }
+        return;
+    }
+
+    const uint32_t cap = 1u << J.ht_lg, mask = cap - 1u;
+    int32_t* keys = ht + J.ht_off;
+    int32_t* pos = keys + cap;
+    int32_t* flag = pos + cap;
+    for (uint32_t i = tid; i < cap; i += kJobThreads) {
+        keys[i] = 0;
+        pos[i] = INT_MAX;
+        flag[i] = 0;
+    }
+    __syncthreads();
+    const bool interest = J.kind == kDjInterest || J.kind == kDjAll;
+    if (interest) {  // recommender_graph.cpp:46-52: existing = adj[u] + {u}
+        for (int j = tid; j <= J.nf; j += kJobThreads) {
+            const int32_t x = j < J.nf ? frow[j] : u;
+            __hip_atomic_store(&flag[ht_claim(keys, mask, x)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+
+    if (J.kind == kDjAll) {  // every profile but the excluded ones, in idx order
+        for (int32_t i = tid; i < J.cap; i += kJobThreads) {
+            bool ex = false;
+            uint32_t h = (node_hash(i) >> 7) & mask;
+            for (;;) {
+                const int32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k == 0) break;
+                if (k == i + 1) {
+                    ex = __hip_atomic_load(&flag[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    break;
+                }
+                h = (h + 1) & mask;
+            }
+            slots[i] = ex ? -1 : g.slot_of[i];
+            ids[i] = ex ? -1 : g.g_uid[i];
+        }
+        if (tid == 0) ncand[blockIdx.x] = J.cap;
+        return;
+    }
+
+    const bool graph = J.kind == kDjInterest || J.kind == kDjRawGraph;
+    const bool raw = J.kind == kDjRawGraph || J.kind == kDjRawCollab;
+    // segment lengths: graph = [f, row(f)...] unless f == u (skipped whole, :18); collab =
+    // row(f) when f has one (:116-118)
+    int32_t* seg = seq + J.seg_off;  // [nf + 1] exclusive prefix
+    if (tid == 0) s_count = 0;
+    {
+        int carry = 0;
+        for (int b = 0; b < J.nf; b += kJobThreads) {
+            const int j = b + tid;
+            int len = 0;
+            if (j < J.nf) {
+                const int32_t f = frow[j];
+                int32_t rl;
+                row_of(g, vw, J, pool, f, rl);
+                if (graph) len = f == u ? 0 : 1 + (rl > 0 ? rl : 0);
+                else len = rl > 0 ? rl : 0;
+            }
+            int tot;
+            const int incl = block_scan_incl(len, wsum, tot);
+            if (j < J.nf) seg[j] = carry + incl - len;
+            carry += tot;
+        }
+        if (tid == 0) seg[J.nf] = carry;
+    }
+    __syncthreads();
+    const int total = seg[J.nf];
+    if (tid == 0) {
+        s_count = 0;
+        s_keep = 0;
+        s_done = 0;
+    }
+    __syncthreads();
+    for (int base = 0; base < total; base += kJobThreads) {
+        const int p = base + tid;
+        int32_t x = -1;
+        if (p < total) {
+            int lo = 0, hi = J.nf;  // last friend j with seg[j] <= p
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (seg[mid] <= p) lo = mid; else hi = mid;
+            }
+            const int32_t f = frow[lo];
+            const int k = p - seg[lo];
+            if (graph && k == 0) x = f;
+            else {
+                int32_t rl;
+                const int32_t* row = row_of(g, vw, J, pool, f, rl);
+                x = row[graph ? k - 1 : k];
+            }
+            if (x == u) x = -1;  // :22 / :120
+        }
+        uint32_t h = 0;
+        if (x >= 0) {
+            h = ht_claim(keys, mask, x);
+            atomicMin(&pos[h], p);
+        }
+        __syncthreads();
+        // the table lives at L2 (device-scope atomics): read it past the CU's L1
+        const bool first = x >= 0 && __hip_atomic_load(&pos[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p;
+        int nfirst;
+        const int rf = block_rank(first, wsum, nfirst);
+        const int cnt = s_count;
+        const bool in = first && cnt + rf < J.L;
+        bool keep = in;
+        if (!raw) {
+            if (interest)  // :46-54
+                keep = keep && __hip_atomic_load(&flag[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && x < g.n;
+            else keep = keep && x < g.n;                           // :167-170
+        }
+        int nkeep;
+        const int rk = block_rank(keep, wsum, nkeep);
+        const int kb = s_keep;
+        if (keep) {
+            slots[kb + rk] = raw ? 0 : g.slot_of[x];
+            ids[kb + rk] = g.g_uid[x];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            s_count = cnt + nfirst;
+            s_keep = kb + nkeep;
+        }
+        __syncthreads();
+        if (s_count >= J.L) break;
+    }
+    const int nk = s_keep;
+    for (int i = nk + tid; i < J.cap; i += kJobThreads) {
+        slots[i] = -1;
+        ids[i] = -1;
+    }
+    if (tid == 0) ncand[blockIdx.x] = nk;
+}
+
+// ---------------------------------------------------------------- K6: query images
+__device__ __forceinline__ int find_val(const int32_t* vals, int n, int32_t v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (vals[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return (lo < n && vals[lo] == v) ? lo : -1;
+}
+
+// float idf of (column t, tid) as the reference reads it (recommender.cpp:78: absent -> 1.0)
+__device__ __forceinline__ double idf_of(const DevJobsStore& g, int t, int32_t tid) {
+    if (!g.has_idf[t]) return 1.0;
+    const int64_t b = g.idf_off[t];
+    const int i = find_val(g.idf_tid + b, (int)(g.idf_off[t + 1] - b), tid);
+    return i < 0 ? 1.0 : (double)g.idf_val[b + i];
+}
+
+// one workgroup per image: QConst | table (ntab << lg, then 2^lge exclusions) | vals
+template <bool PACKED>
+__global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJobsStore g, const ImgJob* __restrict__ ij,
+                                                             uint8_t* __restrict__ pool, uint32_t* __restrict__ scratch,
+                                                             int32_t* __restrict__ fail) {
+    __shared__ int s_fail, s_nuniq;
+    const ImgJob I = ij[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int p = g.slot_of[I.idx];
+    const uint4 h0 = st.hdr0[p], h1 = st.hdr1[p], h2 = st.hdr2[p];
+    QConst* q = reinterpret_cast<QConst*>(pool + I.const_off);
+    // 1. constants: the template, then this user's fields (pf_store.cpp fill_qconst)
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(g.tmpl);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(q);
+        for (uint32_t i = tid; i < sizeof(QConst) / 4; i += kJobThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+    const int32_t comp = (int32_t)h0.z, age = (int32_t)h0.w;
+    const int32_t reg0 = (int32_t)h1.x, reg1 = (int32_t)h1.y, reg2 = (int32_t)h1.z;
+    const int a_regcnt = (reg0 >= 0) + (reg1 >= 0) + (reg2 >= 0);
+    const uint64_t colmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    const int ci = comp > 0 ? find_val(g.comp_vals, g.n_comp, comp) : -1;
+    const int ai = age > 0 ? find_val(g.age_vals, g.n_age, age) : -1;
+    for (int v = tid; v <= kValTab; v += kJobThreads) {
+        q->sig_comp[v] = ci >= 0 ? g.comp_rows[(size_t)ci * (kValTab + 1) + v] : 0.0;
+        q->sig_age[v] = ai >= 0 ? g.age_rows[(size_t)ai * (kValTab + 1) + v] : 0.0;
+    }
+    if (tid < 16) q->sig_reg[tid >> 2][tid & 3] = a_regcnt > 0 ? g.sig_reg[a_regcnt * 16 + tid] : 0.0;
+    const Loc l = loc_of(st, p);
+    for (int t = tid; t < kMaxCols; t += kJobThreads)
+        q->sqrt_na[t] = (t < q->n_cols && ((colmask >> t) & 1ull)) ? col_norm(st, l, colmask, t) : 0.0;
+    const uint32_t nc = h2.y, nf = h2.z, ntok = h2.w;
+    if (tid == 0) {
+        q->colmask = colmask;
+        q->comp = comp;
+        q->age = age;
+        q->reg[0] = reg0;
+        q->reg[1] = reg1;
+        q->reg[2] = reg2;
+        q->a_regcnt = a_regcnt;
+        q->pubcode = h2.x & 0xFFu;
+        q->gencode = (h2.x >> 8) & 0xFFu;
+        q->n_clubs = (int32_t)nc;
+        q->n_friends = (int32_t)nf;
+        q->sqrt_clubs = sqrt((double)nc);
+        q->sqrt_friends = sqrt((double)nf);
+        q->n_vals = (int32_t)ntok;
+        q->lg = I.lg;
+        q->lg_excl = I.lge;
+        q->excl_off = (uint32_t)((PACKED ? 1u : 3u) << I.lg);
+        s_fail = 0;
+        s_nuniq = 0;
+    }
+    // 2. token values in record order (vi = token rank), recommender.cpp:74-85
+    const uint32_t len = record_words(h2, PACKED);
+    const uint32_t qw = chunk_words(len, l.lgk, PACKED);
+    const uint32_t nset = nc + nf;
+    QVal* vals = reinterpret_cast<QVal*>(pool + I.vals_off);
+    for (uint32_t k = tid; k < ntok; k += kJobThreads) {
+        int t;
+        int32_t tid_, tf;
+        if (PACKED) {
+            const uint32_t w = word_at(st, l, qw, nset + k);
+            t = (int)((w >> kTidBits) & 63u);
+            tid_ = (int32_t)(w & kTidMask);
+            tf = (int32_t)(w >> 24);
+        } else {
+            tid_ = (int32_t)word_at(st, l, qw, nset + 2 * k);
+            const uint32_t w = word_at(st, l, qw, nset + 2 * k + 1);
+            t = (int)(w & 0xFFu);
+            tf = (int32_t)w >> 8;
+        }
+        const double idf = idf_of(g, t, tid_);
+        QVal v;
+        v.wq = (double)tf * idf;
+        v.idf = idf;
+        vals[k] = v;
+    }
+    // 3. distinct clubs / friends (a set in scratch), then every item in one list:
+    //    items [0, nuniq) sets, then tokens
+    uint32_t* dset = scratch + I.scr_off;               // 2^dlg keys (0 = empty)
+    uint64_t* items = reinterpret_cast<uint64_t*>(scratch + I.scr_off + (1u << I.dlg));
+    const uint32_t dmask = (1u << I.dlg) - 1u;
+    for (uint32_t i = tid; i <= dmask; i += kJobThreads) dset[i] = 0u;
+    __syncthreads();
+    for (uint32_t j = tid; j < nset; j += kJobThreads) {
+        const uint32_t w = word_at(st, l, qw, j);
+        const bool club = j < nc;
+        const uint32_t id = PACKED ? (club ? (w & ~kTagClub) : w) : w;
+        // set key: id + 1 for clubs, id + 1 with bit 31 for friends (ids < 2^31 - 1 here)
+        const uint32_t key = (id + 1u) | (club ? 0u : 0x80000000u);
+        uint32_t h = (node_hash((int32_t)key) >> 5) & dmask;
+        bool won = false;
+        for (;;) {
+            const uint32_t old = atomicCAS(&dset[h], 0u, key);
+            if (old == 0u) { won = true; break; }
+            if (old == key) break;
+            h = (h + 1u) & dmask;
+        }
+        if (won) {
+            uint64_t e;
+            if (PACKED) e = club ? make_entry(id | kTagClub, 1u) : make_entry(id, 0x10000u);
+            else e = make_entry(id, 0u) | ((uint64_t)(club ? 0u : 1u) << 62);  // table choice in bit 62 (val 0)
+            items[atomicAdd(&s_nuniq, 1)] = e;
+        }
+    }
+    __syncthreads();
+    const uint32_t nuniq = (uint32_t)s_nuniq;
+    for (uint32_t k = tid; k < ntok; k += kJobThreads) {
+        uint64_t e;
+        if (PACKED) {
+            const uint32_t w = word_at(st, l, qw, nset + k);
+            const uint32_t t = (w >> kTidBits) & 63u;
+            e = make_entry(kTagTok | (t << kTidBits) | (w & kTidMask), kTokVal | k | (t << kTidBits));
+        } else {
+            const uint32_t tid_ = word_at(st, l, qw, nset + 2 * k);
+            const uint32_t t = word_at(st, l, qw, nset + 2 * k + 1) & 0xFFu;
+            e = make_entry(tid_, t | (k << 8)) | (2ull << 62);
+        }
+        items[nuniq + k] = e;
+    }
+    __syncthreads();
+    // 4. 2-choice cuckoo (pf_store.cpp cuckoo_fill): parallel insertion with atomic exchange;
+    //    a chain longer than 500 kicks fails the attempt, the next multiplier is tried
+    const uint32_t nitems = nuniq + ntok;
+    const int lg = I.lg;
+    const uint32_t cap = 1u << lg;
+    const uint64_t empty = PACKED ? kEmptyEntryPacked : kEmptyEntry;
+    unsigned long long* tab = reinterpret_cast<unsigned long long*>(pool + I.keys_off);
+    const uint32_t ntab = PACKED ? 1u : 3u;
+    const uint32_t tab_total = (ntab << lg) + (1u << I.lge);
+    for (uint32_t s = 0; s < 16; ++s) {
+        const uint32_t hmul = kHashMul + 2u * s * 0x6A09E667u;
+        for (uint32_t i = tid; i < tab_total; i += kJobThreads) tab[i] = empty;
+        __syncthreads();
+        for (uint32_t i = tid; i < nitems; i += kJobThreads) {
+            uint64_t cur = items[i];
+            const uint32_t tsel = PACKED ? 0u : (uint32_t)(cur >> 62);
+            cur &= PACKED ? ~0ull : ~(3ull << 62);
+            unsigned long long* T = tab + ((size_t)tsel << lg);
+            uint32_t x = cuckoo_x((uint32_t)cur, hmul);
+            uint32_t at = cuckoo_h1(x, lg);
+            bool placed = false;
+            for (int kick = 0; kick < 500; ++kick) {
+                const unsigned long long old = atomicExch(&T[at], (unsigned long long)cur);
+                if (old == empty) { placed = true; break; }
+                cur = old;  // evicted: to its other slot
+                x = cuckoo_x((uint32_t)cur, hmul);
+                const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
+                at = at == a ? b : a;
+            }
+            if (!placed) atomicOr(&s_fail, 1);
+        }
+        __syncthreads();
+        const int failed = s_fail;
+        __syncthreads();
+        if (!failed) {
+            if (tid == 0) q->hmul = hmul;
+            return;
+        }
+        if (tid == 0) s_fail = 0;
+        __syncthreads();
+    }
+    if (tid == 0) atomicOr(fail, 1);
+    (void)cap;
+}
+
+// ---------------------------------------------------------------- K4': collaborative sums
+// recommender_graph.cpp:167-180: for each candidate, sum over friend-list positions (in order,
+// duplicates included) of (double)sim_u_f * (double)FAS(f, c); friends without a profile skip
+__global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __restrict__ jobs, const int32_t* __restrict__ jix,
+                                                             const int32_t* __restrict__ pool, const float* __restrict__ pout,
+                                                             const int32_t* __restrict__ cand_slot, float* __restrict__ score) {
+    const DevJob J = jobs[jix[blockIdx.y]];
+    const int c = blockIdx.x * kJobThreads + threadIdx.x;
+    if (c >= J.cap) return;
+    if (cand_slot[J.cand_off + c] < 0) return;
+    const int32_t* fpos = pool + J.fpos_off;
+    const float* sim = pout + J.sim_off;
+    const float* M = pout + J.m_off;
+    double s = 0.0;
+    for (int j = 0; j < J.nf; ++j) {
+        const int r = fpos[j];
+        if (r < 0) continue;
+        s += (double)sim[r] * (double)M[(size_t)r * J.cap + c];
+    }
+    score[J.out_off + c] = (float)s;
+}
+
+// ---------------------------------------------------------------- K7: clubs
+// recommender_clubs.cpp:34-66 with club_scores[c] += ... in the reference's sequence: every
+// lane of the job's wave walks the same contributions in order and adds only the clubs it
+// owns (dense index % 64 == lane), so each club's double sum is the reference's.
+__global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
+                                                   const int32_t* __restrict__ jix, const int32_t* __restrict__ pool,
+                                                   const int64_t* __restrict__ pool64, const float* __restrict__ pout,
+                                                   double* __restrict__ acc_all, int32_t* __restrict__ touched_all,
+                                                   float* __restrict__ score, int32_t* __restrict__ ids,
+                                                   int32_t* __restrict__ ncand, int64_t acc_stride) {
+    const int slot = blockIdx.x;
+    const DevJob J = jobs[jix[slot]];
+    const int lane = threadIdx.x;
+    double* acc = acc_all + (size_t)slot * acc_stride;     // dense club scores (zero between jobs)
+    int32_t* touched = touched_all + (size_t)slot * acc_stride;  // 0 / 1 per dense club
+    __shared__ int s_n;
+    if (lane == 0) s_n = 0;
+    __syncthreads();
+    const int32_t u = J.u;
+    const int32_t* frow = pool + J.f_off;
+    const int32_t* fpos = pool + J.fpos_off;
+    const float* sim = pout + J.sim_off;
+    const int64_t* sreg = pool64 + J.sreg_off;
+    const int64_t uc0 = g.club_off[u], uc1 = g.club_off[u + 1];
+    auto own_club = [&](int32_t d) {  // user_clubs (the query's clubs)
+        for (int64_t k = uc0; k < uc1; ++k)
+            if (g.club_dense[k] == d) return true;
+        return false;
+    };
+    int32_t* list = ids + J.out_off;  // dense indices of the touched clubs, in touch order
+    auto add = [&](int32_t d, double v) {
+        if ((d & 63) != lane) return;
+        if (!touched[d]) {
+            touched[d] = 1;
+            list[atomicAdd(&s_n, 1)] = d;
+        }
+        acc[d] += v;
+    };
+    // phase 1 (:34-44): friends in order, w > 0, their clubs not in user_clubs
+    for (int j = 0; j < J.nf; ++j) {
+        const int r = fpos[j];
+        if (r < 0) continue;
+        const double w = (double)sim[r];
+        if (w <= 0.0) continue;
+        const int32_t f = frow[j];
+        for (int64_t k = g.club_off[f]; k < g.club_off[f + 1]; ++k) {
+            const int32_t d = g.club_dense[k];
+            if (!own_club(d)) add(d, w);
+        }
+    }
+    // phase 2 (:46-66): friends in order with a row, a profile and w > 0; fof in row order
+    for (int j = 0; j < J.nf; ++j) {
+        const int r = fpos[j];
+        if (r < 0) continue;
+        const int32_t f = frow[j];
+        int32_t len;
+        const int32_t* row = row_of(g, vw, J, pool, f, len);
+        if (len < 0) continue;
+        const double w = (double)sim[r];
+        if (w <= 0.0) continue;
+        const float* S = pout + sreg[r];
+        for (int k = 0; k < len; ++k) {
+            const int32_t x = row[k];
+            if (x == u || x < 0 || x >= g.n) continue;
+            const double s = (double)S[k];
+            if (s <= 0.0) continue;
+            const double contrib = w * s;
+            for (int64_t c = g.club_off[x]; c < g.club_off[x + 1]; ++c) {
+                const int32_t d = g.club_dense[c];
+                if (!own_club(d)) add(d, contrib);
+            }
+        }
+    }
+    __syncthreads();
+    // scored list (score, club id); the accumulators go back to zero for the next job
+    const int n = s_n;
+    for (int i = lane; i < n; i += 64) {
+        const int32_t d = list[i];
+        score[J.out_off + i] = (float)acc[d];
+        acc[d] = 0.0;
+        touched[d] = 0;
+        list[i] = g.club_id[d];
+    }
+    if (lane == 0) ncand[jix[slot]] = n;
+}
+
+// ---------------------------------------------------------------- K8: top-k
+// per job: the k smallest keys of (score desc, id asc) over its scored list (ids < 0 skipped)
+// (user candidates: the slot >= 0 marks a scored pair; clubs: the first ncand entries)
+__global__ __launch_bounds__(kJobThreads) void topk_kernel(const DevJob* __restrict__ jobs, const int32_t* __restrict__ jix,
+                                                           const float* __restrict__ score, const int32_t* __restrict__ ids,
+                                                           const int32_t* __restrict__ slots,
+                                                           const int32_t* __restrict__ ncand, uint64_t* __restrict__ out,
+                                                           int k) {
+    __shared__ uint64_t sc[kJobWaves * kMaxTopK];
+    const int jn = jix[blockIdx.x];
+    const DevJob J = jobs[jn];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n = ncand[jn];
+    const int lim = J.kind == kDjClubs ? n : J.cap;
+    uint64_t list = ~0ull;
+    for (int b = wave * 64; b < lim; b += kJobThreads) {
+        const int i = b + lane;
+        uint64_t key = ~0ull;
+        if (i < lim) {
+            if (J.kind == kDjClubs || slots[J.out_off + i] >= 0) key = score_key(score[J.out_off + i], ids[J.out_off + i]);
+        }
+        topk_push(list, key, k, lane);
+    }
+    if (lane < k) sc[wave * k + lane] = list;
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t acc = ~0ull;
+        const int m = kJobWaves * k;
+        for (int b = 0; b < m; b += 64) topk_push(acc, b + lane < m ? sc[b + lane] : ~0ull, k, lane);
+        if (lane < k) out[(size_t)jn * k + lane] = acc;
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
+                         const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
+                         int32_t* ncand, hipStream_t s) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kJobThreads), 0, s, g, v, jobs, pool, ht, seq, cand_slot,
+                       cand_id, ncand, pool64);
+    return hipGetLastError();
+}
+
+hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n, uint8_t* pool,
+                          uint32_t* scratch, int32_t* fail, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (st.packed) hipLaunchKernelGGL(qimage_kernel<true>, dim3(n), dim3(kJobThreads), 0, s, st, g, ij, pool, scratch, fail);
+    else hipLaunchKernelGGL(qimage_kernel<false>, dim3(n), dim3(kJobThreads), 0, s, st, g, ij, pool, scratch, fail);
+    return hipGetLastError();
+}
+
+hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
+                         const float* pout, const int32_t* cand_slot, float* score, hipStream_t s) {
+    if (njobs <= 0 || max_cap <= 0) return hipSuccess;
+    for (int b = 0; b < njobs; b += 65535) {
+        const int nb = njobs - b < 65535 ? njobs - b : 65535;
+        hipLaunchKernelGGL(collab_kernel, dim3((max_cap + kJobThreads - 1) / kJobThreads, nb), dim3(kJobThreads), 0, s,
+                           jobs, jix + b, pool, pout, cand_slot, score);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
+                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, int32_t* touched,
+                        float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(clubs_kernel, dim3(njobs), dim3(64), 0, s, g, v, jobs, jix, pool, pool64, pout, acc, touched,
+                       score, ids, ncand, acc_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_job_topk(const DevJob* jobs, const int32_t* jix, int njobs, const float* score, const int32_t* ids,
+                           const int32_t* slots, const int32_t* ncand, uint64_t* out, int k, hipStream_t s) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(topk_kernel, dim3(njobs), dim3(kJobThreads), 0, s, jobs, jix, score, ids, slots, ncand, out, k);
+    return hipGetLastError();
+}
+
+}  // namespace pf

@@ -1,0 +1,748 @@
+// pf_jobs_plan.cpp — host side of the device job pipeline (pf_jobs.hip): the graph store and
+// image-builder tables built at pf_open, and run_jobs, which plans a batch of the reference's
+// recommender calls (recommend_by_interest / _collaborative / recommend_clubs_collab under an
+// adjacency view, pf_batch.h) and runs it as one chain of device stages on the context's
+// stream: K6 images -> K3 gathers -> K1' pairs -> K4' / K7 -> K8 top-k, one copy back.
+//
+// The host works on 1-hop data only (the job's own adjacency row and its friends' row lengths,
+// for sizing); every 2-hop walk, de-duplication, FAS pair, sum and top-k runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+#include "pf_batch.h"
+#include "pf_ctx.h"
+#include "pf_kernels.h"
+
+namespace pf {
+
+namespace {
+
+constexpr int kDevTopK = kMaxTopK;           // K8 keeps up to 64 keys per job
+constexpr int64_t kChunkElems = 192ll << 20; // element workspace per chunk (x 12 B)
+constexpr int64_t kChunkHt = 128ll << 20;    // gather hash tables per chunk (int32 words)
+constexpr uint32_t kStageLimitJobs = 48 * 1024;  // as pf_api.cpp kStageLimit (LDS-staged tables)
+
+int32_t node_of(const pf_ctx* c, int32_t uid) {
+    const int32_t i = c->hc.idx_of(uid);
+    if (i >= 0) return i;
+    auto it = c->jb.xnode.find(uid);
+    return it == c->jb.xnode.end() ? -1 : it->second;
+}
+
+int32_t ensure_node(pf_ctx* c, int32_t uid) {
+    int32_t x = node_of(c, uid);
+    if (x >= 0) return x;
+    auto& J = c->jb;
+    x = (int32_t)J.g_uid.size();
+    J.xnode.emplace(uid, x);
+    J.g_uid.push_back(uid);
+    J.g_len.push_back(-1);
+    J.nodes_dirty = true;
+    return x;
+}
+
+template <class T>
+hipError_t up(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
+    return upload(c, b, v);
+}
+
+int a16(int64_t x) { return (int)((x + 15) & ~15ll); }
+size_t a16z(size_t x) { return (x + 15) & ~(size_t)15; }
+
+int pow2_lg(int64_t n) {
+    int lg = 4;
+    while (((int64_t)1 << lg) < n) ++lg;
+    return lg;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- open
+int jobs_open(pf_ctx* c) {
+    auto& J = c->jb;
+    const HostCorpus& hc = c->hc;
+    const HostStore& hs = c->hs;
+    const int32_t n = hc.n, T = hc.T;
+    const bool packed = hs.packed;
+    J.ok = false;
+    // image-builder tables: QConst template, region rows, completion / age rows (glibc exp)
+    QConst tmpl;
+    qconst_template(hc, packed, tmpl);
+    std::vector<QConst> tv(1, tmpl);
+    std::vector<double> sreg(4 * 16, 0.0);
+    for (int a = 1; a <= 3; ++a) {
+        double r[4][4];
+        qconst_sig_reg(hc, a, r);
+        for (int b = 0; b < 4; ++b)
+            for (int m = 0; m < 4; ++m) sreg[a * 16 + b * 4 + m] = r[b][m];
+    }
+    auto ratio_rows = [&](const std::vector<int32_t>& v, int slot, std::vector<int32_t>& vals, std::vector<double>& rows) {
+        for (int32_t x : v) if (x > 0) vals.push_back(x);
+        std::sort(vals.begin(), vals.end());
+        vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+        rows.assign(vals.size() * (kValTab + 1), 0.0);
+        par_jobs(vals.size(), [&](size_t i) { qconst_ratio_row(hc, slot, vals[i], &rows[i * (kValTab + 1)]); }, 16);
+    };
+    std::vector<int32_t> comp_vals, age_vals;
+    std::vector<double> comp_rows, age_rows;
+    ratio_rows(hc.comp, PF_F_COMPLETION, comp_vals, comp_rows);
+    ratio_rows(hc.age, PF_F_AGE, age_vals, age_rows);
+    // idf per column, sorted by tid (recommender.cpp:78: absent -> 1.0)
+    std::vector<int64_t> idf_off(T + 1, 0);
+    std::vector<int32_t> idf_tid;
+    std::vector<float> idf_val;
+    for (int t = 0; t < T; ++t) {
+        std::vector<std::pair<int32_t, float>> v(hc.idf[t].begin(), hc.idf[t].end());
+        std::sort(v.begin(), v.end());
+        for (auto& e : v) { idf_tid.push_back(e.first); idf_val.push_back(e.second); }
+        idf_off[t + 1] = (int64_t)idf_tid.size();
+    }
+    // graph: nodes 0..n-1 = profiles (idx), then adj_list uids without a profile
+    J.xnode.clear();
+    J.g_uid.assign(hc.uid.begin(), hc.uid.end());
+    std::vector<const std::pair<const int32_t, std::vector<int32_t>>*> rows;
+    rows.reserve(hc.adj.size());
+    for (auto& kv : hc.adj) rows.push_back(&kv);
+    {
+        std::vector<std::vector<int32_t>> unknown(16);
+        const size_t R = rows.size();
+        std::vector<std::thread> ts;
+        for (int w = 0; w < 16; ++w)
+            ts.emplace_back([&, w]() {
+                for (size_t r = w; r < R; r += 16) {
+                    if (hc.idx_of(rows[r]->first) < 0) unknown[w].push_back(rows[r]->first);
+                    for (int32_t x : rows[r]->second)
+                        if (hc.idx_of(x) < 0) unknown[w].push_back(x);
+                }
+            });
+        for (auto& t : ts) t.join();
+        for (auto& u : unknown)
+            for (int32_t x : u)
+                if (!J.xnode.count(x)) {
+                    J.xnode.emplace(x, (int32_t)J.g_uid.size());
+                    J.g_uid.push_back(x);
+                }
+    }
+    const int32_t M = (int32_t)J.g_uid.size();
+    J.g_len.assign(M, -1);
+    std::vector<int64_t> g_off(M, 0);
+    std::vector<int32_t> rnode(rows.size());
+    std::vector<int64_t> roff(rows.size() + 1, 0);
+    for (size_t r = 0; r < rows.size(); ++r) roff[r + 1] = roff[r] + (int64_t)rows[r]->second.size();
+    std::vector<int32_t> g_nbr((size_t)roff.back());
+    par_jobs(rows.size(), [&](size_t r) {
+        const int32_t x = node_of(c, rows[r]->first);
+        rnode[r] = x;
+        const auto& row = rows[r]->second;
+        for (size_t k = 0; k < row.size(); ++k) g_nbr[roff[r] + k] = node_of(c, row[k]);
+    }, 4096);
+    for (size_t r = 0; r < rows.size(); ++r) {
+        g_off[rnode[r]] = roff[r];
+        J.g_len[rnode[r]] = (int32_t)rows[r]->second.size();
+    }
+    // clubs as dense indices (K7), per profile idx in profile order
+    std::vector<int32_t> club_id(hc.clubs.begin(), hc.clubs.end());
+    std::sort(club_id.begin(), club_id.end());
+    club_id.erase(std::unique(club_id.begin(), club_id.end()), club_id.end());
+    std::vector<int32_t> club_dense(hc.clubs.size());
+    par_jobs(hc.clubs.size(), [&](size_t k) {
+        club_dense[k] = (int32_t)(std::lower_bound(club_id.begin(), club_id.end(), (int32_t)hc.clubs[k]) - club_id.begin());
+    }, 1 << 16);
+    // per profile: query-table size (pf_store.cpp build_query) and its raw set words
+    J.img_lg.assign(n, 0);
+    J.img_nset.assign(n, 0);
+    par_jobs((size_t)n, [&](size_t i) {
+        std::vector<uint32_t> v(hc.clubs.begin() + hc.club_off[i], hc.clubs.begin() + hc.club_off[i + 1]);
+        std::sort(v.begin(), v.end());
+        const size_t dc = (size_t)(std::unique(v.begin(), v.end()) - v.begin());
+        v.assign(hc.friends.begin() + hc.friend_off[i], hc.friends.begin() + hc.friend_off[i + 1]);
+        std::sort(v.begin(), v.end());
+        const size_t df = (size_t)(std::unique(v.begin(), v.end()) - v.begin());
+        const size_t nt = (size_t)(hc.tok_off[(i + 1) * (size_t)T] - hc.tok_off[i * (size_t)T]);
+        const int lg = packed ? lg_for(dc + df + nt) : std::max({lg_for(dc), lg_for(df), lg_for(nt)});
+        const bool ok = lg <= kMaxHashLog2 && nt < (packed ? (1u << kTidBits) : (1u << 22));
+        J.img_lg[i] = ok ? (uint8_t)lg : 0;
+        J.img_nset[i] = (int32_t)((hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]));
+    }, 4096);
+    std::vector<int32_t> slot_of(hs.slot_of_idx.begin(), hs.slot_of_idx.end());
+    std::vector<uint8_t> has_idf(hc.has_idf.begin(), hc.has_idf.end());
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = up(c, J.d_tmpl, tv);
+    if (e == hipSuccess) e = up(c, J.d_sigreg, sreg);
+    if (e == hipSuccess) e = up(c, J.d_comp_vals, comp_vals);
+    if (e == hipSuccess) e = up(c, J.d_comp_rows, comp_rows);
+    if (e == hipSuccess) e = up(c, J.d_age_vals, age_vals);
+    if (e == hipSuccess) e = up(c, J.d_age_rows, age_rows);
+    if (e == hipSuccess) e = up(c, J.d_idf_off, idf_off);
+    if (e == hipSuccess) e = up(c, J.d_idf_tid, idf_tid);
+    if (e == hipSuccess) e = up(c, J.d_idf_val, idf_val);
+    if (e == hipSuccess) e = up(c, J.d_has_idf, has_idf);
+    if (e == hipSuccess) e = up(c, J.d_slot_of, slot_of);
+    if (e == hipSuccess) e = up(c, J.d_goff, g_off);
+    if (e == hipSuccess) e = up(c, J.d_glen, J.g_len);
+    if (e == hipSuccess) e = up(c, J.d_gnbr, g_nbr);
+    if (e == hipSuccess) e = up(c, J.d_guid, J.g_uid);
+    if (e == hipSuccess) e = up(c, J.d_club_off, hc.club_off);
+    if (e == hipSuccess) e = up(c, J.d_club_dense, club_dense);
+    if (e == hipSuccess) e = up(c, J.d_club_id, club_id);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the host vectors die here
+    if (e != hipSuccess) return c->hip_fail(e, "job pipeline upload");
+    DevJobsStore& g = J.js;
+    g.tmpl = J.d_tmpl.as<QConst>();
+    g.sig_reg = J.d_sigreg.as<double>();
+    g.comp_vals = J.d_comp_vals.as<int32_t>();
+    g.comp_rows = J.d_comp_rows.as<double>();
+    g.age_vals = J.d_age_vals.as<int32_t>();
+    g.age_rows = J.d_age_rows.as<double>();
+    g.n_comp = (int32_t)comp_vals.size();
+    g.n_age = (int32_t)age_vals.size();
+    g.idf_off = J.d_idf_off.as<int64_t>();
+    g.idf_tid = J.d_idf_tid.as<int32_t>();
+    g.idf_val = J.d_idf_val.as<float>();
+    g.has_idf = J.d_has_idf.as<uint8_t>();
+    g.slot_of = J.d_slot_of.as<int32_t>();
+    g.g_off = J.d_goff.as<int64_t>();
+    g.g_len = J.d_glen.as<int32_t>();
+    g.g_nbr = J.d_gnbr.as<int32_t>();
+    g.g_uid = J.d_guid.as<int32_t>();
+    g.n = n;
+    g.M = M;
+    g.club_off = J.d_club_off.as<int64_t>();
+    g.club_dense = J.d_club_dense.as<int32_t>();
+    g.club_id = J.d_club_id.as<int32_t>();
+    g.n_club_ids = (int32_t)club_id.size();
+    J.edited.clear();
+    J.edit_gen = 1;
+    J.view_gen = 0;
+    J.view_over = nullptr;
+    J.view_over_n = 0;
+    J.nodes_dirty = false;
+    J.ok = true;
+    return PF_OK;
+}
+
+void jobs_note_edit(pf_ctx* c, int32_t uid) {
+    auto& J = c->jb;
+    if (!J.ok) return;
+    ensure_node(c, uid);
+    auto it = c->hc.adj.find(uid);
+    if (it != c->hc.adj.end())
+        for (int32_t x : it->second) ensure_node(c, x);
+    J.edited.insert(uid);
+    ++J.edit_gen;
+}
+
+namespace {
+
+// the node arrays grew (pf_set_adj named new uids): upload them again
+int sync_nodes(pf_ctx* c) {
+    auto& J = c->jb;
+    if (!J.nodes_dirty) return PF_OK;
+    const int32_t M = (int32_t)J.g_uid.size();
+    std::vector<int64_t> off(M, 0);  // the new nodes have no base row
+    std::vector<int64_t> old((size_t)J.js.M);
+    HIPCHK(c, hipMemcpyAsync(old.data(), J.js.g_off, old.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::copy(old.begin(), old.end(), off.begin());
+    DBuf noff;
+    HIPCHK(c, upload(c, noff, off));
+    HIPCHK(c, upload(c, J.d_glen, J.g_len));
+    HIPCHK(c, upload(c, J.d_guid, J.g_uid));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::swap(J.d_goff.p, noff.p);
+    std::swap(J.d_goff.cap, noff.cap);
+    J.js.g_off = J.d_goff.as<int64_t>();
+    J.js.g_len = J.d_glen.as<int32_t>();
+    J.js.g_uid = J.d_guid.as<int32_t>();
+    J.js.M = M;
+    J.nodes_dirty = false;
+    return PF_OK;
+}
+
+// The overrides this call sees: pf_set_adj's edits (always) and the batched drivers' versioned
+// edits `over` (AdjView::over), uploaded again only when either changed.
+int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>>* over) {
+    auto& J = c->jb;
+    const size_t on = over ? over->size() : 0;
+    if (J.view_gen == J.edit_gen && J.view_over == (const void*)over && J.view_over_n == on) return PF_OK;
+    struct E { int32_t node, ver; int32_t len; const std::vector<int32_t>* row; };
+    std::vector<E> es;
+    for (int32_t u : J.edited) {
+        auto it = c->hc.adj.find(u);
+        es.push_back(E{node_of(c, u), INT_MIN, it == c->hc.adj.end() ? -1 : (int32_t)it->second.size(),
+                       it == c->hc.adj.end() ? nullptr : &it->second});
+    }
+    if (over)
+        for (auto& kv : *over)
+            es.push_back(E{node_of(c, kv.first), kv.second.first, (int32_t)kv.second.second.size(), &kv.second.second});
+    for (const E& x : es)
+        if (x.node < 0) return c->fail(PF_EINTERNAL, "adjacency override names an unmapped uid");
+    std::sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.node != b.node ? a.node < b.node : a.ver > b.ver; });
+    std::vector<int32_t> node(es.size()), ver(es.size()), len(es.size()), nbr;
+    std::vector<int64_t> off(es.size());
+    for (size_t i = 0; i < es.size(); ++i) {
+        node[i] = es[i].node;
+        ver[i] = es[i].ver;
+        len[i] = es[i].len;
+        off[i] = (int64_t)nbr.size();
+        if (es[i].row)
+            for (int32_t x : *es[i].row) {
+                const int32_t y = node_of(c, x);
+                if (y < 0) return c->fail(PF_EINTERNAL, "adjacency override names an unmapped uid");
+                nbr.push_back(y);
+            }
+    }
+    if (nbr.empty()) nbr.push_back(0);
+    HIPCHK(c, upload(c, J.d_view_node, node));
+    HIPCHK(c, upload(c, J.d_view_ver, ver));
+    HIPCHK(c, upload(c, J.d_view_off, off));
+    HIPCHK(c, upload(c, J.d_view_len, len));
+    HIPCHK(c, upload(c, J.d_view_nbr, nbr));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    J.view.node = J.d_view_node.as<int32_t>();
+    J.view.ver = J.d_view_ver.as<int32_t>();
+    J.view.off = J.d_view_off.as<int64_t>();
+    J.view.len = J.d_view_len.as<int32_t>();
+    J.view.nbr = J.d_view_nbr.as<int32_t>();
+    J.view.n = (int32_t)es.size();
+    J.view_gen = J.edit_gen;
+    J.view_over = over;
+    J.view_over_n = on;
+    return PF_OK;
+}
+
+// One planned job (host side).
+struct JP {
+    int kind = -1;               // DevJobKind, -1 = no device work (empty result)
+    int32_t u = -1;              // query node
+    std::vector<int32_t> F;      // row(u) as nodes
+    std::vector<int32_t> fd;     // distinct friends with a profile, first-occurrence order
+    std::vector<int32_t> fpos;   // per row position: index into fd or -1
+    std::vector<int32_t> flen;   // clubs: |row(fd[r])| (0 when absent)
+    std::vector<int32_t> own;    // own row as nodes (when the view replaces u's row)
+    int32_t own_node = -1, own_len = -1;
+    int64_t cap = 0, seqlen = 0;
+    int ht_lg = 0;
+    int64_t elems = 0, ht_words = 0;
+};
+
+// Plan job i of `jobs` under its view: 1-hop work only.
+void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
+    const HostCorpus& hc = c->hc;
+    const int32_t uid = Jb.uid;
+    const int32_t u = raw ? node_of(c, uid) : hc.idx_of(uid);
+    if (u < 0 || (!raw && Jb.topk <= 0)) return;  // recommender_graph.cpp:39-40,130; recommender_clubs.cpp:16
+    p.u = u;
+    const std::vector<int32_t>* ru = Jb.view.row(uid);
+    if (Jb.view.own_row) {  // recommendation_tests.cpp:111-114: the user's row replaced
+        const int32_t o = node_of(c, Jb.view.own);
+        if (o >= 0) {
+            p.own_node = o;
+            p.own_len = (int32_t)Jb.view.own_row->size();
+            for (int32_t x : *Jb.view.own_row) p.own.push_back(node_of(c, x));
+        }
+    }
+    if (ru)
+        for (int32_t x : *ru) p.F.push_back(node_of(c, x));
+    const int64_t L = std::max<int32_t>(Jb.limit, 1);
+    auto rowlen = [&](int32_t node) -> int64_t {
+        const std::vector<int32_t>* r = Jb.view.row(c->jb.g_uid[node]);
+        return r ? (int64_t)r->size() : -1;
+    };
+    if (raw || Jb.kind == kJobInterest) {
+        const bool graph = raw ? Jb.limit_flavour == PF_FOF_GRAPH : true;
+        if (!raw && Jb.all_candidates) {
+            p.kind = kDjAll;
+            p.cap = hc.n;
+            p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1));
+        } else {
+            p.kind = raw ? (graph ? kDjRawGraph : kDjRawCollab) : kDjInterest;
+            for (int32_t f : p.F) {
+                const int64_t rl = rowlen(f);
+                if (graph) p.seqlen += f == u ? 0 : 1 + std::max<int64_t>(rl, 0);
+                else p.seqlen += std::max<int64_t>(rl, 0);
+            }
+            p.cap = std::min<int64_t>(L, p.seqlen);
+            p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + 256));
+        }
+        p.elems = p.cap;
+        p.ht_words = 3ll << p.ht_lg;
+        return;
+    }
+    // collab / clubs: sim_u_f over the distinct friends with a profile (recommender_graph.cpp:132-136)
+    std::unordered_map<int32_t, int32_t> seen;
+    for (int32_t f : p.F) {
+        if (f < 0 || f >= hc.n) { p.fpos.push_back(-1); continue; }
+        auto it = seen.find(f);
+        if (it == seen.end()) {
+            it = seen.emplace(f, (int32_t)p.fd.size()).first;
+            p.fd.push_back(f);
+        }
+        p.fpos.push_back(it->second);
+    }
+    if (Jb.kind == kJobCollab) {
+        p.kind = kDjCollab;
+        for (int32_t f : p.F) p.seqlen += std::max<int64_t>(rowlen(f), 0);
+        p.cap = std::min<int64_t>(L, p.seqlen);
+        p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + 256));
+        p.elems = p.cap + (int64_t)p.fd.size() * (1 + p.cap);
+        p.ht_words = 3ll << p.ht_lg;
+    } else {
+        p.kind = kDjClubs;
+        int64_t s = 0;
+        for (int32_t f : p.fd) {
+            const int64_t rl = std::max<int64_t>(rowlen(f), 0);
+            p.flen.push_back((int32_t)rl);
+            s += rl;
+        }
+        p.elems = (int64_t)p.fd.size() + s + c->jb.js.n_club_ids;
+    }
+}
+
+// Runs jobs[b, e) (planned in P) on the device; fills jobs[i].out, or raw lists in raw_out.
+int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, size_t e,
+              std::vector<std::vector<int32_t>>* raw_out) {
+    auto& J = c->jb;
+    const HostCorpus& hc = c->hc;
+    const bool packed = c->hs.packed;
+    // ---- layout
+    std::vector<DevJob> dj;
+    std::vector<int32_t> pool32;
+    std::vector<int64_t> pool64;
+    std::vector<int32_t> jmap;  // dj index -> job index
+    int64_t E = 0, HT = 0, SEQ = 0;
+    std::unordered_map<int32_t, int32_t> img_of;
+    std::vector<int32_t> img_idx;
+    auto img = [&](int32_t idx) {
+        auto it = img_of.find(idx);
+        if (it != img_of.end()) return it->second;
+        const int32_t k = (int32_t)img_idx.size();
+        img_of.emplace(idx, k);
+        img_idx.push_back(idx);
+        return k;
+    };
+    std::vector<PairBlock> blocks;
+    auto add_blocks = [&](int32_t im, int64_t begin, int64_t count, int64_t out) {
+        for (int64_t x = 0; x < count; x += 256)
+            blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(256, count - x),
+                                       (int32_t)(out + x)});
+    };
+    std::vector<int32_t> jix_collab, jix_clubs, jix_topk;
+    int max_cap_collab = 0, ktop = 1;
+    for (size_t i = b; i < e; ++i) {
+        JP& p = P[i];
+        if (p.kind < 0) continue;
+        DevJob d{};
+        d.kind = p.kind;
+        d.u = p.u;
+        d.L = std::max<int32_t>(jobs[i].limit, 1);
+        d.version = jobs[i].view.version;
+        d.own = p.own_node;
+        d.own_len = p.own_len;
+        d.own_off = (int64_t)pool32.size();
+        pool32.insert(pool32.end(), p.own.begin(), p.own.end());
+        d.f_off = (int64_t)pool32.size();
+        pool32.insert(pool32.end(), p.F.begin(), p.F.end());
+        d.nf = (int32_t)p.F.size();
+        d.ht_lg = p.ht_lg;
+        d.ht_off = HT;
+        HT += p.ht_words;
+        d.seg_off = SEQ;
+        SEQ += (int64_t)p.F.size() + 1;
+        d.cap = (int32_t)p.cap;
+        d.topk = jobs[i].topk;
+        d.nfd = (int32_t)p.fd.size();
+        d.fd_off = (int64_t)pool32.size();
+        pool32.insert(pool32.end(), p.fd.begin(), p.fd.end());
+        d.fpos_off = (int64_t)pool32.size();
+        pool32.insert(pool32.end(), p.fpos.begin(), p.fpos.end());
+        const int32_t jn = (int32_t)dj.size();
+        if (p.kind == kDjClubs) {
+            d.sim_off = E;
+            E += d.nfd;
+            d.sreg_off = (int64_t)pool64.size();
+            for (size_t r = 0; r < p.fd.size(); ++r) {
+                pool64.push_back(E);
+                E += p.flen[r];
+            }
+            d.out_off = E;
+            d.cand_off = E;
+            E += J.js.n_club_ids;
+            const int32_t iu = img(p.u);
+            add_blocks(iu, d.sim_off, d.nfd, d.sim_off);
+            for (size_t r = 0; r < p.fd.size(); ++r) add_blocks(img(p.fd[r]), pool64[d.sreg_off + r], p.flen[r], pool64[d.sreg_off + r]);
+            jix_clubs.push_back(jn);
+        } else {
+            d.cand_off = E;
+            d.out_off = E;
+            E += p.cap;
+            if (p.kind == kDjCollab) {
+                d.sim_off = E;
+                E += d.nfd;
+                d.m_off = E;
+                E += (int64_t)d.nfd * p.cap;
+                const int32_t iu = img(p.u);
+                add_blocks(iu, d.sim_off, d.nfd, d.sim_off);
+                for (int r = 0; r < d.nfd; ++r) add_blocks(img(p.fd[r]), d.cand_off, p.cap, d.m_off + (int64_t)r * p.cap);
+                jix_collab.push_back(jn);
+                max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);
+            } else if (p.kind == kDjInterest || p.kind == kDjAll) {
+                add_blocks(img(p.u), d.cand_off, p.cap, d.cand_off);
+            }
+        }
+        if (p.kind != kDjRawGraph && p.kind != kDjRawCollab && jobs[i].topk <= kDevTopK) {
+            jix_topk.push_back(jn);
+            ktop = std::max(ktop, jobs[i].topk);
+        }
+        dj.push_back(d);
+        jmap.push_back((int32_t)i);
+    }
+    if (dj.empty()) return PF_OK;
+    if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
+    // ---- images (pf_api.cpp plan_images layout)
+    std::vector<ImgJob> ij(img_idx.size());
+    std::vector<QImageRef> refs(img_idx.size());
+    uint32_t max_lds = 0;
+    bool gtab = false;
+    size_t ipool = 0;
+    int64_t scr = 0;
+    const uint32_t ntab = packed ? 1u : 3u;
+    const int lge = lg_for(0);
+    for (size_t k = 0; k < img_idx.size(); ++k) {
+        const int32_t idx = img_idx[k];
+        const int lg = J.img_lg[idx];
+        if (lg == 0) return c->fail(PF_EUNSUPP, "query hash table too large");
+        const int64_t ntok = hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T];
+        ImgJob& m = ij[k];
+        m.idx = idx;
+        m.lg = lg;
+        m.lge = lge;
+        m.dlg = pow2_lg(2 * (int64_t)J.img_nset[idx] + 2);
+        m.const_off = (uint32_t)ipool;
+        m.keys_off = (uint32_t)(ipool + sizeof(QConst));
+        const size_t nkeys = ((size_t)ntab << lg) + ((size_t)1 << lge);
+        m.vals_off = (uint32_t)a16z(m.keys_off + nkeys * 8);
+        ipool = a16z(m.vals_off + (size_t)ntok * sizeof(QVal));
+        if (ipool >= (size_t)UINT32_MAX) return c->fail(PF_EUNSUPP, "query images of one batch exceed 4 GB");
+        m.scr_off = scr;
+        scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 item list
+        QImageRef& r = refs[k];
+        r.const_off = m.const_off;
+        r.keys_off = m.keys_off;
+        r.vals_off = m.vals_off;
+        const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
+        r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;
+        gtab = gtab || r.lds_bytes == 0;
+        const uint32_t need = (uint32_t)sizeof(QConst) + r.lds_bytes + (kHitCap + 1) * (packed ? 4u : 8u) * 256u +
+                              4u * 256u + 2048u;
+        max_lds = std::max(max_lds, need);
+    }
+    // ---- staging: [DevJob | pool32 | pool64 | ImgJob | QImageRef | PairBlock | jix x3]
+    if (pool32.empty()) pool32.push_back(0);
+    if (pool64.empty()) pool64.push_back(0);
+    const size_t o_dj = 0;
+    const size_t o_p32 = a16z(o_dj + dj.size() * sizeof(DevJob));
+    const size_t o_p64 = a16z(o_p32 + pool32.size() * 4);
+    const size_t o_ij = a16z(o_p64 + pool64.size() * 8);
+    const size_t o_refs = a16z(o_ij + ij.size() * sizeof(ImgJob));
+    const size_t o_blk = a16z(o_refs + refs.size() * sizeof(QImageRef));
+    const size_t o_jc = a16z(o_blk + blocks.size() * sizeof(PairBlock));
+    const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
+    const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
+    const size_t total = a16z(o_jt + jix_topk.size() * 4) + 16;
+    HIPCHK(c, J.h_plan.ensure(total));
+    uint8_t* h = J.h_plan.as<uint8_t>();
+    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(h + o, src, bytes); };
+    put(o_dj, dj.data(), dj.size() * sizeof(DevJob));
+    put(o_p32, pool32.data(), pool32.size() * 4);
+    put(o_p64, pool64.data(), pool64.size() * 8);
+    put(o_ij, ij.data(), ij.size() * sizeof(ImgJob));
+    put(o_refs, refs.data(), refs.size() * sizeof(QImageRef));
+    put(o_blk, blocks.data(), blocks.size() * sizeof(PairBlock));
+    put(o_jc, jix_collab.data(), jix_collab.size() * 4);
+    put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
+    put(o_jt, jix_topk.data(), jix_topk.size() * 4);
+    HIPCHK(c, J.d_plan.ensure(total));
+    HIPCHK(c, hipMemcpyAsync(J.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
+    uint8_t* d = J.d_plan.as<uint8_t>();
+    const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
+    const int32_t* d_p32 = reinterpret_cast<const int32_t*>(d + o_p32);
+    const int64_t* d_p64 = reinterpret_cast<const int64_t*>(d + o_p64);
+    const ImgJob* d_ij = reinterpret_cast<const ImgJob*>(d + o_ij);
+    const QImageRef* d_refs = reinterpret_cast<const QImageRef*>(d + o_refs);
+    const PairBlock* d_blk = reinterpret_cast<const PairBlock*>(d + o_blk);
+    const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
+    const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
+    const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
+    // ---- workspaces
+    const size_t nE = (size_t)std::max<int64_t>(E, 1);
+    HIPCHK(c, J.d_slots.ensure(nE * 4));
+    HIPCHK(c, J.d_ids.ensure(nE * 4));
+    HIPCHK(c, J.d_fl.ensure(nE * 4));
+    HIPCHK(c, J.d_ht.ensure((size_t)std::max<int64_t>(HT, 1) * 4));
+    HIPCHK(c, J.d_seq.ensure((size_t)std::max<int64_t>(SEQ, 1) * 4));
+    HIPCHK(c, J.d_img.ensure(std::max<size_t>(ipool, 16)));
+    HIPCHK(c, J.d_scr.ensure((size_t)std::max<int64_t>(scr, 1) * 4));
+    HIPCHK(c, J.d_ncand.ensure(dj.size() * 4));
+    HIPCHK(c, J.d_keys.ensure(dj.size() * (size_t)ktop * 8));
+    HIPCHK(c, J.d_fail.ensure(16));
+    HIPCHK(c, hipMemsetAsync(J.d_fail.p, 0, 16, c->stream));
+    if (!jix_clubs.empty()) {
+        const int64_t want = (int64_t)jix_clubs.size();
+        if (want > J.acc_jobs) {
+            const size_t words = (size_t)want * (size_t)std::max(J.js.n_club_ids, 1);
+            HIPCHK(c, J.d_acc.ensure(words * 8));
+            HIPCHK(c, J.d_touched.ensure(words * 4));
+            HIPCHK(c, hipMemsetAsync(J.d_acc.p, 0, J.d_acc.cap, c->stream));
+            HIPCHK(c, hipMemsetAsync(J.d_touched.p, 0, J.d_touched.cap, c->stream));
+            J.acc_jobs = want;
+        }
+    }
+    // ---- the stages, in stream order
+    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, (int)ij.size(), J.d_img.as<uint8_t>(), J.d_scr.as<uint32_t>(),
+                             J.d_fail.as<int32_t>(), c->stream));
+    HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
+                            J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
+                            J.d_ncand.as<int32_t>(), c->stream));
+    HIPCHK(c, launch_pairs(c->ds, J.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(),
+                           J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
+    HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, J.d_fl.as<float>(),
+                            J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
+    HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, J.d_fl.as<float>(),
+                           J.d_acc.as<double>(), J.d_touched.as<int32_t>(), J.d_fl.as<float>(), J.d_ids.as<int32_t>(),
+                           J.d_ncand.as<int32_t>(), (int64_t)J.js.n_club_ids, c->stream));
+    HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), J.d_fl.as<float>(), J.d_ids.as<int32_t>(),
+                              J.d_slots.as<int32_t>(), J.d_ncand.as<int32_t>(), J.d_keys.as<uint64_t>(), ktop,
+                              c->stream));
+    // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
+    std::vector<int32_t> tpos(dj.size(), -1);
+    for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;
+    std::vector<size_t> full;  // dj indices copied whole
+    size_t ob = a16z(dj.size() * 4) + a16z(dj.size() * (size_t)ktop * 8) + 16;
+    std::vector<size_t> full_off;
+    for (size_t x = 0; x < dj.size(); ++x) {
+        if (tpos[x] >= 0) continue;
+        full.push_back(x);
+        full_off.push_back(ob);
+        ob += a16z((size_t)std::max(dj[x].cap, dj[x].kind == kDjClubs ? J.js.n_club_ids : 0) * 12);
+    }
+    HIPCHK(c, J.h_out.ensure(ob));
+    uint8_t* ho = J.h_out.as<uint8_t>();
+    const size_t o_cnt = 0, o_keys = a16z(dj.size() * 4), o_fail = o_keys + a16z(dj.size() * (size_t)ktop * 8);
+    HIPCHK(c, hipMemcpyAsync(ho + o_cnt, J.d_ncand.p, dj.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho + o_keys, J.d_keys.p, dj.size() * (size_t)ktop * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho + o_fail, J.d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
+    for (size_t q = 0; q < full.size(); ++q) {
+        const DevJob& x = dj[full[q]];
+        const size_t cnt = (size_t)std::max(x.cap, x.kind == kDjClubs ? J.js.n_club_ids : 0);
+        uint8_t* dst = ho + full_off[q];
+        HIPCHK(c, hipMemcpyAsync(dst, J.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, J.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, J.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (*reinterpret_cast<const int32_t*>(ho + o_fail))
+        return c->fail(PF_EINTERNAL, "device query table build did not converge");
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(ho + o_cnt);
+    const uint64_t* keys = reinterpret_cast<const uint64_t*>(ho + o_keys);
+    for (size_t x = 0; x < dj.size(); ++x) {
+        Job& jb = jobs[jmap[x]];
+        jb.out.clear();
+        if (tpos[x] >= 0) {
+            const uint64_t* kx = keys + (size_t)x * ktop;
+            for (int q = 0; q < jb.topk && q < ktop; ++q) {
+                if (kx[q] == ~0ull) break;
+                jb.out.emplace_back(key_uid(kx[q]), key_score(kx[q]));
+            }
+        }
+    }
+    for (size_t q = 0; q < full.size(); ++q) {
+        const size_t x = full[q];
+        const DevJob& dx = dj[x];
+        const size_t cntx = (size_t)std::max(dx.cap, dx.kind == kDjClubs ? J.js.n_club_ids : 0);
+        const uint8_t* src = ho + full_off[q];
+        const float* sc = reinterpret_cast<const float*>(src);
+        const int32_t* id = reinterpret_cast<const int32_t*>(src + cntx * 4);
+        const int32_t* sl = reinterpret_cast<const int32_t*>(src + cntx * 8);
+        if (dx.kind == kDjRawGraph || dx.kind == kDjRawCollab) {
+            auto& v = (*raw_out)[jmap[x]];
+            v.assign(id, id + cnt[x]);
+            continue;
+        }
+        Job& jb = jobs[jmap[x]];
+        Ranked r;
+        if (dx.kind == kDjClubs) {
+            for (int32_t k = 0; k < cnt[x]; ++k) r.emplace_back(id[k], sc[k]);
+        } else {
+            for (size_t k = 0; k < cntx; ++k)
+                if (sl[k] >= 0) r.emplace_back(id[k], sc[k]);
+        }
+        rank(r, jb.topk);
+        jb.out = std::move(r);
+    }
+    return PF_OK;
+}
+
+int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector<int32_t>>* raw_out) {
+    auto& J = c->jb;
+    if (!J.ok) return c->fail(PF_EUNSUPP, "device job pipeline unavailable: " + J.why);
+    (void)hipSetDevice(c->device);
+    for (Job& jb : jobs) jb.out.clear();
+    if (jobs.empty()) return PF_OK;
+    int rc = sync_nodes(c);
+    if (rc != PF_OK) return rc;
+    const std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>>* over = nullptr;
+    for (const Job& jb : jobs) {
+        if (jb.view.over && over && jb.view.over != over)
+            return c->fail(PF_EINTERNAL, "one call mixes two versioned adjacency edit sets");
+        if (jb.view.over) over = jb.view.over;
+    }
+    rc = sync_view(c, over);
+    if (rc != PF_OK) return rc;
+    HpLap hl;
+    std::vector<JP> P(jobs.size());
+    par_jobs(jobs.size(), [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 16);
+    hl.lap(kHpPrep);
+    size_t b = 0;
+    while (b < jobs.size()) {
+        size_t e = b;
+        int64_t el = 0, ht = 0;
+        while (e < jobs.size()) {
+            const JP& p = P[e];
+            if (e > b && (el + p.elems > kChunkElems || ht + p.ht_words > kChunkHt)) break;
+            el += p.elems;
+            ht += p.ht_words;
+            ++e;
+        }
+        rc = run_chunk(c, jobs, P, b, e, raw_out);
+        if (rc != PF_OK) return rc;
+        b = e;
+    }
+    hl.lap(kHpGpu);
+    return PF_OK;
+}
+
+}  // namespace
+
+int run_jobs(pf_ctx* c, std::vector<Job>& jobs) { return run_all(c, jobs, false, nullptr); }
+
+int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out) {
+    std::vector<Job> jobs(1);
+    jobs[0].uid = uid;
+    jobs[0].limit = limit;
+    jobs[0].limit_flavour = flavour;
+    jobs[0].topk = INT32_MAX;
+    jobs[0].view.base = &c->hc.adj;
+    std::vector<std::vector<int32_t>> raw(1);
+    const int rc = run_all(c, jobs, true, &raw);
+    out = std::move(raw[0]);
+    return rc;
+}
+
+}  // namespace pf

@@ -6,9 +6,10 @@
 
 namespace pf {
 
-// one 256-thread block of the pair kernel: pairs [begin, begin+count) of query image qimg
+// one 256-thread block of the pair kernel: FAS(image qimg, slots[begin + i]) -> out[out + i]
+// for i < count; a slot < 0 is skipped (its output is not written)
 struct PairBlock {
-    int32_t qimg, begin, count, pad;
+    int32_t qimg, begin, count, out;
 };
 
 // lds: dynamic LDS bytes per block = max over the batch of

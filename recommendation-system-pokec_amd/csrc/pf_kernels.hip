@@ -21,97 +21,13 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "pf_device.h"
 #include "pf_kernels.h"
 
 namespace pf {
 
 static_assert(sizeof(QConst) % 16 == 0, "QConst must keep the LDS carve 16-B aligned");
 static_assert(sizeof(QVal) == 16, "QVal is one 16-B load");
-
-// ---------------------------------------------------------------- arithmetic
-// recommender_similarity.cpp:18-26 — both branches evaluate exp(-|x|)
-__device__ __forceinline__ double dev_sigmoid(double x) {
-    const bool pos = x >= 0.0;
-    const double e = exp(pos ? -x : x);
-    return (pos ? 1.0 : e) / (1.0 + e);
-}
-
-__device__ __forceinline__ bool zmode_of(const QConst& q, int slot) {
-    if (slot < kNumFixed) return (q.zmode_fx >> slot) & 1u;
-    const int t = slot - kNumFixed;
-    return t < 32 ? ((q.zmode_lo >> t) & 1u) : ((q.zmode_hi >> (t - 32)) & 1u);
-}
-
-// recommender_similarity.cpp:28-36,105-111
-__device__ __forceinline__ double term_of(const QConst& q, int slot, double s) {
-    const double z = zmode_of(q, slot) ? (s - q.zmean[slot]) / q.zsd[slot] : 6.0 * (s - 0.5);
-    return dev_sigmoid(z);
-}
-
-// recommender.cpp:119-128: inter counted over B (with duplicates) / (sqrt|A| sqrt|B|), as float
-__device__ __forceinline__ double set_term(const QConst& q, int slot, int inter, int nb, double sqrt_na) {
-    const double den = sqrt_na * sqrt((double)nb);
-    const double s = den <= 0.0 ? 0.0 : (double)(float)((double)inter / den);
-    return term_of(q, slot, s);
-}
-
-// recommender.cpp:114-116: (float)(dot / (sqrt(na) * sqrt(nb)))
-__device__ __forceinline__ double text_term(const QConst& q, int t, double dot, double sqrt_nb) {
-    const double den = q.sqrt_na[t] * sqrt_nb;
-    const double s = den <= 0.0 ? 0.0 : (double)(float)(dot / den);
-    return term_of(q, kNumFixed + t, s);
-}
-
-// completion / age ratio outside the host table (recommender_similarity.cpp:40-53)
-__device__ __forceinline__ double ratio_term(const QConst& q, int slot, int a, int b) {
-    const int lo = a < b ? a : b, hi = a < b ? b : a;
-    return term_of(q, slot, (double)lo / (double)hi);
-}
-
-// ---------------------------------------------------------------- query hash (cuckoo)
-struct QView {
-    const QConst* q;
-    const uint2* tab;  // packed: T | T3;  wide: T0 | T1 | T2 (2^lg each) | T3 (2^lg_excl)
-    const QVal* vals;
-    void* hits;        // LDS [kHitCap + 1][blockDim.x] per-lane token-hit list
-    uint32_t* nh;      // LDS [blockDim.x] hit counts, read across the lanes of a split record
-    int lg, lge;
-    uint32_t hmul, excl_off;
-};
-
-// Wide tables: 2-choice probe of table `off` (entries), capacity 2^lg; val or kEmptyVal
-__device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, uint32_t key) {
-    const uint32_t x = cuckoo_x(key, v.hmul);
-    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
-    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
-    // a key sits in at most one of its two slots: AND-combining keeps both reads
-    // unconditional (a ?: chain lets the compiler sink the second read into a branch)
-    const uint32_t r1 = e1.x == key ? e1.y : kEmptyVal;
-    const uint32_t r2 = e2.x == key ? e2.y : kEmptyVal;
-    return r1 & r2;
-}
-
-// Packed tables: the same probe with miss = 0 (empty slots are {~0, 0})
-__device__ __forceinline__ uint32_t probe_p(const QView& v, uint32_t off, int lg, uint32_t key) {
-    const uint32_t x = cuckoo_x(key, v.hmul);
-    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
-    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
-    return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
-}
-
-template <bool PACKED>
-__device__ __forceinline__ bool excluded(const QView& v, uint32_t uid) {
-    if (PACKED) return probe_p(v, v.excl_off, v.lge, uid) != 0u;
-    return probe(v, v.excl_off, v.lge, uid) != kEmptyVal;
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t u = (uint32_t)__shfl_xor((int)v, o);
-        v = u > v ? u : v;
-    }
-    return v;
-}
 
 // Per-lane record walk state
 struct Walk {
@@ -202,47 +118,6 @@ __device__ __forceinline__ void walk_step_w(Walk& W, const uint4& cw, uint32_t j
         reinterpret_cast<uint2*>(v.hits)[slot] = make_uint2(val[i], w[i]);
         W.nh += (hit && tok[i]) ? 1u : 0u;
     }
-}
-
-// product of one shared token, recommender.cpp:74-85 (wA * wB, wB = tf * idf)
-__device__ __forceinline__ double hit_product(const QView& v, uint32_t vi, int32_t tf) {
-    const QVal qv = v.vals[vi];
-    return qv.wq * ((double)tf * qv.idf);
-}
-
-// Where a candidate lives: tile, index in the tile, lanes per record (1 << lgk)
-struct Loc {
-    int tile;
-    int cand;
-    uint32_t lgk;
-};
-
-__device__ __forceinline__ Loc loc_of(const DevStore& st, int p) {
-    Loc l;
-    l.tile = (int)st.slot_tile[p];
-    l.cand = p - (int)st.tile_slot0[l.tile];
-    l.lgk = st.tile_lgk[l.tile];
-    return l;
-}
-
-__device__ __forceinline__ double col_norm(const DevStore& st, const Loc& l, uint64_t cmask, int t) {
-    const uint32_t r = (uint32_t)__popcll(cmask & ((1ull << t) - 1ull));
-    // [tile][candidate][rank]: a candidate's norms share cache lines, so its hit columns
-    // re-use the lines its first one brought in
-    const uint64_t base = st.norm_off[l.tile], mr = (st.norm_off[l.tile + 1] - base) >> 6;
-    return st.norms[base + (uint64_t)l.cand * mr + r];
-}
-
-// word j of a candidate's record (chunk j / q in lane cand * k + j / q)
-__device__ __forceinline__ uint32_t word_at(const DevStore& st, const Loc& l, uint32_t q, uint32_t j) {
-    const uint32_t c = j / q, o = j - c * q;
-    const uint32_t lane = ((uint32_t)l.cand << l.lgk) + c;
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(st.stream + st.tile_off[l.tile]);
-    return base[((size_t)(o >> 2) * kTileSlots + lane) * 4 + (o & 3)];
-}
-
-__device__ __forceinline__ uint32_t record_words(const uint4& h2, bool packed) {
-    return h2.y + h2.z + (packed ? h2.w : 2 * h2.w);
 }
 
 // Text terms of a candidate whose hit list overflowed: re-walk its token words from
@@ -448,68 +323,6 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     if (!active) return 0.0f;
     const uint32_t nh = W.nh;
     return fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
-}
-
-// ---------------------------------------------------------------- wave top-k
-__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// ascending bitonic sort of one key per lane across the wave
-__device__ __forceinline__ uint64_t wave_sort64(uint64_t x, int lane) {
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t y = shfl_xor64(x, j);
-            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
-        }
-    }
-    return x;
-}
-
-// The wave keeps the 64 smallest keys seen so far, sorted ascending across lanes
-// (lane i = i-th best); a top-k caller reads lanes < k.  Few qualifying keys are
-// inserted one by one; many are merged with a bitonic sort + merge (O(log^2 64)).
-__device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int lane) {
-    uint64_t thr = rdlane64(list, k - 1);
-    uint64_t m = __ballot(x < thr);
-    if (!m) return;
-    if (__popcll(m) > 3) {
-        uint64_t xs = wave_sort64(x < thr ? x : ~0ull, lane);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)xs, 63 - lane);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(xs >> 32), 63 - lane);
-        const uint64_t rev = ((uint64_t)hi << 32) | lo;
-        uint64_t y = list < rev ? list : rev;  // bitonic: the 64 smallest of both lists
-#pragma unroll
-        for (int j = 32; j > 0; j >>= 1) {
-            const uint64_t z = shfl_xor64(y, j);
-            y = (lane & j) ? (y < z ? z : y) : (y < z ? y : z);
-        }
-        list = y;
-        return;
-    }
-    while (m) {
-        const int src = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        const uint64_t y = rdlane64(x, src);
-        if (y < thr) {
-            const int pos = __popcll(__ballot(list < y));
-            const uint64_t up = __shfl_up(list, 1);
-            if (lane > pos) list = up;
-            if (lane == pos) list = y;
-            thr = rdlane64(list, k - 1);
-        }
-    }
 }
 
 // ---------------------------------------------------------------- LDS staging
@@ -1259,10 +1072,11 @@ __global__ __launch_bounds__(256) void fas_pairs_kernel(DevStore st, const uint8
     char* scratch;
     const QView v = stage_query<GTAB>(smem, pool, refs[b.qimg], &scratch);
     const int i = (int)threadIdx.x;
-    const bool active = i < b.count;
-    const int p = active ? slots[b.begin + i] : 0;
+    int p = i < b.count ? slots[b.begin + i] : -1;
+    const bool active = p >= 0;
+    if (!active) p = 0;
     const float f = fas_slot<PACKED>(st, v, p, active);
-    if (active) out[b.begin + i] = f;
+    if (active) out[b.out + i] = f;
 }
 
 // ---------------------------------------------------------------- K4: collaborative sum

@@ -361,17 +361,27 @@ bool cuckoo_fill(uint64_t* tab, int lg, uint32_t hmul, const std::vector<uint64_
     return true;
 }
 
+}  // namespace
+
 int lg_for(size_t n) {
     int lg = 4;
     while (((size_t)1 << lg) * 2 < n * 5) ++lg;  // load factor <= 0.4
     return lg;
 }
 
+// The A side's constants (recommender_similarity.cpp:10-124), in three parts the device image
+// builder (pf_jobs.hip K6) shares bit for bit: the query-independent fields (normaliser modes,
+// s = 0 terms, equality terms), the region row per a_regcnt and the completion / age rows per
+// query value, all glibc-exp sigmoid values.
+namespace {
+double zval(const HostCorpus& hc, int slot, double s) {
+    if (hc.npres[slot] && hc.nsd[slot] > 0.0f) return (s - (double)hc.nmean[slot]) / (double)hc.nsd[slot];
+    return 6.0 * (s - 0.5);
+}
+double term(const HostCorpus& hc, int slot, double s) { return ref_sigmoid(zval(hc, slot, s)); }
 }  // namespace
 
-// The A side's constants: normaliser modes, glibc-exp sigmoid tables, s = 0 terms,
-// column mask and sqrt(na) per column (recommender_similarity.cpp:10-124).
-static void fill_qconst(const HostCorpus& hc, int32_t i, QConst& c) {
+void qconst_template(const HostCorpus& hc, bool packed, QConst& c) {
     const int T = hc.T;
     std::memset(&c, 0, sizeof c);
     c.n_cols = T;
@@ -386,12 +396,37 @@ static void fill_qconst(const HostCorpus& hc, int32_t i, QConst& c) {
             else c.zmode_hi |= 1u << (k - kNumFixed - 32);
         }
     }
-    auto zval = [&](int slot, double s) -> double {
-        if (hc.npres[slot] && hc.nsd[slot] > 0.0f) return (s - (double)hc.nmean[slot]) / (double)hc.nsd[slot];
-        return 6.0 * (s - 0.5);
-    };
-    auto term = [&](int slot, double s) { return ref_sigmoid(zval(slot, s)); };
+    for (int e = 0; e < 2; ++e) {
+        c.sig_pub[e] = term(hc, PF_F_PUBLIC, e ? 1.0 : 0.0);
+        c.sig_gen[e] = term(hc, PF_F_GENDER, e ? 1.0 : 0.0);
+    }
+    c.sig0_clubs = term(hc, PF_F_CLUBS, 0.0);
+    c.sig0_friends = term(hc, PF_F_FRIENDS, 0.0);
+    for (int t = 0; t < T; ++t) c.sig0_col[t] = term(hc, kNumFixed + t, 0.0);
+    c.n_hits_max = (kHitCap + 1) * (packed ? 4u : 8u);  // + the dump slot
+}
 
+void qconst_sig_reg(const HostCorpus& hc, int a_regcnt, double out[4][4]) {
+    for (int b = 0; b < 4; ++b)
+        for (int m = 0; m < 4; ++m) out[b][m] = 0.0;
+    if (a_regcnt <= 0) return;
+    for (int b = 1; b <= 3; ++b)
+        for (int m = 0; m <= 3; ++m) {
+            // recommender.cpp:130-139, cast to float then back to double
+            double s = (double)(float)((double)m / (std::sqrt((double)a_regcnt) * std::sqrt((double)b)));
+            out[b][m] = term(hc, PF_F_REGION, s);
+        }
+}
+
+void qconst_ratio_row(const HostCorpus& hc, int slot, int a, double* out) {
+    out[0] = 0.0;
+    for (int v = 1; v <= kValTab; ++v)
+        out[v] = a > 0 ? term(hc, slot, (double)std::min(a, v) / (double)std::max(a, v)) : 0.0;
+}
+
+static void fill_qconst(const HostCorpus& hc, bool packed, int32_t i, QConst& c) {
+    const int T = hc.T;
+    qconst_template(hc, packed, c);
     c.pubcode = hc.pub[i] < 0 ? kCodeMissing : hc.pub_code.at(hc.pub[i]);
     c.gencode = hc.gen[i] < 0 ? kCodeMissing : hc.gen_code.at(hc.gen[i]);
     c.comp = hc.comp[i];
@@ -402,27 +437,12 @@ static void fill_qconst(const HostCorpus& hc, int32_t i, QConst& c) {
     c.n_friends = (int32_t)(hc.friend_off[i + 1] - hc.friend_off[i]);
     c.sqrt_clubs = std::sqrt((double)c.n_clubs);
     c.sqrt_friends = std::sqrt((double)c.n_friends);
-    for (int e = 0; e < 2; ++e) {
-        c.sig_pub[e] = term(PF_F_PUBLIC, e ? 1.0 : 0.0);
-        c.sig_gen[e] = term(PF_F_GENDER, e ? 1.0 : 0.0);
-    }
-    if (c.a_regcnt > 0)
-        for (int b = 1; b <= 3; ++b)
-            for (int m = 0; m <= 3; ++m) {
-                // recommender.cpp:130-139, cast to float then back to double
-                double s = (double)(float)((double)m / (std::sqrt((double)c.a_regcnt) * std::sqrt((double)b)));
-                c.sig_reg[b][m] = term(PF_F_REGION, s);
-            }
-    for (int v = 1; v <= kValTab; ++v) {
-        if (c.comp > 0) c.sig_comp[v] = term(PF_F_COMPLETION, (double)std::min(c.comp, v) / (double)std::max(c.comp, v));
-        if (c.age > 0) c.sig_age[v] = term(PF_F_AGE, (double)std::min(c.age, v) / (double)std::max(c.age, v));
-    }
-    c.sig0_clubs = term(PF_F_CLUBS, 0.0);
-    c.sig0_friends = term(PF_F_FRIENDS, 0.0);
+    qconst_sig_reg(hc, c.a_regcnt, c.sig_reg);
+    qconst_ratio_row(hc, PF_F_COMPLETION, c.comp, c.sig_comp);
+    qconst_ratio_row(hc, PF_F_AGE, c.age, c.sig_age);
     c.colmask = 0;
     for (int t = 0; t < T; ++t) {
         const size_t r = (size_t)i * T + t;
-        c.sig0_col[t] = term(kNumFixed + t, 0.0);
         c.sqrt_na[t] = hc.sqrt_nb[r];
         if (hc.tok_off[r + 1] != hc.tok_off[r]) c.colmask |= 1ull << t;
     }
@@ -431,7 +451,7 @@ static void fill_qconst(const HostCorpus& hc, int32_t i, QConst& c) {
 bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector<int32_t>* excl, QImageHost& out) {
     const int T = hc.T;
     QConst& c = out.c;
-    fill_qconst(hc, i, c);
+    fill_qconst(hc, packed, i, c);
     // hash items: distinct clubs (T0), distinct friends (T1), (column, token) weights (T2),
     // exclusions (T3); packed corpora merge T0..T2 into one tagged table (pf_types.h)
     std::vector<uint64_t> items[4];
@@ -460,7 +480,6 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
             out.vals.push_back(v);
         }
     }
-    c.n_hits_max = (kHitCap + 1) * (packed ? 4u : 8u);  // + the dump slot
     if (excl) {
         tmp.assign(excl->begin(), excl->end());
         std::sort(tmp.begin(), tmp.end());
@@ -707,7 +726,7 @@ void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const
                       std::vector<uint8_t>& img) {
     const int T = hc.T;
     QConst c;
-    fill_qconst(hc, i, c);
+    fill_qconst(hc, true, i, c);
     std::vector<QTok> toks;
     std::vector<QCol> cols;
     for (int t = 0; t < T; ++t) {

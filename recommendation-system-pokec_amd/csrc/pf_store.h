@@ -83,4 +83,13 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t idx, const std::vect
 // exact reference arithmetic on the host (glibc exp)
 double ref_sigmoid(double x);
 
+// QConst in parts (pf_store.cpp fill_qconst; the device image builder K6 assembles the same):
+// the query-independent fields, the region row of a query with a_regcnt parts, and the
+// completion / age row [kValTab + 1] of query value a (zeros when a <= 0)
+void qconst_template(const HostCorpus& hc, bool packed, QConst& c);
+void qconst_sig_reg(const HostCorpus& hc, int a_regcnt, double out[4][4]);
+void qconst_ratio_row(const HostCorpus& hc, int slot, int a, double* out);
+// cuckoo table log2 for n items (load <= 0.4)
+int lg_for(size_t n);
+
 }  // namespace pf

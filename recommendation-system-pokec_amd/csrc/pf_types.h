@@ -217,4 +217,83 @@ struct PostStore {
     int32_t bsize;            // candidates per block (<= kBlockCands), chosen so the blocks fill whole waves of resident workgroups
 };
 
+
+// ---------------------------------------------------------------- device job pipeline (K3, K6-K8)
+// The reference's recommenders (recommender_graph.cpp:10-237, recommender_clubs.cpp:10-73) run
+// as device stages over a batch of jobs: K3 gathers each job's ordered 2-hop candidates on the
+// CSR adjacency, K6 builds the query images of the job's users, K1' scores every pair, K4'
+// sums the collaborative scores, K7 accumulates club scores in the reference's loop order, K8
+// keeps each job's top-k.  The host plans sizes (1-hop only) and never walks the 2-hop graph.
+enum DevJobKind {
+    kDjInterest = 0,   // recommend_graph_registration / by_interest: gather_candidates_local, filtered
+    kDjCollab = 1,     // recommend_collaborative
+    kDjClubs = 2,      // recommend_clubs_collab
+    kDjAll = 3,        // every candidate (interest, top-k beyond the scan kernels' bound)
+    kDjRawGraph = 4,   // pf_fof_candidates, PF_FOF_GRAPH (uids of the raw list)
+    kDjRawCollab = 5,  // pf_fof_candidates, PF_FOF_COLLAB
+};
+
+// Graph nodes: 0 .. n-1 are the profiles (node = candidate idx), n .. M-1 the uids of
+// adj_list without a profile.  Rows are adj_list's, in its order, as node ids.
+struct DevJobsStore {
+    // query-image inputs (K6)
+    const QConst* tmpl;         // the query-independent QConst fields
+    const double* sig_reg;      // [a_regcnt 4][b 4][m 4]
+    const int32_t* comp_vals;   // sorted distinct completion values > 0 ...
+    const double* comp_rows;    // ... and their sig_comp rows [kValTab + 1]
+    const int32_t* age_vals;
+    const double* age_rows;
+    int32_t n_comp, n_age;
+    const int64_t* idf_off;     // [T + 1] per column: sorted tids and their float idf
+    const int32_t* idf_tid;
+    const float* idf_val;
+    const uint8_t* has_idf;     // [T]
+    const int32_t* slot_of;     // [n] idx -> tile-store slot
+    // graph
+    const int64_t* g_off;       // [M] row start in g_nbr
+    const int32_t* g_len;       // [M] row length, -1 = no adj_list row
+    const int32_t* g_nbr;
+    const int32_t* g_uid;       // [M]
+    int32_t n, M;
+    // clubs (K7): per profile idx its clubs as dense club indices, in profile order
+    const int64_t* club_off;    // [n + 1]
+    const int32_t* club_dense;
+    const int32_t* club_id;     // [n_club_ids] dense index -> club id
+    int32_t n_club_ids, pad;
+};
+
+// Row overrides one call sees, sorted by (node asc, version desc): pf_set_adj edits (version
+// INT32_MIN: always visible) and the batched drivers' versioned edits (visible to jobs whose
+// version is >= theirs).  len -1 = the row is erased.
+struct DevView {
+    const int32_t* node;
+    const int32_t* ver;
+    const int64_t* off;         // into nbr
+    const int32_t* len;
+    const int32_t* nbr;
+    int32_t n, pad;
+};
+
+// One job of a batch (host-planned; every offset is into the batch's workspaces).
+struct DevJob {
+    int32_t kind, u, L, version;       // u = query node; L = max(limit, 1)
+    int32_t own, own_len;              // own row override (node or -1), its length (-1 = erased)
+    int64_t own_off;                   // own row's nodes in the plan's int32 pool
+    int64_t f_off;                     // row(u) as nodes in the plan's int32 pool
+    int32_t nf;                        // |row(u)|
+    int32_t ht_lg;                     // gather hash-table capacity log2
+    int64_t ht_off;                    // keys | pos | flags (3 << ht_lg int32) in the hash workspace
+    int64_t seg_off;                   // per friend: prefix (nf + 1) int32 in the seq workspace
+    int64_t cand_off;                  // candidate slots / ids (cap entries) in the slot / id arrays
+    int32_t cap;                       // candidate region size
+    int32_t nfd;                       // distinct friends with a profile (collab / clubs)
+    int64_t fd_off;                    // Fd nodes (nfd) in the plan's int32 pool; then their slots
+    int64_t fpos_off;                  // per row(u) position: index into Fd or -1 (plan int32 pool)
+    int64_t sim_off;                   // pair outputs FAS(u, Fd[r]) (nfd floats)
+    int64_t m_off;                     // collab: M[r][c] (nfd x cap floats)
+    int64_t sreg_off;                  // clubs: per Fd r, the element offset of its S region (plan int64 pool)
+    int64_t out_off;                   // scored list (score float, id int32), cap entries
+    int32_t topk, pad;
+};
+
 }  // namespace pf

@@ -471,6 +471,14 @@ class Oracle:
     def idf(self, col, tid):
         return self.L.ro_idf(self.h, col, tid)
 
+    def set_adj(self, uid, nbrs):
+        """adj_list[uid] = nbrs (None erases the row), as pf_set_adj."""
+        if nbrs is None:
+            self.L.ro_set_adj(self.h, uid, None, -1)
+        else:
+            a = np.ascontiguousarray(nbrs, np.int32) if len(nbrs) else np.zeros(1, np.int32)
+            self.L.ro_set_adj(self.h, uid, a.ctypes.data, len(nbrs))
+
     def profile_order(self):
         n = self.L.ro_num_users(self.h)
         out = np.zeros(n, np.int32)

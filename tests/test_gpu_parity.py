@@ -159,6 +159,20 @@ def hub():
     return c, tl.engine(c), tl.Oracle(c)
 
 
+@pytest.fixture(scope="module")
+def hubs():
+    """The 20k-user edge-case corpus with a hub adjacency: uid 4242's adj_list row names the 60
+    highest-degree users (its 2-hop lists pass 10,000), itself, a duplicate and two uids without
+    a profile, one of which (999999) has a row of its own."""
+    base = tl.synth.Corpus(n_users=20000, seed=77, edge_cases=1)
+    c = tl.corpus_from_desc(base.desc_ptr())
+    deg = np.diff(c.adj_off)
+    top = [int(x) for x in c.adj_uid[np.argsort(-deg)[:60]]]
+    row = top[:48] + [4242, top[3], 999999, 888888] + top[48:]
+    c = tl.with_rows(c, adj={4242: row, 999999: [1, 2, 4242, 3, 2, 777777]})
+    return c, tl.engine(c), tl.Oracle(c)
+
+
 def test_heavy_query_routes_to_stream_scan(hub):
     """a query whose lists exceed K5's LDS is scored by K1 in its own launch, in the
     same call as ordinary queries (which stay on K5), and matches the oracle bit for bit."""
@@ -171,6 +185,68 @@ def test_heavy_query_routes_to_stream_scan(hub):
         assert len(g[0]) == 10, u
         assert list(g[0]) == list(r[0]), u
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def _hub_queries(c):
+    deg = np.diff(c.adj_off)
+    return [4242, 999999, 888888, 5] + [int(x) for x in c.adj_uid[np.argsort(-deg)[:3]]]
+
+
+def test_fof_gathers_hub_vs_oracle(hubs):
+    """K3 (device 2-hop gather) against the oracle on hubs: 2-hop lists far beyond the limit
+    (10,000), a row naming the user itself, duplicates, uids without a profile (one with a row of
+    its own), and a user absent from adj_list; both flavours (recommender_graph.cpp:10-31, :114-125)."""
+    c, eng, orc = hubs
+    for u in _hub_queries(c) + [123456789]:
+        for lim in (0, 1, 37, 1000, 10000, 50000):
+            for fl in (tl.PF_FOF_GRAPH, tl.PF_FOF_COLLAB):
+                got, ref = eng.fof_candidates(u, lim, fl), orc.fof(u, lim, fl)
+                assert list(got) == list(ref), (u, lim, fl, len(got), len(ref))
+    assert len(orc.fof(4242, 10000, tl.PF_FOF_COLLAB)) == 10000
+
+
+def test_hub_recommenders_vs_oracle(hubs):
+    """The device job pipeline (K3 gather, K6 images, K1' pairs, K4' sums, K7 clubs, K8 top-k)
+    against the oracle on the hub corpus: interest (FoF), collaborative and clubs, at the limits
+    the reference's callers use and beyond, top-k inside and beyond K8's 64."""
+    c, eng, orc = hubs
+    q = _hub_queries(c)
+    qc = q[:4]  # collaborative: 4242 (friends = the 60 hubs, 2-hop list > 10,000) and the edge users
+    for lim, k in ((10000, 10), (5000, 20), (1000, 100)):
+        ops = [(eng.recommend_clubs_collab, orc.clubs, q)]
+        if lim < 10000:  # the oracle's collaborative at 10,000 takes ~45 s on one core
+            ops.append((eng.recommend_collaborative, orc.collab, qc))
+        for fn_e, fn_o, qq in ops:
+            for u, g, r in zip(qq, fn_e(qq, k, lim), fn_o(qq, k, lim)):
+                assert list(g[0]) == list(r[0]), (fn_e.__name__, u, lim, k)
+                assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), (fn_e.__name__, u, lim, k)
+        got = eng.recommend_interest(q, k, tl.PF_MODE_FOF, lim)
+        for u, g, r in zip(q, got, orc.interest(q, k, tl.PF_MODE_FOF, lim)):
+            assert list(g[0]) == list(r[0]), ("interest", u, lim, k)
+            assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), ("interest", u, lim, k)
+
+
+def test_set_adj_reaches_device_graph():
+    """pf_set_adj edits (a new uid, an erased row, a row naming a user without a row) are seen
+    by the device gathers and recommenders exactly as the oracle's adj_list edits."""
+    base = tl.synth.Corpus(n_users=4000, seed=13, edge_cases=1)
+    ptr = base.desc_ptr()
+    eng, orc = tl.engine(ptr), tl.Oracle(None, desc_ptr=ptr)
+    edits = [(7, [3, 9, 555555, 7, 12]), (555555, [1, 2, 3]), (12, None), (9, [])]
+    for u, row in edits:
+        eng.set_adj(u, row)
+        orc.set_adj(u, row)
+    for u in (7, 9, 12, 3, 555555):
+        for lim in (1, 50, 5000):
+            for fl in (tl.PF_FOF_GRAPH, tl.PF_FOF_COLLAB):
+                assert list(eng.fof_candidates(u, lim, fl)) == list(orc.fof(u, lim, fl)), (u, lim, fl)
+    q = [7, 9, 3, 100]
+    for g, r in zip(eng.recommend_collaborative(q, 10, 5000), orc.collab(q, 10, 5000)):
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32))
+    for g, r in zip(eng.recommend_clubs_collab(q, 10, 5000), orc.clubs(q, 10, 5000)):
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32))
+    for g, r in zip(eng.recommend_interest(q, 10, tl.PF_MODE_FOF, 5000), orc.interest(q, 10, tl.PF_MODE_FOF, 5000)):
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32))
 
 
 def test_big_pairs_vs_oracle(big):

@@ -150,7 +150,7 @@ def pmc_pass(args, kernel_name):
         return None, "rocprofv3 not found"
     factor, fsrc = 2.0, "MI355X_MICROARCH.md (16-B/lane streams)"
     cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
-    if os.path.exists(cal):
+    if os.path.exists(cal) and kernel_name == "fas_post_kernel":  # 4/8-B loads; K1 / K1' read 16-B steps
         try:
             with open(cal) as f:
                 c = json.load(f)
@@ -186,6 +186,129 @@ def pmc_pass(args, kernel_name):
         shutil.rmtree(d, ignore_errors=True)
 
 
+CFG3_QUERIES = 64      # cfg 3 step: a batch of seeded query users
+CFG3_LIMIT = 10000     # recommend_collaborative's default candidate_limit (include/recommender.h)
+
+
+def cpu_baseline_collab(desc_ptr, n_queries=16):
+    """Oracle recommend_collaborative (reference algorithm, one core) over a bounded prefix of the
+    same corpus: pair-FAS/s = the oracle's profile_similarity evaluations / time, 16 seeded
+    queries with friends inside the prefix (the 16-query set for cfg 3)."""
+    import pokec_testlib as tl
+    t0 = time.time()
+    orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=desc_ptr)
+    build_s = time.time() - t0
+    rng = np.random.default_rng(44)
+    per, calls, el = [], 0, 0.0
+    tried = 0
+    while len(per) < n_queries and tried < 2000:
+        tried += 1
+        q = int(rng.integers(1, SAMPLE_USERS + 1))
+        orc.fas_calls(True)
+        t = time.perf_counter()
+        orc.collab([q], TOPK, CFG3_LIMIT)
+        dt = time.perf_counter() - t
+        nc = orc.fas_calls(True)
+        if nc == 0:  # no friend with a profile inside the prefix
+            continue
+        per.append(nc / dt)
+        calls += nc
+        el += dt
+    orc.close()
+    return {"value": calls / el if el > 0 else None, "unit": "pair-FAS/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(), "median_query_rate": float(np.median(per)) if per else None,
+            "queries": len(per), "fas_calls": calls,
+            "sample": f"{len(per)} recommend_collaborative(u, 10, {CFG3_LIMIT}) queries over the first {SAMPLE_USERS} "
+                      f"users of the same corpus (oracle/refcpu.cpp -O3, one core; profile_similarity calls counted "
+                      f"by the oracle, {el:.1f}s timed, {build_s:.1f}s map build untimed)"}
+
+
+def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s):
+    """cfg 3 (BASELINE configs[2]): collaborative FoF propagation top-10 on the full corpus.  A
+    step = recommend_collaborative(u, 10, 10000) for a batch of 64 seeded users (this rank's share
+    of them at N > 1: query users split, strong scaling), through the device job pipeline
+    (K3 gather, K6 images, K1' pairs, K4' sums, K8 top-k) and back to the host.  value =
+    FAS pairs scored / s (SURVEY D3's cfg-3 unit, |F| + |F|.|C| per user)."""
+    Q = CFG3_QUERIES
+    steps, warm = args.steps, args.warmup
+    rng = np.random.default_rng(4)
+    qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
+    mine = [qs[rank::world] for qs in qstream]
+    for i in range(warm):
+        eng.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    eng.jobs_stats_reset(True)
+    t0 = time.perf_counter()
+    nres = 0
+    for i in range(warm, warm + steps):
+        out = eng.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
+        nres += sum(len(o[0]) for o in out)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.jobs_stats()
+    eng.jobs_stats_reset(False)
+    pairs, cands = st["pairs"], st["candidates"]
+    if dist:
+        t = torch.tensor([elapsed, pairs, cands], dtype=torch.float64, device="cuda")
+        tm = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        pairs, cands, elapsed = float(t[1]), float(t[2]), float(tm.item())
+    value = pairs / elapsed
+    ms = st["pair_ms"]
+    launches = st["pair_launches"]
+    avg_ms = ms / launches if launches else None
+    phys = (st["pair_record_bytes"] + st["pair_image_bytes"]) / launches if launches else None
+
+    def rate(b):
+        return None if (b is None or not avg_ms) else b / (avg_ms * 1e-3) / 1e9
+
+    achieved = rate(phys)
+    alg_pl = st["pair_alg_bytes"] / launches if launches else None
+    traffic = pmc["bytes_per_launch"] if pmc else None
+    rec = {
+        "metric": METRIC, "value": value, "unit": "pair-FAS/s", "n_gpus": world, "steps": steps, "warmup": warm,
+        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
+        "config": {"workload": f"cfg3: collaborative FoF top-10 on the full {args.users}-user corpus, {Q} query users "
+                               f"per step (limit {CFG3_LIMIT})" + (f", split over {world} GPUs" if world > 1 else ""),
+                   "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{Q}_limit{CFG3_LIMIT}_world{world}",
+                   "n_users": args.users, "queries_per_step": Q, "topk": TOPK, "limit": CFG3_LIMIT,
+                   "parallelism": f"query-users x{world}"},
+        "candidates_per_s": cands / elapsed, "queries_per_s": Q * steps / elapsed,
+        "pairs_per_step": pairs / steps, "candidates_per_step": cands / steps, "results": nres,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "fas_pairs_kernel", "avg_launch_ms": avg_ms, "timed_launches": launches,
+                     "bytes_per_launch": phys,
+                     "bytes_model": "pf_jobs_stats: per scored pair the candidate's 48-B tile-store headers + record "
+                                    "words (K1' walks the record), per 256-pair block the staged query image",
+                     "dram_gbs": rate(traffic),
+                     "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
+                     "traffic_source": pmc if pmc else pmc_err,
+                     "alg_effective_gbs": rate(alg_pl),
+                     "alg_effective_frac": None if rate(alg_pl) is None else rate(alg_pl) / HBM_PEAK_GBS,
+                     "alg_bytes_per_launch": alg_pl,
+                     "pair_kernel_share_of_step": (ms / (elapsed * 1e3)) if elapsed > 0 else None},
+        "open_s": open_s,
+    }
+    if rank == 0 and world == 1 and base is not None:
+        rec["cpu_baseline"] = base
+        rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None
+    elif rank == 0:
+        rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -193,8 +316,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
-    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default=None,
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default=None,
                     help="cfg2: N queries per step (1 per GPU, weak scaling; the default at N = 1); "
+                         "cfg3: collaborative FoF top-10, 64 queries per step (limit 10000), query users "
+                         "split over the ranks; "
                          "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong "
                          "scaling; the default at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,10 +346,12 @@ def main():
     # rank 0 at N = 1, before this process touches the GPU: the CPU baseline (its all-cores part
     # forks oracle workers) and the rocprofv3 PMC pass (a child running this same command)
     want_kernel = "fas_scan_kernel" if args.scan_kernel == "stream" else "fas_post_kernel"
+    if args.workload == "cfg3":
+        want_kernel = "fas_pairs_kernel"
     base, pmc, pmc_err = None, None, "not run (N > 1 or --no-pmc)"
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
-            base = cpu_baseline(desc)
+            base = cpu_baseline_collab(desc) if args.workload == "cfg3" else cpu_baseline(desc)
         if not args.no_pmc:
             pmc, pmc_err = pmc_pass(args, want_kernel)
             if pmc_err:
@@ -242,6 +369,8 @@ def main():
     t2 = time.time()
     eng = pf.FasEngine(desc, local)
     t3 = time.time()
+    if args.workload == "cfg3":
+        return run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, t3 - t2)
     eng.set_shard(rank, world)
     eng.set_scan_kernel({"auto": pf.PF_SCAN_AUTO, "stream": pf.PF_SCAN_STREAM, "postings": pf.PF_SCAN_POSTINGS}
                         [args.scan_kernel])

@@ -241,6 +241,22 @@ int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
  * workgroup stages its query's image once per block.) */
 int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* out_bytes);
 
+/* Statistics of the recommenders' device job pipeline (pf_recommend_collab / _clubs /
+ * _interest FoF and the batched drivers) since pf_jobs_stats_reset(ctx, 1): jobs run,
+ * candidate-list entries scored, FAS pairs scored by the pair kernel (K1'), their
+ * SURVEY 8(d) D3 bytes (b_c of each pair's candidate), the tile-store bytes the kernel
+ * reads for them (48-B headers + record words), the staged query-image bytes (one image
+ * per 256-pair block), and the pair kernel's device time (HIP events around each launch)
+ * and launch count.  enable = 0 stops the counting (and the events). */
+typedef struct pf_jobs_stats {
+    int64_t jobs, candidates, pairs;
+    int64_t pair_alg_bytes, pair_record_bytes, pair_image_bytes;
+    double  pair_ms;
+    int64_t pair_launches;
+} pf_jobs_stats;
+int pf_jobs_stats_reset(pf_ctx* ctx, int32_t enable);
+int pf_jobs_stats_read(pf_ctx* ctx, pf_jobs_stats* out);
+
 /* Device time (ms) of the last all-candidates scan kernel (HIP events on the
  * stream it was launched on). */
 float pf_last_scan_ms(const pf_ctx* ctx);

@@ -46,6 +46,7 @@ struct ro_ctx {
     std::vector<char> has_idf;
     std::vector<char> npres;
     std::vector<float> nmean, nsd;
+    mutable int64_t fas_calls = 0;  // profile_similarity evaluations (bench pair counts)
 
     // --- A10 helpers -------------------------------------------------------
     static double logistic(double x) {            // recommender_similarity.cpp:18-26
@@ -126,6 +127,7 @@ struct ro_ctx {
 
     // recommender_similarity.cpp:10-124
     float fas(const Prof& A, const Prof& B) const {
+        ++fas_calls;
         const int possible = PF_NUM_FIXED + T;
         int used = 0;
         double acc = 0.0;
@@ -394,6 +396,11 @@ int ro_open(const pf_corpus_desc* d, int32_t max_users, ro_ctx** out) {
 }
 
 void ro_close(ro_ctx* h) { delete h; }
+int64_t ro_fas_calls(ro_ctx* h, int reset) {
+    const int64_t n = h->fas_calls;
+    if (reset) h->fas_calls = 0;
+    return n;
+}
 int32_t ro_num_users(const ro_ctx* h) { return (int32_t)h->prof.size(); }
 
 float ro_idf(const ro_ctx* h, int32_t col, int32_t tid) {

@@ -21,6 +21,8 @@ typedef struct ro_ctx ro_ctx;
 /* max_users > 0 keeps only the first max_users profiles of desc (bounded CPU samples) */
 int   ro_open(const pf_corpus_desc* d, int32_t max_users, ro_ctx** out);
 void  ro_close(ro_ctx* h);
+/* profile_similarity evaluations since the last reset (reset != 0 zeroes the count) */
+int64_t ro_fas_calls(ro_ctx* h, int reset);
 int32_t ro_num_users(const ro_ctx* h);
 float ro_idf(const ro_ctx* h, int32_t col, int32_t tid);
 int   ro_fas_pairs(ro_ctx* h, const int32_t* a, const int32_t* b, int64_t n, float* out);

@@ -839,6 +839,9 @@ int pf_merge_keys_async(pf_ctx* c, const uint64_t* d_parts, int32_t nparts, int3
     return PF_OK;
 }
 
+int pf_jobs_stats_reset(pf_ctx* c, int32_t enable) { return c ? pf::jobs_stats_reset(c, enable) : PF_EINVAL; }
+int pf_jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) { return (c && o) ? pf::jobs_stats_read(c, o) : PF_EINVAL; }
+
 int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     if (!c || nq < 0 || (nq && (!q || !out))) return PF_EINVAL;
     (void)hipSetDevice(c->device);

@@ -92,6 +92,12 @@ struct JobsState {
     DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr, d_ncand, d_keys, d_acc, d_touched, d_fail;
     PinBuf h_plan, h_out;
     int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
+    // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
+    bool stats_on = false;
+    DBuf d_stats;                                // 3 x u64: pairs, D3 bytes, tile-store bytes
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> stat_ev;
+    size_t stat_used = 0;
+    int64_t st_jobs = 0, st_cands = 0, st_img_bytes = 0, st_launches = 0;
 };
 
 }  // namespace pf
@@ -214,5 +220,7 @@ inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 int jobs_open(pf_ctx* c);                            // after the tile store is on the device
 void jobs_note_edit(pf_ctx* c, int32_t uid);         // pf_set_adj changed uid's row
 int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out);
+int jobs_stats_reset(pf_ctx* c, int enable);
+int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o);
 
 }  // namespace pf

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "pf_kernels.h"
 #include "pf_types.h"
 
 namespace pf {
@@ -25,6 +26,8 @@ hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int 
 hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
                         const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, int32_t* touched,
                         float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);
+hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
+                             unsigned long long* acc, hipStream_t s);
 hipError_t launch_job_topk(const DevJob* jobs, const int32_t* jix, int njobs, const float* score, const int32_t* ids,
                            const int32_t* slots, const int32_t* ncand, uint64_t* out, int k, hipStream_t s);
 

@@ -611,7 +611,46 @@ __global__ __launch_bounds__(kJobThreads) void topk_kernel(const DevJob* __restr
     }
 }
 
+// ---------------------------------------------------------------- pair statistics
+// (pf_jobs_stats) per scored pair: 1, SURVEY 8(d) D3's b_c of the candidate, and the tile-store
+// bytes K1' reads for it (48-B headers + its record words)
+template <bool PACKED>
+__global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const PairBlock* __restrict__ blocks,
+                                                         const int32_t* __restrict__ slots,
+                                                         unsigned long long* __restrict__ acc) {
+    const PairBlock b = blocks[blockIdx.x];
+    const int i = threadIdx.x;
+    unsigned long long v[3] = {0ull, 0ull, 0ull};
+    if (i < b.count) {
+        const int p = slots[b.begin + i];
+        if (p >= 0) {
+            const uint4 h2 = st.hdr2[p];
+            v[0] = 1ull;
+            v[1] = 32ull + 4ull * (h2.y + h2.z) + 8ull * h2.w;
+            v[2] = 48ull + 4ull * record_words(h2, PACKED);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long x = v[k];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, o);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), o);
+            x += ((unsigned long long)hi << 32) | lo;
+        }
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&acc[k], x);
+    }
+}
+
 // ---------------------------------------------------------------- launchers
+hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
+                             unsigned long long* acc, hipStream_t s) {
+    if (nblocks <= 0) return hipSuccess;
+    if (st.packed) hipLaunchKernelGGL(pair_stats_kernel<true>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc);
+    else hipLaunchKernelGGL(pair_stats_kernel<false>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
                          int32_t* ncand, hipStream_t s) {

@@ -609,8 +609,33 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
                             J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
                             J.d_ncand.as<int32_t>(), c->stream));
+    hipEvent_t pe0 = nullptr, pe1 = nullptr;
+    if (J.stats_on && !blocks.empty()) {
+        if (J.stat_used == J.stat_ev.size()) {
+            hipEvent_t a, b2;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b2));
+            J.stat_ev.emplace_back(a, b2);
+        }
+        pe0 = J.stat_ev[J.stat_used].first;
+        pe1 = J.stat_ev[J.stat_used].second;
+        ++J.stat_used;
+        HIPCHK(c, hipEventRecord(pe0, c->stream));
+    }
     HIPCHK(c, launch_pairs(c->ds, J.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(),
                            J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
+    if (pe1) {
+        HIPCHK(c, hipEventRecord(pe1, c->stream));
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), J.d_slots.as<int32_t>(),
+                                    J.d_stats.as<unsigned long long>(), c->stream));
+        ++J.st_launches;
+        for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
+            const QImageRef& r = refs[pb.qimg];
+            J.st_img_bytes += (int64_t)(r.vals_off - r.const_off) +
+                              (int64_t)(ij[pb.qimg].idx >= 0 ? (hc.tok_off[(size_t)(ij[pb.qimg].idx + 1) * hc.T] -
+                                                               hc.tok_off[(size_t)ij[pb.qimg].idx * hc.T]) * 16 : 0);
+        }
+    }
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, J.d_fl.as<float>(),
                             J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, J.d_fl.as<float>(),
@@ -650,6 +675,11 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     if (*reinterpret_cast<const int32_t*>(ho + o_fail))
         return c->fail(PF_EINTERNAL, "device query table build did not converge");
     const int32_t* cnt = reinterpret_cast<const int32_t*>(ho + o_cnt);
+    if (J.stats_on) {
+        J.st_jobs += (int64_t)dj.size();
+        for (size_t x = 0; x < dj.size(); ++x)
+            if (dj[x].kind == kDjInterest || dj[x].kind == kDjCollab || dj[x].kind == kDjAll) J.st_cands += cnt[x];
+    }
     const uint64_t* keys = reinterpret_cast<const uint64_t*>(ho + o_keys);
     for (size_t x = 0; x < dj.size(); ++x) {
         Job& jb = jobs[jmap[x]];
@@ -731,6 +761,45 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
 }  // namespace
 
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs) { return run_all(c, jobs, false, nullptr); }
+
+int jobs_stats_reset(pf_ctx* c, int enable) {
+    auto& J = c->jb;
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, J.d_stats.ensure(64));
+    HIPCHK(c, hipMemsetAsync(J.d_stats.p, 0, 64, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    J.stats_on = enable != 0;
+    J.stat_used = 0;
+    J.st_jobs = J.st_cands = J.st_img_bytes = J.st_launches = 0;
+    return PF_OK;
+}
+
+int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) {
+    auto& J = c->jb;
+    (void)hipSetDevice(c->device);
+    std::memset(o, 0, sizeof *o);
+    unsigned long long v[3] = {0, 0, 0};
+    if (J.d_stats.p) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(v, J.d_stats.p, sizeof v, hipMemcpyDeviceToHost));
+    }
+    double ms = 0.0;
+    for (size_t i = 0; i < J.stat_used; ++i) {
+        float t = 0.f;
+        HIPCHK(c, hipEventSynchronize(J.stat_ev[i].second));
+        HIPCHK(c, hipEventElapsedTime(&t, J.stat_ev[i].first, J.stat_ev[i].second));
+        ms += t;
+    }
+    o->jobs = J.st_jobs;
+    o->candidates = J.st_cands;
+    o->pairs = (int64_t)v[0];
+    o->pair_alg_bytes = (int64_t)v[1];
+    o->pair_record_bytes = (int64_t)v[2];
+    o->pair_image_bytes = J.st_img_bytes;
+    o->pair_ms = ms;
+    o->pair_launches = J.st_launches;
+    return PF_OK;
+}
 
 int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out) {
     std::vector<Job> jobs(1);

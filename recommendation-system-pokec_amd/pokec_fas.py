@@ -27,7 +27,7 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
            "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel",
-           "pf_scan_bytes"]
+           "pf_scan_bytes", "pf_jobs_stats_reset", "pf_jobs_stats_read"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -40,6 +40,12 @@ class PfLayoutStats(ctypes.Structure):
     _fields_ = [("n_slots", ctypes.c_int64), ("stream_bytes", ctypes.c_int64), ("header_bytes", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32),
                 ("post_bytes", ctypes.c_int64), ("scan_kernel", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class PfJobsStats(ctypes.Structure):
+    _fields_ = [("jobs", ctypes.c_int64), ("candidates", ctypes.c_int64), ("pairs", ctypes.c_int64),
+                ("pair_alg_bytes", ctypes.c_int64), ("pair_record_bytes", ctypes.c_int64),
+                ("pair_image_bytes", ctypes.c_int64), ("pair_ms", ctypes.c_double), ("pair_launches", ctypes.c_int64)]
 
 
 class PfDatasetInfo(ctypes.Structure):
@@ -92,6 +98,8 @@ def lib():
         L.pf_profile_sample.argtypes = [V, I32]
         L.pf_profile_read.argtypes = [V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64)]
         L.pf_scan_bytes.argtypes = [V, V, I32, V]
+        L.pf_jobs_stats_reset.argtypes = [V, I32]
+        L.pf_jobs_stats_read.argtypes = [V, ctypes.POINTER(PfJobsStats)]
         L.pf_dataset_load.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(V)]
         L.pf_dataset_load_cached.argtypes = [ctypes.c_char_p, I64, ctypes.c_char_p, ctypes.POINTER(I32), ctypes.POINTER(V)]
         L.pf_dataset_free.argtypes = [V]
@@ -247,6 +255,15 @@ class FasEngine:
         ms, n = ctypes.c_double(), ctypes.c_int64()
         self._check(self._L.pf_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)), "pf_profile_read")
         return ms.value, n.value
+
+    def jobs_stats_reset(self, enable=True):
+        """Start (or stop) counting the recommenders' job-pipeline statistics (pf_jobs_stats)."""
+        self._check(self._L.pf_jobs_stats_reset(self.h, 1 if enable else 0), "pf_jobs_stats_reset")
+
+    def jobs_stats(self):
+        s = PfJobsStats()
+        self._check(self._L.pf_jobs_stats_read(self.h, ctypes.byref(s)), "pf_jobs_stats_read")
+        return {k: getattr(s, k) for k, _ in PfJobsStats._fields_}
 
     def scan_bytes(self, uids):
         """Bytes the all-candidates scan kernel reads per query over this shard (pf_scan_bytes)."""

@@ -397,6 +397,8 @@ def oracle_lib():
     V, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     L.ro_open.argtypes = [V, I32, ctypes.POINTER(V)]
     L.ro_close.argtypes = [V]
+    L.ro_fas_calls.argtypes = [V, ctypes.c_int]
+    L.ro_fas_calls.restype = I64
     L.ro_num_users.argtypes = [V]
     L.ro_num_users.restype = I32
     L.ro_idf.argtypes = [V, I32, I32]
@@ -470,6 +472,10 @@ class Oracle:
 
     def idf(self, col, tid):
         return self.L.ro_idf(self.h, col, tid)
+
+    def fas_calls(self, reset=True):
+        """profile_similarity evaluations since the last reset."""
+        return int(self.L.ro_fas_calls(self.h, 1 if reset else 0))
 
     def set_adj(self, uid, nbrs):
         """adj_list[uid] = nbrs (None erases the row), as pf_set_adj."""

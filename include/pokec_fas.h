@@ -247,7 +247,9 @@ int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* ou
  * SURVEY 8(d) D3 bytes (b_c of each pair's candidate), the tile-store bytes the kernel
  * reads for them (48-B headers + record words), the staged query-image bytes (one image
  * per 256-pair block), and the pair kernel's device time (HIP events around each launch)
- * and launch count.  enable = 0 stops the counting (and the events). */
+ * and launch count.  enable: bit 0 = time the pair kernel (HIP events around each
+ * launch), bit 1 = count pairs and bytes (one extra small kernel per launch); 0 stops
+ * both.  Fields of a part that is off read 0. */
 typedef struct pf_jobs_stats {
     int64_t jobs, candidates, pairs;
     int64_t pair_alg_bytes, pair_record_bytes, pair_image_bytes;

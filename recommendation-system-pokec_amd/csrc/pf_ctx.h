@@ -77,6 +77,7 @@ struct JobsState {
     std::string why;
     DevJobsStore js{};
     DBuf d_tmpl, d_sigreg, d_comp_vals, d_comp_rows, d_age_vals, d_age_rows, d_idf_off, d_idf_tid, d_idf_val,
+        d_idf_doff, d_idf_dlen, d_idf_dense,
         d_has_idf, d_slot_of, d_goff, d_glen, d_gnbr, d_guid, d_club_off, d_club_dense, d_club_id;
     std::unordered_map<int32_t, int32_t> xnode;  // uid -> node for adj_list uids without a profile
     std::vector<int32_t> g_uid, g_len;           // host mirrors (new uids from pf_set_adj append nodes)
@@ -93,7 +94,8 @@ struct JobsState {
     PinBuf h_plan, h_out;
     int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
-    bool stats_on = false;
+    bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)
+    bool stats_count = false;                    // pair counters (bit 1)
     DBuf d_stats;                                // 3 x u64: pairs, D3 bytes, tile-store bytes
     std::vector<std::pair<hipEvent_t, hipEvent_t>> stat_ev;
     size_t stat_used = 0;

@@ -294,20 +294,29 @@ __device__ __forceinline__ int find_val(const int32_t* vals, int n, int32_t v) {
     return (lo < n && vals[lo] == v) ? lo : -1;
 }
 
-// float idf of (column t, tid) as the reference reads it (recommender.cpp:78: absent -> 1.0)
+// float idf of (column t, tid) as the reference reads it (recommender.cpp:78: absent -> 1.0):
+// one load from the column's dense table when it has one, else a bisection of its sorted tids
 __device__ __forceinline__ double idf_of(const DevJobsStore& g, int t, int32_t tid) {
     if (!g.has_idf[t]) return 1.0;
+    const int64_t d = g.idf_dense_off[t];
+    if (d >= 0) return (tid >= 0 && tid < g.idf_dense_len[t]) ? (double)g.idf_dense[d + tid] : 1.0;
     const int64_t b = g.idf_off[t];
     const int i = find_val(g.idf_tid + b, (int)(g.idf_off[t + 1] - b), tid);
     return i < 0 ? 1.0 : (double)g.idf_val[b + i];
 }
 
-// one workgroup per image: QConst | table (ntab << lg, then 2^lge exclusions) | vals
-template <bool PACKED>
+// One workgroup per image: QConst | table (ntab << lg, then 2^lge exclusions) | vals.
+// LDS = true (the common case, table + set + item list <= kImgLds): the de-duplication set, the
+// item list and the cuckoo table live in LDS (ds_ atomics) and the table is copied out at the
+// end; LDS = false (hub users): the same in global memory (the image's own table and scratch).
+constexpr uint32_t kImgLds = 48 * 1024;
+
+template <bool PACKED, bool LDS>
 __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJobsStore g, const ImgJob* __restrict__ ij,
                                                              uint8_t* __restrict__ pool, uint32_t* __restrict__ scratch,
                                                              int32_t* __restrict__ fail) {
     __shared__ int s_fail, s_nuniq;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const ImgJob I = ij[blockIdx.x];
     const int tid = threadIdx.x;
     const int p = g.slot_of[I.idx];
@@ -315,9 +324,9 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     QConst* q = reinterpret_cast<QConst*>(pool + I.const_off);
     // 1. constants: the template, then this user's fields (pf_store.cpp fill_qconst)
     {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(g.tmpl);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(q);
-        for (uint32_t i = tid; i < sizeof(QConst) / 4; i += kJobThreads) dst[i] = src[i];
+        const uint4* src = reinterpret_cast<const uint4*>(g.tmpl);
+        uint4* dst = reinterpret_cast<uint4*>(q);
+        for (uint32_t i = tid; i < sizeof(QConst) / 16; i += kJobThreads) dst[i] = src[i];
     }
     __syncthreads();
     const int32_t comp = (int32_t)h0.z, age = (int32_t)h0.w;
@@ -356,43 +365,60 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
         s_fail = 0;
         s_nuniq = 0;
     }
-    // 2. token values in record order (vi = token rank), recommender.cpp:74-85
+    // 2. the record's words once (tokens: their value entries, vi = token rank, recommender.cpp:74-85)
     const uint32_t len = record_words(h2, PACKED);
     const uint32_t qw = chunk_words(len, l.lgk, PACKED);
     const uint32_t nset = nc + nf;
+    const int lg = I.lg;
+    const uint32_t ntab = PACKED ? 1u : 3u;
+    const uint32_t tab_total = (ntab << lg) + (1u << I.lge);
+    const uint32_t dmask = (1u << I.dlg) - 1u;
+    // carve: table (8-B entries) | item list (8 B each) | set (4 B each)
+    uint64_t* tab;
+    uint64_t* items;
+    uint32_t* dset;
+    if constexpr (LDS) {
+        tab = reinterpret_cast<uint64_t*>(smem);
+        items = tab + tab_total;
+        dset = reinterpret_cast<uint32_t*>(items + nset + ntok);
+    } else {
+        tab = reinterpret_cast<uint64_t*>(pool + I.keys_off);
+        dset = scratch + I.scr_off;
+        items = reinterpret_cast<uint64_t*>(scratch + I.scr_off + (1u << I.dlg));
+    }
     QVal* vals = reinterpret_cast<QVal*>(pool + I.vals_off);
+    for (uint32_t i = tid; i <= dmask; i += kJobThreads) dset[i] = 0u;
+    __syncthreads();
     for (uint32_t k = tid; k < ntok; k += kJobThreads) {
         int t;
         int32_t tid_, tf;
+        uint64_t e;
         if (PACKED) {
             const uint32_t w = word_at(st, l, qw, nset + k);
             t = (int)((w >> kTidBits) & 63u);
             tid_ = (int32_t)(w & kTidMask);
             tf = (int32_t)(w >> 24);
+            e = make_entry(kTagTok | ((uint32_t)t << kTidBits) | (w & kTidMask), kTokVal | k | ((uint32_t)t << kTidBits));
         } else {
             tid_ = (int32_t)word_at(st, l, qw, nset + 2 * k);
             const uint32_t w = word_at(st, l, qw, nset + 2 * k + 1);
             t = (int)(w & 0xFFu);
             tf = (int32_t)w >> 8;
+            e = make_entry((uint32_t)tid_, (uint32_t)t | (k << 8)) | (2ull << 62);
         }
         const double idf = idf_of(g, t, tid_);
         QVal v;
         v.wq = (double)tf * idf;
         v.idf = idf;
         vals[k] = v;
+        items[nset + k] = e;  // tokens are distinct (column, tid) pairs
     }
-    // 3. distinct clubs / friends (a set in scratch), then every item in one list:
-    //    items [0, nuniq) sets, then tokens
-    uint32_t* dset = scratch + I.scr_off;               // 2^dlg keys (0 = empty)
-    uint64_t* items = reinterpret_cast<uint64_t*>(scratch + I.scr_off + (1u << I.dlg));
-    const uint32_t dmask = (1u << I.dlg) - 1u;
-    for (uint32_t i = tid; i <= dmask; i += kJobThreads) dset[i] = 0u;
-    __syncthreads();
+    // 3. distinct clubs / friends: a thread owns a word it claims first in the set; items
+    //    [0, nuniq) are the sets, [nset, nset + ntok) the tokens
     for (uint32_t j = tid; j < nset; j += kJobThreads) {
         const uint32_t w = word_at(st, l, qw, j);
         const bool club = j < nc;
         const uint32_t id = PACKED ? (club ? (w & ~kTagClub) : w) : w;
-        // set key: id + 1 for clubs, id + 1 with bit 31 for friends (ids < 2^31 - 1 here)
         const uint32_t key = (id + 1u) | (club ? 0u : 0x80000000u);
         uint32_t h = (node_hash((int32_t)key) >> 5) & dmask;
         bool won = false;
@@ -411,43 +437,24 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     }
     __syncthreads();
     const uint32_t nuniq = (uint32_t)s_nuniq;
-    for (uint32_t k = tid; k < ntok; k += kJobThreads) {
-        uint64_t e;
-        if (PACKED) {
-            const uint32_t w = word_at(st, l, qw, nset + k);
-            const uint32_t t = (w >> kTidBits) & 63u;
-            e = make_entry(kTagTok | (t << kTidBits) | (w & kTidMask), kTokVal | k | (t << kTidBits));
-        } else {
-            const uint32_t tid_ = word_at(st, l, qw, nset + 2 * k);
-            const uint32_t t = word_at(st, l, qw, nset + 2 * k + 1) & 0xFFu;
-            e = make_entry(tid_, t | (k << 8)) | (2ull << 62);
-        }
-        items[nuniq + k] = e;
-    }
-    __syncthreads();
     // 4. 2-choice cuckoo (pf_store.cpp cuckoo_fill): parallel insertion with atomic exchange;
     //    a chain longer than 500 kicks fails the attempt, the next multiplier is tried
-    const uint32_t nitems = nuniq + ntok;
-    const int lg = I.lg;
-    const uint32_t cap = 1u << lg;
     const uint64_t empty = PACKED ? kEmptyEntryPacked : kEmptyEntry;
-    unsigned long long* tab = reinterpret_cast<unsigned long long*>(pool + I.keys_off);
-    const uint32_t ntab = PACKED ? 1u : 3u;
-    const uint32_t tab_total = (ntab << lg) + (1u << I.lge);
     for (uint32_t s = 0; s < 16; ++s) {
         const uint32_t hmul = kHashMul + 2u * s * 0x6A09E667u;
         for (uint32_t i = tid; i < tab_total; i += kJobThreads) tab[i] = empty;
         __syncthreads();
-        for (uint32_t i = tid; i < nitems; i += kJobThreads) {
-            uint64_t cur = items[i];
+        for (uint32_t i = tid; i < nuniq + ntok; i += kJobThreads) {
+            uint64_t cur = items[i < nuniq ? i : nset + (i - nuniq)];
             const uint32_t tsel = PACKED ? 0u : (uint32_t)(cur >> 62);
             cur &= PACKED ? ~0ull : ~(3ull << 62);
-            unsigned long long* T = tab + ((size_t)tsel << lg);
+            uint64_t* T = tab + ((size_t)tsel << lg);
             uint32_t x = cuckoo_x((uint32_t)cur, hmul);
             uint32_t at = cuckoo_h1(x, lg);
             bool placed = false;
             for (int kick = 0; kick < 500; ++kick) {
-                const unsigned long long old = atomicExch(&T[at], (unsigned long long)cur);
+                const uint64_t old = (uint64_t)atomicExch(reinterpret_cast<unsigned long long*>(&T[at]),
+                                                          (unsigned long long)cur);
                 if (old == empty) { placed = true; break; }
                 cur = old;  // evicted: to its other slot
                 x = cuckoo_x((uint32_t)cur, hmul);
@@ -461,13 +468,22 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
         __syncthreads();
         if (!failed) {
             if (tid == 0) q->hmul = hmul;
+            if constexpr (LDS) {
+                uint64_t* out = reinterpret_cast<uint64_t*>(pool + I.keys_off);
+                for (uint32_t i = tid; i < tab_total; i += kJobThreads) out[i] = tab[i];
+            }
             return;
         }
         if (tid == 0) s_fail = 0;
         __syncthreads();
     }
     if (tid == 0) atomicOr(fail, 1);
-    (void)cap;
+}
+
+// LDS bytes of an image's build (table + item list + set), pf_jobs_plan.cpp splits the launch by it
+uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed) {
+    const uint64_t b = 8ull * (((uint64_t)(packed ? 1 : 3) << lg) + (1ull << lge)) + 8ull * nitems + 4ull * (1ull << dlg);
+    return b <= kImgLds ? (uint32_t)b : 0u;
 }
 
 // ---------------------------------------------------------------- K4': collaborative sums
@@ -618,6 +634,7 @@ template <bool PACKED>
 __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const PairBlock* __restrict__ blocks,
                                                          const int32_t* __restrict__ slots,
                                                          unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long red[3][4];
     const PairBlock b = blocks[blockIdx.x];
     const int i = threadIdx.x;
     unsigned long long v[3] = {0ull, 0ull, 0ull};
@@ -638,7 +655,12 @@ __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const Pair
             const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), o);
             x += ((unsigned long long)hi << 32) | lo;
         }
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&acc[k], x);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {  // one atomic per counter and block
+        const unsigned long long t = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (t) atomicAdd(&acc[threadIdx.x], t);
     }
 }
 
@@ -660,11 +682,25 @@ hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* 
     return hipGetLastError();
 }
 
-hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n, uint8_t* pool,
-                          uint32_t* scratch, int32_t* fail, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    if (st.packed) hipLaunchKernelGGL(qimage_kernel<true>, dim3(n), dim3(kJobThreads), 0, s, st, g, ij, pool, scratch, fail);
-    else hipLaunchKernelGGL(qimage_kernel<false>, dim3(n), dim3(kJobThreads), 0, s, st, g, ij, pool, scratch, fail);
+hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_lds, int n_glob,
+                          uint8_t* pool, uint32_t* scratch, int32_t* fail, hipStream_t s) {
+    // images [0, n_lds) build in LDS (kImgLds bytes each), [n_lds, n_lds + n_glob) in global memory
+    if (n_lds > 0) {
+        if (st.packed)
+            hipLaunchKernelGGL((qimage_kernel<true, true>), dim3(n_lds), dim3(kJobThreads), kImgLds, s, st, g, ij, pool,
+                               scratch, fail);
+        else
+            hipLaunchKernelGGL((qimage_kernel<false, true>), dim3(n_lds), dim3(kJobThreads), kImgLds, s, st, g, ij,
+                               pool, scratch, fail);
+    }
+    if (n_glob > 0) {
+        if (st.packed)
+            hipLaunchKernelGGL((qimage_kernel<true, false>), dim3(n_glob), dim3(kJobThreads), 0, s, st, g, ij + n_lds,
+                               pool, scratch, fail);
+        else
+            hipLaunchKernelGGL((qimage_kernel<false, false>), dim3(n_glob), dim3(kJobThreads), 0, s, st, g, ij + n_lds,
+                               pool, scratch, fail);
+    }
     return hipGetLastError();
 }
 

@@ -102,6 +102,21 @@ int jobs_open(pf_ctx* c) {
         for (auto& e : v) { idf_tid.push_back(e.first); idf_val.push_back(e.second); }
         idf_off[t + 1] = (int64_t)idf_tid.size();
     }
+    // dense idf tables where the column's tids are small and the total stays under 512 MB
+    std::vector<int64_t> dense_off(T, -1);
+    std::vector<int32_t> dense_len(T, 0);
+    std::vector<float> dense;
+    for (int t = 0; t < T; ++t) {
+        const int64_t b0 = idf_off[t], b1 = idf_off[t + 1];
+        if (!hc.has_idf[t] || b1 == b0 || idf_tid[b0] < 0 || idf_tid[b1 - 1] >= (1 << 24)) continue;
+        const int64_t len = (int64_t)idf_tid[b1 - 1] + 1;
+        if ((int64_t)dense.size() + len > (128ll << 20)) continue;
+        dense_off[t] = (int64_t)dense.size();
+        dense_len[t] = (int32_t)len;
+        dense.resize(dense.size() + (size_t)len, 1.0f);
+        for (int64_t k = b0; k < b1; ++k) dense[dense_off[t] + idf_tid[k]] = idf_val[k];
+    }
+    if (dense.empty()) dense.push_back(1.0f);
     // graph: nodes 0..n-1 = profiles (idx), then adj_list uids without a profile
     J.xnode.clear();
     J.g_uid.assign(hc.uid.begin(), hc.uid.end());
@@ -181,6 +196,9 @@ int jobs_open(pf_ctx* c) {
     if (e == hipSuccess) e = up(c, J.d_idf_off, idf_off);
     if (e == hipSuccess) e = up(c, J.d_idf_tid, idf_tid);
     if (e == hipSuccess) e = up(c, J.d_idf_val, idf_val);
+    if (e == hipSuccess) e = up(c, J.d_idf_doff, dense_off);
+    if (e == hipSuccess) e = up(c, J.d_idf_dlen, dense_len);
+    if (e == hipSuccess) e = up(c, J.d_idf_dense, dense);
     if (e == hipSuccess) e = up(c, J.d_has_idf, has_idf);
     if (e == hipSuccess) e = up(c, J.d_slot_of, slot_of);
     if (e == hipSuccess) e = up(c, J.d_goff, g_off);
@@ -204,6 +222,9 @@ int jobs_open(pf_ctx* c) {
     g.idf_off = J.d_idf_off.as<int64_t>();
     g.idf_tid = J.d_idf_tid.as<int32_t>();
     g.idf_val = J.d_idf_val.as<float>();
+    g.idf_dense_off = J.d_idf_doff.as<int64_t>();
+    g.idf_dense_len = J.d_idf_dlen.as<int32_t>();
+    g.idf_dense = J.d_idf_dense.as<float>();
     g.has_idf = J.d_has_idf.as<uint8_t>();
     g.slot_of = J.d_slot_of.as<int32_t>();
     g.g_off = J.d_goff.as<int64_t>();
@@ -410,6 +431,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     auto& J = c->jb;
     const HostCorpus& hc = c->hc;
     const bool packed = c->hs.packed;
+    HpLap hl;
     // ---- layout
     std::vector<DevJob> dj;
     std::vector<int32_t> pool32;
@@ -504,25 +526,43 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     }
     if (dj.empty()) return PF_OK;
     if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
-    // ---- images (pf_api.cpp plan_images layout)
+    // ---- images (pf_api.cpp plan_images layout); the ones K6 builds in LDS first
+    const uint32_t ntab = packed ? 1u : 3u;
+    const int lge = lg_for(0);
+    auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
+    auto dlg_of = [&](int32_t idx) { return pow2_lg(2 * (int64_t)J.img_nset[idx] + 2); };
+    int n_lds = 0;
+    {
+        std::vector<int32_t> order(img_idx.size()), pos(img_idx.size());
+        std::vector<uint8_t> in_lds(img_idx.size());
+        for (size_t k = 0; k < img_idx.size(); ++k) {
+            const int32_t idx = img_idx[k];
+            in_lds[k] = J.img_lg[idx] && qimage_lds(J.img_lg[idx], lge, dlg_of(idx),
+                                                    (uint32_t)(J.img_nset[idx] + ntok_of(idx)), packed) > 0;
+            n_lds += in_lds[k];
+        }
+        int a = 0, g2 = n_lds;
+        for (size_t k = 0; k < img_idx.size(); ++k) pos[k] = in_lds[k] ? a++ : g2++;
+        for (size_t k = 0; k < img_idx.size(); ++k) order[pos[k]] = img_idx[k];
+        img_idx.swap(order);
+        for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
+    }
     std::vector<ImgJob> ij(img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
     uint32_t max_lds = 0;
     bool gtab = false;
     size_t ipool = 0;
     int64_t scr = 0;
-    const uint32_t ntab = packed ? 1u : 3u;
-    const int lge = lg_for(0);
     for (size_t k = 0; k < img_idx.size(); ++k) {
         const int32_t idx = img_idx[k];
         const int lg = J.img_lg[idx];
         if (lg == 0) return c->fail(PF_EUNSUPP, "query hash table too large");
-        const int64_t ntok = hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T];
+        const int64_t ntok = ntok_of(idx);
         ImgJob& m = ij[k];
         m.idx = idx;
         m.lg = lg;
         m.lge = lge;
-        m.dlg = pow2_lg(2 * (int64_t)J.img_nset[idx] + 2);
+        m.dlg = dlg_of(idx);
         m.const_off = (uint32_t)ipool;
         m.keys_off = (uint32_t)(ipool + sizeof(QConst));
         const size_t nkeys = ((size_t)ntab << lg) + ((size_t)1 << lge);
@@ -530,7 +570,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         ipool = a16z(m.vals_off + (size_t)ntok * sizeof(QVal));
         if (ipool >= (size_t)UINT32_MAX) return c->fail(PF_EUNSUPP, "query images of one batch exceed 4 GB");
         m.scr_off = scr;
-        scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 item list
+        if ((int)k >= n_lds) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 items
         QImageRef& r = refs[k];
         r.const_off = m.const_off;
         r.keys_off = m.keys_off;
@@ -542,6 +582,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
                               4u * 256u + 2048u;
         max_lds = std::max(max_lds, need);
     }
+    hl.lap(kHpImages);
     // ---- staging: [DevJob | pool32 | pool64 | ImgJob | QImageRef | PairBlock | jix x3]
     if (pool32.empty()) pool32.push_back(0);
     if (pool64.empty()) pool64.push_back(0);
@@ -579,6 +620,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
+    hl.lap(kHpPack);
     // ---- workspaces
     const size_t nE = (size_t)std::max<int64_t>(E, 1);
     HIPCHK(c, J.d_slots.ensure(nE * 4));
@@ -604,13 +646,13 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         }
     }
     // ---- the stages, in stream order
-    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, (int)ij.size(), J.d_img.as<uint8_t>(), J.d_scr.as<uint32_t>(),
-                             J.d_fail.as<int32_t>(), c->stream));
+    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, J.d_img.as<uint8_t>(),
+                             J.d_scr.as<uint32_t>(), J.d_fail.as<int32_t>(), c->stream));
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
                             J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
                             J.d_ncand.as<int32_t>(), c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
-    if (J.stats_on && !blocks.empty()) {
+    if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {
             hipEvent_t a, b2;
             HIPCHK(c, hipEventCreate(&a));
@@ -626,9 +668,11 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
                            J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
     if (pe1) {
         HIPCHK(c, hipEventRecord(pe1, c->stream));
+        ++J.st_launches;
+    }
+    if (J.stats_count && !blocks.empty()) {
         HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), J.d_slots.as<int32_t>(),
                                     J.d_stats.as<unsigned long long>(), c->stream));
-        ++J.st_launches;
         for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
             const QImageRef& r = refs[pb.qimg];
             J.st_img_bytes += (int64_t)(r.vals_off - r.const_off) +
@@ -671,11 +715,13 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, J.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
                                  c->stream));
     }
+    hl.lap(kHpStage2);  // launches issued
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    hl.lap(kHpGpu);
     if (*reinterpret_cast<const int32_t*>(ho + o_fail))
         return c->fail(PF_EINTERNAL, "device query table build did not converge");
     const int32_t* cnt = reinterpret_cast<const int32_t*>(ho + o_cnt);
-    if (J.stats_on) {
+    if (J.stats_on || J.stats_count) {
         J.st_jobs += (int64_t)dj.size();
         for (size_t x = 0; x < dj.size(); ++x)
             if (dj[x].kind == kDjInterest || dj[x].kind == kDjCollab || dj[x].kind == kDjAll) J.st_cands += cnt[x];
@@ -716,6 +762,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         rank(r, jb.topk);
         jb.out = std::move(r);
     }
+    hl.lap(kHpUnpack);
     return PF_OK;
 }
 
@@ -739,6 +786,7 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     std::vector<JP> P(jobs.size());
     par_jobs(jobs.size(), [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 16);
     hl.lap(kHpPrep);
+    hl.skip();
     size_t b = 0;
     while (b < jobs.size()) {
         size_t e = b;
@@ -754,7 +802,6 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         if (rc != PF_OK) return rc;
         b = e;
     }
-    hl.lap(kHpGpu);
     return PF_OK;
 }
 
@@ -768,7 +815,8 @@ int jobs_stats_reset(pf_ctx* c, int enable) {
     HIPCHK(c, J.d_stats.ensure(64));
     HIPCHK(c, hipMemsetAsync(J.d_stats.p, 0, 64, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    J.stats_on = enable != 0;
+    J.stats_on = (enable & 1) != 0;
+    J.stats_count = (enable & 2) != 0;
     J.stat_used = 0;
     J.st_jobs = J.st_cands = J.st_img_bytes = J.st_launches = 0;
     return PF_OK;

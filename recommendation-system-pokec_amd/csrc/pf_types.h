@@ -247,6 +247,9 @@ struct DevJobsStore {
     const int64_t* idf_off;     // [T + 1] per column: sorted tids and their float idf
     const int32_t* idf_tid;
     const float* idf_val;
+    const int64_t* idf_dense_off;  // [T] a column's dense idf table (1.0 for absent tids), -1 = none
+    const int32_t* idf_dense_len;  // [T]
+    const float* idf_dense;
     const uint8_t* has_idf;     // [T]
     const int32_t* slot_of;     // [n] idx -> tile-store slot
     // graph

@@ -256,9 +256,11 @@ class FasEngine:
         self._check(self._L.pf_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)), "pf_profile_read")
         return ms.value, n.value
 
-    def jobs_stats_reset(self, enable=True):
-        """Start (or stop) counting the recommenders' job-pipeline statistics (pf_jobs_stats)."""
-        self._check(self._L.pf_jobs_stats_reset(self.h, 1 if enable else 0), "pf_jobs_stats_reset")
+    def jobs_stats_reset(self, time_pairs=True, count=True):
+        """Start (or stop) the recommenders' job-pipeline statistics (pf_jobs_stats): pair-kernel
+        timing events and/or the pair / byte counters."""
+        self._check(self._L.pf_jobs_stats_reset(self.h, (1 if time_pairs else 0) | (2 if count else 0)),
+                    "pf_jobs_stats_reset")
 
     def jobs_stats(self):
         s = PfJobsStats()

@@ -559,6 +559,8 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     if (e == hipSuccess) e = upload(c, c->d_hdr0, hs.hdr0);
     if (e == hipSuccess) e = upload(c, c->d_hdr1, hs.hdr1);
     if (e == hipSuccess) e = upload(c, c->d_hdr2, hs.hdr2);
+    if (e == hipSuccess) e = upload(c, c->d_rowstore, hs.rows);
+    if (e == hipSuccess) e = upload(c, c->d_rowstore_off, hs.row_off);
     if (c->hp.ok) {
         auto& hp = c->hp;
         if (e == hipSuccess) e = upload(c, c->d_phdr, hp.hdr);
@@ -576,6 +578,8 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     c->norm_bytes = (int64_t)hs.norms.size() * 8;
     std::vector<uint4>().swap(hs.stream);
     std::vector<double>().swap(hs.norms);
+    std::vector<uint4>().swap(hs.rows);
+    std::vector<uint64_t>().swap(hs.row_off);
     c->ds.stream = c->d_stream.as<uint4>();
     c->ds.tile_off = c->d_tile_off.as<uint64_t>();
     c->ds.tile_steps = c->d_tile_steps.as<uint32_t>();
@@ -587,6 +591,8 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     c->ds.hdr0 = c->d_hdr0.as<uint4>();
     c->ds.hdr1 = c->d_hdr1.as<uint4>();
     c->ds.hdr2 = c->d_hdr2.as<uint4>();
+    c->ds.rows = c->d_rowstore.as<uint4>();
+    c->ds.row_off = c->d_rowstore_off.as<uint64_t>();
     c->ds.n_slots = c->hc.n;
     c->ds.n_tiles = (int32_t)hs.tile_steps.size();
     c->ds.packed = hs.packed ? 1 : 0;

@@ -117,12 +117,12 @@ struct pf_ctx {
     pf::HostCorpus hc;
     pf::HostStore hs;       // metadata only after upload (stream freed)
     int64_t stream_bytes = 0, norm_bytes = 0;
-    DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2;
+    DBuf d_stream, d_tile_off, d_tile_steps, d_tile_slot0, d_tile_lgk, d_slot_tile, d_norms, d_norm_off, d_hdr0, d_hdr1, d_hdr2,
+        d_rowstore, d_rowstore_off;
     pf::DevStore ds{};
     // workspaces
-    DBuf d_pool, d_refs, d_out, d_rows, d_slots, d_blocks, d_scores, d_w, d_wrow, d_csum, d_part, d_cjobs;
-    PinBuf h_pool, h_slots, h_scores;  // pair batches: images, candidate slots, scores
-    DBuf d_pairs1;                     // run_jobs stage-1 scores (the collaborative matrices)
+    DBuf d_pool, d_refs, d_out, d_slots, d_blocks, d_scores, d_part;
+    PinBuf h_pool, h_slots, h_scores;  // pf_fas_pairs batches: images, candidate slots, scores
     int32_t tile_begin = 0, tile_end = 0;
     // postings store (K5); wave blocks [wb_begin, wb_end) are this context's shard
     pf::HostPost hp;

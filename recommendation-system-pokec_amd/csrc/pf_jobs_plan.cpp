@@ -510,7 +510,14 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
                 E += (int64_t)d.nfd * p.cap;
                 const int32_t iu = img(p.u);
                 add_blocks(iu, d.sim_off, d.nfd, d.sim_off);
-                for (int r = 0; r < d.nfd; ++r) add_blocks(img(p.fd[r]), d.cand_off, p.cap, d.m_off + (int64_t)r * p.cap);
+                // candidate-chunk major: the friends' blocks of one 256-candidate chunk are
+                // consecutive, so they run together and share the chunk's records in cache
+                std::vector<int32_t> fimg(d.nfd);
+                for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
+                for (int64_t x = 0; x < p.cap; x += 256)
+                    for (int r = 0; r < d.nfd; ++r)
+                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), (int32_t)std::min<int64_t>(256, p.cap - x),
+                                                   (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
                 jix_collab.push_back(jn);
                 max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);
             } else if (p.kind == kDjInterest || p.kind == kDjAll) {
@@ -784,7 +791,9 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     if (rc != PF_OK) return rc;
     HpLap hl;
     std::vector<JP> P(jobs.size());
-    par_jobs(jobs.size(), [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 16);
+    // 1-hop planning is a few microseconds per job: threads only for large batches (spawning
+    // them costs more than planning a 64-user step)
+    par_jobs(jobs.size(), [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 256);
     hl.lap(kHpPrep);
     hl.skip();
     size_t b = 0;

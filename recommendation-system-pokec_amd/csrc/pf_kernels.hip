@@ -173,13 +173,15 @@ __device__ __forceinline__ double text_terms_slow(const DevStore& st, const QVie
 // padding, so loads need no clamp and words no mask.  MASKED = true (pairs): lanes of
 // different tiles; loads are clamped to the lane's last step and words past the chunk
 // are masked.
-template <bool PACKED, bool MASKED>
+// STRIDE: uint4 distance between a lane's successive steps (kTileSlots in the tile stream,
+// 1 in the row store).
+template <bool PACKED, bool MASKED, int STRIDE = kTileSlots>
 __device__ __forceinline__ void walk_chunk(Walk& W, const uint4* base, uint32_t j0, uint32_t clen, uint32_t nc,
                                            uint32_t nset, const QView& v, uint32_t hstride) {
     const uint32_t steps = (clen + 3) >> 2;
     const uint32_t smax = wave_max_u32(steps);
     const uint32_t last = steps ? steps - 1 : 0;
-    auto ld = [&](uint32_t s) { return base[(size_t)(MASKED ? (s < last ? s : last) : s) * kTileSlots]; };
+    auto ld = [&](uint32_t s) { return base[(size_t)(MASKED ? (s < last ? s : last) : s) * STRIDE]; };
     const int tb = (int)nset - (int)j0, lim = (int)clen;
     const uint32_t len = j0 + clen;
     auto walk = [&](const uint4& c, uint32_t s) {
@@ -295,31 +297,26 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
     return (float)((2.0 * S * F) / (S + F));
 }
 
-// FAS of slot p by one lane alone (pairs kernel): its chunks are walked one after the
-// other, so its own hit list holds the whole record's hits in order.
+// FAS of slot p by one lane alone (pairs kernel): the lane walks the slot's record in the row
+// store (contiguous 16-B steps, so the lane's loads consume whole cache lines), its own hit list
+// then holds the whole record's hits in order.
 template <bool PACKED>
 __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
     Loc l{0, 0, 0};
+    uint64_t ro = 0;
     if (active) {
         h0 = st.hdr0[p];
         h1 = st.hdr1[p];
         h2 = st.hdr2[p];
         l = loc_of(st, p);
+        ro = st.row_off[p];
     }
     const uint32_t nc = h2.y, nset = h2.y + h2.z;
-    const uint32_t len = record_words(h2, PACKED);
-    const uint32_t k = active ? 1u << l.lgk : 0u;
-    const uint32_t q = chunk_words(len, l.lgk, PACKED);
+    const uint32_t len = active ? record_words(h2, PACKED) : 0u;
     Walk W;
     W.cnt = 0; W.nh = 0; W.pend = 0;
-    const uint32_t kmax = wave_max_u32(k);
-    const uint4* tb = st.stream + (active ? st.tile_off[l.tile] + ((uint32_t)l.cand << l.lgk) : 0);
-    for (uint32_t c = 0; c < kmax; ++c) {
-        const uint32_t j0 = c * q;
-        const uint32_t clen = (c < k && len > j0) ? min(q, len - j0) : 0u;
-        walk_chunk<PACKED, true>(W, tb + (c < k ? c : 0), j0, clen, nc, nset, v, blockDim.x);
-    }
+    walk_chunk<PACKED, true, 1>(W, st.rows + ro, 0u, len, nc, nset, v, blockDim.x);
     if (!active) return 0.0f;
     const uint32_t nh = W.nh;
     return fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });

@@ -42,6 +42,8 @@ struct HostStore {
     std::vector<double> norms;
     std::vector<uint64_t> norm_off;
     std::vector<uint4> hdr0, hdr1, hdr2;
+    std::vector<uint4> rows;            // row store: slot p's record at rows[row_off[p]], 16-B padded
+    std::vector<uint64_t> row_off;      // [n + 1]
     std::vector<int32_t> slot_of_idx;
     std::vector<int32_t> idx_of_slot;
     bool packed = true;

@@ -158,6 +158,8 @@ struct DevStore {
     const uint4* hdr0;         // [n_slots]
     const uint4* hdr1;
     const uint4* hdr2;
+    const uint4* rows;         // row store: slot p's record contiguous from rows[row_off[p]] (pair kernel)
+    const uint64_t* row_off;   // [n_slots + 1]
     int32_t n_slots;
     int32_t n_tiles;
     int32_t packed;

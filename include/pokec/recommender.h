@@ -5,14 +5,24 @@
 // setters, same recommender signatures and results (bit-identical scores, same
 // order); the scoring runs on the GPU.  Header-only; link libpokec_fas.so.
 //
+// The class is a template over the profile type, pokec::BasicRecommender<Profile>; any
+// struct with the reference's UserProfile fields (include/user_profile.h:10-20) works.
+//   - pokec::Recommender = BasicRecommender<pokec::UserProfile> (this header's twin struct);
+//   - drop-in mode: a translation unit that includes the reference's user_profile.h and
+//     defines POKEC_DROP_IN before this header gets ::Recommender =
+//     BasicRecommender<::UserProfile>, so the reference's own call sites (api_cli.cpp:155-234,
+//     test.cpp:36-75, recommendation_tests.cpp:50-140) compile unchanged against the engine.
+//
 // Differences a caller must know:
 //   - The engine snapshots the maps when it first scores (pf_open copies them to
 //     HBM).  The reference reads *adj_list live, so a caller that mutates the
 //     adjacency afterwards (the hold-out drivers' adj_mod) calls
 //     sync_adjacency(uid) for each row it changed.  Profiles and normalisers are
 //     also fixed at that point; a setter called later re-opens the engine.
-//   - profile_similarity(A, B) scores two profiles OF THE MAP (by user_id), which
-//     is how every reference caller uses it.  It returns NaN otherwise.
+//   - profile_similarity(A, B[, text_columns]) scores two profiles OF THE MAP (by
+//     user_id), which is how every reference caller uses it.  It returns NaN otherwise.
+//     With a text_columns list other than set_text_columns', a second engine context is
+//     opened (once per distinct list) with that list as its columns.
 //   - The legacy user_feats constructor and recommend_from_supernodes
 //     (recommender_clubs.cpp:75-...) are not provided: no live caller uses them
 //     (SURVEY.md §8 A12).
@@ -25,6 +35,7 @@
 #include <array>
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -47,20 +58,21 @@ struct UserProfile {
     std::array<int, 3> region_parts = {-1, -1, -1};
 };
 
-class Recommender {
+template <class Profile>
+class BasicRecommender {
 public:
     using Ranked = std::vector<std::pair<int, float>>;
     using NormMap = std::unordered_map<std::string, std::pair<float, float>>;
     using IdfMap = std::unordered_map<std::string, std::unordered_map<int, float>>;
 
-    Recommender(const std::unordered_map<int, UserProfile>* profiles_in,
-                const std::unordered_map<int, std::vector<int>>* al, int device = 0)
+    BasicRecommender(const std::unordered_map<int, Profile>* profiles_in,
+                     const std::unordered_map<int, std::vector<int>>* al, int device = 0)
         : profiles(profiles_in), adj_list(al), device_(device) {
         total_users = profiles ? profiles->size() : 0;
     }
-    ~Recommender() { close_(); }
-    Recommender(const Recommender&) = delete;
-    Recommender& operator=(const Recommender&) = delete;
+    ~BasicRecommender() { close_(); }
+    BasicRecommender(const BasicRecommender&) = delete;
+    BasicRecommender& operator=(const BasicRecommender&) = delete;
 
     // recommender.cpp:27-41
     void set_field_normalizers(const NormMap& m) { field_normalizers = m; close_(); }
@@ -110,12 +122,29 @@ public:
     // user and its adj_list row, one GPU pass.
     Ranked recommend_interest_all(int user, int topk) const { return run_(3, user, topk, 0); }
 
-    // recommender_similarity.cpp:10-124, for two profiles of the map
-    float profile_similarity(const UserProfile& A, const UserProfile& B) const {
+    // recommender_similarity.cpp:10-124,126-128, for two profiles of the map
+    float profile_similarity(const Profile& A, const Profile& B) const {
         if (!open_()) return NAN;
         const int32_t a = A.user_id, b = B.user_id;
         float out = NAN;
         if (pf_fas_pairs(ctx_, &a, &b, 1, &out) != PF_OK) return NAN;
+        return out;
+    }
+    // recommender_similarity.cpp:10-124 over a caller-given column list (include/recommender.h:41):
+    // its names pick the normalisers and idf maps, its length the columns compared and F's
+    // denominator.  The set_text_columns list is the context's own; another list opens (once)
+    // a second context with that list.
+    float profile_similarity(const Profile& A, const Profile& B, const std::vector<std::string>& text_columns) const {
+        if (text_columns == text_columns_internal_) return profile_similarity(A, B);
+        auto it = alt_.find(text_columns);
+        if (it == alt_.end()) {
+            pf_ctx* c = nullptr;
+            if (!open_with_(text_columns, &c)) return NAN;
+            it = alt_.emplace(text_columns, c).first;
+        }
+        const int32_t a = A.user_id, b = B.user_id;
+        float out = NAN;
+        if (pf_fas_pairs(it->second, &a, &b, 1, &out) != PF_OK) return NAN;
         return out;
     }
 
@@ -131,7 +160,7 @@ public:
     pf_ctx* engine() const { return open_() ? ctx_ : nullptr; }
 
     // the reference's public data members (include/recommender.h:49-60)
-    const std::unordered_map<int, UserProfile>* profiles = nullptr;
+    const std::unordered_map<int, Profile>* profiles = nullptr;
     const std::unordered_map<int, std::vector<int>>* adj_list = nullptr;
     NormMap field_normalizers;
     NormMap column_normalizers;
@@ -168,20 +197,26 @@ private:
     void close_() const {
         if (ctx_) pf_close(ctx_);
         ctx_ = nullptr;
+        for (auto& kv : alt_) pf_close(kv.second);
+        alt_.clear();
     }
 
-    // Flatten the maps into a pf_corpus_desc and open the engine (once).
     bool open_() const {
         if (ctx_) return true;
+        if (!open_with_(text_columns_internal_, &ctx_)) return false;
+        return true;
+    }
+
+    // Flatten the maps into a pf_corpus_desc over column list `cols` and open an engine context.
+    bool open_with_(const std::vector<std::string>& cols, pf_ctx** out) const {
         if (!profiles || !adj_list) { err_ = "null profiles or adj_list"; return false; }
-        const std::vector<std::string>& cols = text_columns_internal_;
         const int T = (int)cols.size();
         D& d = d_;
         d = D();
         const size_t n = profiles->size();
         d.club_off.push_back(0); d.friend_off.push_back(0); d.tok_off.push_back(0);
         for (auto& kv : *profiles) {
-            const UserProfile& p = kv.second;
+            const Profile& p = kv.second;
             d.uid.push_back(kv.first); d.pub.push_back(p.public_flag); d.comp.push_back(p.completion_percentage);
             d.gen.push_back(p.gender); d.age.push_back(p.age);
             for (int k = 0; k < 3; ++k) d.reg.push_back(p.region_parts[k]);
@@ -222,7 +257,7 @@ private:
         c.n_adj = (int32_t)d.adj_uid.size();
         c.adj_uid = d.adj_uid.data(); c.adj_off = d.adj_off.data(); c.adj_nbr = d.adj_nbr.data();
         c.norm_present = d.npres.data(); c.norm_mean = d.nmean.data(); c.norm_sd = d.nsd.data();
-        if (!idf_explicit_ && idf_cols_ == cols) {
+        if (!idf_explicit_ && idf_cols_ == cols) {  // recommender.cpp:43-66 over the same columns
             c.idf_mode = PF_IDF_FROM_PROFILES;
         } else {
             // explicit maps: set_tfidf_index, or IDF computed over another column list
@@ -247,9 +282,9 @@ private:
             c.col_has_idf = d.has_idf.data(); c.idf_off = d.idf_off.data();
             c.idf_tid = d.idf_tid.data(); c.idf_val = d.idf_val.data();
         }
-        if (pf_open(&c, device_, &ctx_) != PF_OK) {
+        if (pf_open(&c, device_, out) != PF_OK) {
             err_ = pf_last_error(nullptr);
-            ctx_ = nullptr;
+            *out = nullptr;
             return false;
         }
         n_users_ = (int64_t)n;
@@ -285,11 +320,19 @@ private:
     std::vector<std::string> idf_cols_;
     bool idf_explicit_ = false;
     mutable pf_ctx* ctx_ = nullptr;
+    mutable std::map<std::vector<std::string>, pf_ctx*> alt_;  // 3-argument profile_similarity lists
     mutable int64_t n_users_ = 0, n_club_entries_ = 0;
     mutable D d_;
     mutable std::string err_;
 };
 
+using Recommender = BasicRecommender<UserProfile>;
+
 }  // namespace pokec
+
+#ifdef POKEC_DROP_IN
+// the reference's names: ::UserProfile is the caller's (the reference's user_profile.h)
+using Recommender = pokec::BasicRecommender<::UserProfile>;
+#endif
 
 #endif  // POKEC_RECOMMENDER_H

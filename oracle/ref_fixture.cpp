@@ -217,6 +217,77 @@ int main(int argc, char** argv) {
     }
     fclose(f);
 
+    // ---- A7 / set_tfidf_index: an explicit idf map that omits columns (raw-count cosine,
+    //      recommender_similarity.cpp:99-104 -> recommender.cpp:141-163), omits tokens (idf 1.0,
+    //      recommender.cpp:78), holds one empty column map, and scales the rest ----
+    {
+        std::unordered_map<std::string, std::unordered_map<int, float>> em;
+        for (size_t t = 0; t < cols.size(); ++t) {
+            if (t % 7 == 1 || t == 4) continue;  // absent columns
+            auto it = rec.idf_per_col.find(cols[t]);
+            std::unordered_map<int, float> m;
+            if (t != 10 && it != rec.idf_per_col.end())
+                for (auto& kv : it->second) {
+                    if (kv.first % 5 == 3) continue;  // absent tokens
+                    m[kv.first] = kv.second * (t % 2 ? 1.5f : 0.75f);
+                }
+            em[cols[t]] = m;
+        }
+        Recommender rx(&profiles, &adj);
+        rx.set_field_normalizers(norms);
+        rx.set_column_normalizers(norms);
+        rx.set_tfidf_index(em);
+        rx.set_text_columns(cols);
+        f = open("idf_explicit_map.txt");
+        fprintf(f, "cols");
+        for (size_t t = 0; t < cols.size(); ++t) if (em.count(cols[t])) fprintf(f, " %zu", t);
+        fprintf(f, "\n");
+        for (size_t t = 0; t < cols.size(); ++t) {
+            auto it = em.find(cols[t]);
+            if (it == em.end()) continue;
+            std::vector<std::pair<int, float>> v(it->second.begin(), it->second.end());
+            std::sort(v.begin(), v.end());
+            for (auto& kv : v) fprintf(f, "%zu %d %08x\n", t, kv.first, fbits(kv.second));
+        }
+        fclose(f);
+        f = open("idf_explicit_pairs.txt");
+        std::mt19937 rx_rng(seed + 1);
+        for (int i = 0; i < npairs / 3; ++i) {
+            int a = uids[pick(rx_rng)], b = uids[pick(rx_rng)];
+            fprintf(f, "%d %d %08x\n", a, b, fbits(rx.profile_similarity(profiles.at(a), profiles.at(b))));
+        }
+        fclose(f);
+        f = open("idf_explicit_recs.txt");
+        for (int u : queries) {
+            dump_list(f, "collab", u, 20, 5000, rx.recommend_collaborative(u, 20, 5000));
+            dump_list(f, "interest", u, 20, 5000, rx.recommend_by_interest(u, 20, 5000));
+            dump_list(f, "clubs", u, 20, 5000, rx.recommend_clubs_collab(u, 20, 5000));
+        }
+        fclose(f);
+        f = open("idf_explicit_all.txt");
+        for (int u : queries) {
+            auto itq = profiles.find(u);
+            std::vector<std::pair<int, float>> v;
+            if (itq != profiles.end()) {
+                std::unordered_set<int> excl;
+                auto ia = adj.find(u);
+                if (ia != adj.end()) excl.insert(ia->second.begin(), ia->second.end());
+                excl.insert(u);
+                for (auto& kv : profiles) {
+                    if (excl.count(kv.first)) continue;
+                    v.emplace_back(kv.first, rx.profile_similarity(itq->second, kv.second));
+                }
+                std::sort(v.begin(), v.end(), [](const std::pair<int, float>& A, const std::pair<int, float>& B) {
+                    if (A.second == B.second) return A.first < B.first;
+                    return A.second > B.second;
+                });
+                if (v.size() > 50) v.resize(50);
+            }
+            dump_list(f, "all", u, 50, 0, v);
+        }
+        fclose(f);
+    }
+
     // ---- A19 hold-out drivers ----
     if (holdout_n > 0) {
         std::string p = out + "/holdout_friends.txt";

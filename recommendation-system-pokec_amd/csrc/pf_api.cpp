@@ -478,8 +478,8 @@ HostProf::HostProf() {
 }
 HostProf::~HostProf() {
     if (!on) return;
-    static const char* nm[kHpStages] = {"plan", "prep", "layout", "staging", "wait", "decode", "launch", "collab",
-                                        "finish"};
+    static const char* nm[kHpStages] = {"workspaces", "prep", "layout", "staging", "wait", "decode", "launch-b",
+                                        "launch-a", "finish"};
     fprintf(stderr, "pokec_fas host stages (s):");
     for (int i = 0; i < kHpStages; ++i) fprintf(stderr, " %s=%.3f", nm[i], (double)ns[i].load() * 1e-9);
     fprintf(stderr, "\n");

@@ -80,6 +80,7 @@ struct JobsState {
         d_idf_doff, d_idf_dlen, d_idf_dense,
         d_has_idf, d_slot_of, d_goff, d_glen, d_gnbr, d_guid, d_club_off, d_club_dense, d_club_id;
     std::unordered_map<int32_t, int32_t> xnode;  // uid -> node for adj_list uids without a profile
+    std::vector<int32_t> dense_node;             // uid -> node (-1 none) when the uids are dense
     std::vector<int32_t> g_uid, g_len;           // host mirrors (new uids from pf_set_adj append nodes)
     bool nodes_dirty = false;
     std::vector<uint8_t> img_lg;                 // per idx: query-table log2 (0 = outside the device limits)

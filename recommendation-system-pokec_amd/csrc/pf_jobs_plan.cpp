@@ -28,6 +28,11 @@ constexpr int64_t kChunkHt = 128ll << 20;    // gather hash tables per chunk (in
 constexpr uint32_t kStageLimitJobs = 48 * 1024;  // as pf_api.cpp kStageLimit (LDS-staged tables)
 
 int32_t node_of(const pf_ctx* c, int32_t uid) {
+    const auto& dn = c->jb.dense_node;  // uids of a dense range: one load (built at open)
+    if (uid >= 0 && (size_t)uid < dn.size()) {
+        const int32_t x = dn[uid];
+        if (x >= 0 || !c->jb.nodes_dirty) return x;
+    }
     const int32_t i = c->hc.idx_of(uid);
     if (i >= 0) return i;
     auto it = c->jb.xnode.find(uid);
@@ -42,6 +47,7 @@ int32_t ensure_node(pf_ctx* c, int32_t uid) {
     J.xnode.emplace(uid, x);
     J.g_uid.push_back(uid);
     J.g_len.push_back(-1);
+    if (uid >= 0 && (size_t)uid < J.dense_node.size()) J.dense_node[uid] = x;
     J.nodes_dirty = true;
     return x;
 }
@@ -145,6 +151,20 @@ int jobs_open(pf_ctx* c) {
     }
     const int32_t M = (int32_t)J.g_uid.size();
     J.g_len.assign(M, -1);
+    // uid -> node as a dense table when the uids are non-negative and not too sparse
+    J.dense_node.clear();
+    {
+        int64_t mx = -1;
+        bool ok = true;
+        for (int32_t u : J.g_uid) {
+            if (u < 0) { ok = false; break; }
+            mx = std::max<int64_t>(mx, u);
+        }
+        if (ok && mx >= 0 && mx < 4 * (int64_t)M + 4096) {
+            J.dense_node.assign((size_t)mx + 1, -1);
+            for (int32_t x = 0; x < M; ++x) J.dense_node[J.g_uid[x]] = x;
+        }
+    }
     std::vector<int64_t> g_off(M, 0);
     std::vector<int32_t> rnode(rows.size());
     std::vector<int64_t> roff(rows.size() + 1, 0);
@@ -641,6 +661,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     HIPCHK(c, J.d_keys.ensure(dj.size() * (size_t)ktop * 8));
     HIPCHK(c, J.d_fail.ensure(16));
     HIPCHK(c, hipMemsetAsync(J.d_fail.p, 0, 16, c->stream));
+    hl.lap(kHpPlan);  // workspaces
     if (!jix_clubs.empty()) {
         const int64_t want = (int64_t)jix_clubs.size();
         if (want > J.acc_jobs) {
@@ -687,6 +708,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
                                                                hc.tok_off[(size_t)ij[pb.qimg].idx * hc.T]) * 16 : 0);
         }
     }
+    hl.lap(kHpCollab);  // images, gathers, pairs launched
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, J.d_fl.as<float>(),
                             J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, J.d_fl.as<float>(),

@@ -84,6 +84,28 @@ class Corpus:
     def n_users(self):
         return len(self.uid)
 
+    def set_explicit_idf(self, present, entries):
+        """idf_mode = PF_IDF_EXPLICIT (Recommender::set_tfidf_index): present = columns whose name
+        is in idf_per_col; entries = {col: [(tid, float32), ...]} for them."""
+        T = self.n_cols
+        self.col_has_idf = np.zeros(T, np.uint8)
+        off, tid, val = [0], [], []
+        for t in range(T):
+            if t in present:
+                self.col_has_idf[t] = 1
+                for k, v in sorted(entries.get(t, [])):
+                    tid.append(k)
+                    val.append(v)
+            off.append(len(tid))
+        self.idf_off = np.array(off, np.int64)
+        self.idf_tid = np.array(tid if tid else [0], np.int32)
+        self.idf_val = np.array(val if val else [0], np.float32)
+        d = self.desc
+        d.idf_mode = PF_IDF_EXPLICIT
+        d.col_has_idf, d.idf_off = _ptr(self.col_has_idf), _ptr(self.idf_off)
+        d.idf_tid, d.idf_val = _ptr(self.idf_tid), _ptr(self.idf_val)
+        return self
+
     def desc_ptr(self):
         return ctypes.addressof(self.desc)
 
@@ -376,6 +398,33 @@ def golden_lists(name, fn):
         items = [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:5 + n]]
         out[(tag, uid, k, lim)] = items
     return out
+
+
+def golden_explicit_idf(name):
+    """The explicit idf map of tests/golden/<name>/idf_explicit_map.txt: (present columns,
+    {col: [(tid, float32), ...]})."""
+    lines = fixture_lines(name, "idf_explicit_map.txt")
+    present = {int(x) for x in lines[0].split()[1:]}
+    entries = {}
+    for ln in lines[1:]:
+        t, k, h = ln.split()
+        entries.setdefault(int(t), []).append((int(k), f32(h)))
+    return present, entries
+
+
+def explicit_idf_corpus(name):
+    """Golden corpus `name` (a fresh Corpus object sharing its arrays) with the golden explicit idf map."""
+    c = with_rows(golden_corpus(name))
+    present, entries = golden_explicit_idf(name)
+    return c.set_explicit_idf(present, entries)
+
+
+def golden_pairs_file(name, fn):
+    a, b, s = [], [], []
+    for ln in fixture_lines(name, fn):
+        x, y, h = ln.split()
+        a.append(int(x)); b.append(int(y)); s.append(int(h, 16))
+    return np.array(a, np.int32), np.array(b, np.int32), np.array(s, np.uint32)
 
 
 def golden_idf(name):

@@ -80,6 +80,37 @@ def test_all_candidates_scan_matches_reference(gold, kernel):
         eng.set_scan_kernel(0)
 
 
+@pytest.mark.parametrize("name", ["A", "B"])
+def test_explicit_idf_matches_reference(name):
+    """PF_IDF_EXPLICIT (Recommender::set_tfidf_index, recommender.h:31): columns absent from the
+    map take the raw-count cosine (A7, recommender.cpp:141-163 via recommender_similarity.cpp:
+    99-104), absent tokens idf 1.0, one column map empty.  FAS pairs, all-candidates top-50 on
+    both scan kernels, and the recommenders (device job pipeline) equal the reference's bits."""
+    c = tl.explicit_idf_corpus(name)
+    eng = tl.engine(c)
+    present, entries = tl.golden_explicit_idf(name)
+    for t in range(c.n_cols):  # the engine reports NaN for a column without a map
+        assert np.isnan(eng.idf(t, 1)) == (t not in present), t
+    a, b, s = tl.golden_pairs_file(name, "idf_explicit_pairs.txt")
+    got = eng.fas_pairs(a, b)
+    assert int(np.count_nonzero(got.view(np.uint32) != s)) == 0
+    g = tl.golden_lists(name, "idf_explicit_all.txt")
+    keys = list(g.keys())
+    for kern in (1, 2):
+        eng.set_scan_kernel(kern)
+        for key, res in zip(keys, eng.recommend_interest_all([k[1] for k in keys], 50)):
+            _check_lists(res, g[key], (kern,) + key)
+    eng.set_scan_kernel(0)
+    for (tag, uid, k, lim), items in tl.golden_lists(name, "idf_explicit_recs.txt").items():
+        if tag == "collab":
+            got, = eng.recommend_collaborative([uid], k, lim)
+        elif tag == "clubs":
+            got, = eng.recommend_clubs_collab([uid], k, lim)
+        else:
+            got, = eng.recommend_interest([uid], k, tl.PF_MODE_FOF, lim)
+        _check_lists(got, items, (tag, uid, k, lim))
+
+
 def test_fof_gathers_match_oracle(gold):
     name, corpus, eng = gold
     orc = tl.Oracle(corpus)
@@ -371,6 +402,7 @@ def test_cpp_facade_matches_reference():
     akey = list(allg.keys())[0]
     q = [f"{t} {u} {k} {lim}" for t, u, k, lim in keys]
     q += [f"pair {x} {y}" for x, y in zip(a[:500], b[:500])]
+    q += [f"pair3 {x} {y}" for x, y in zip(a[:50], b[:50])]  # recommender.h:41, the same column list
     q += [f"all {akey[1]} 50 0", "sync 1 2 3 4", "collab 1 10 5000"]
     with tempfile.TemporaryDirectory() as d:
         tl.regen_reference_dir("A", d)
@@ -384,7 +416,9 @@ def test_cpp_facade_matches_reference():
         assert int(p[4]) == len(g[key]) and items == g[key], key
     for i, ln in enumerate(out[len(keys):len(keys) + 500]):
         assert int(ln.split()[3], 16) == int(s[i]), ln
-    p = out[len(keys) + 500].split()
+    for i, ln in enumerate(out[len(keys) + 500:len(keys) + 550]):
+        assert ln.startswith("pair3") and int(ln.split()[3], 16) == int(s[i]), ln
+    p = out[len(keys) + 550].split()
     assert [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:]] == allg[akey]
     assert out[-2] == "sync 1 0"
     # after the edit, collab for uid 1 equals the engine's with the same adj row
@@ -395,6 +429,39 @@ def test_cpp_facade_matches_reference():
     p = out[-1].split()
     assert [int(x.split(":")[0]) for x in p[5:]] == list(ids)
     assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))
+
+
+def test_cpp_facade_explicit_idf_matches_reference():
+    """The drop-in facade's set_tfidf_index (recommender.h:31) with the golden explicit map:
+    FAS pairs, all-candidates and recommenders equal the reference's (A7 columns included)."""
+    import gzip
+    import os
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(tl.ROOT, "tests", "cpp", "facade_check")
+    a, b, s = tl.golden_pairs_file("A", "idf_explicit_pairs.txt")
+    allg = tl.golden_lists("A", "idf_explicit_all.txt")
+    recs = tl.golden_lists("A", "idf_explicit_recs.txt")
+    akeys = list(allg.keys())[:4]
+    rkeys = list(recs.keys())[::4]
+    q = [f"pair {x} {y}" for x, y in zip(a[:400], b[:400])]
+    q += [f"all {k[1]} 50 0" for k in akeys] + [f"{t} {u} {k} {lim}" for t, u, k, lim in rkeys]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        mp = os.path.join(d, "idf_map.txt")
+        with gzip.open(os.path.join(tl.GOLDEN, "A", "idf_explicit_map.txt.gz"), "rb") as fi, open(mp, "wb") as fo:
+            shutil.copyfileobj(fi, fo)
+        r = subprocess.run([exe, d, mp], input="\n".join(q) + "\n", capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.splitlines()
+    assert len(out) == len(q)
+    for i, ln in enumerate(out[:400]):
+        assert int(ln.split()[3], 16) == int(s[i]), ln
+    for key, ln in zip(akeys + rkeys, out[400:]):
+        p = ln.split()
+        items = [(int(x.split(":")[0]), int(x.split(":")[1], 16)) for x in p[5:]]
+        assert items == (allg if key in allg else recs)[key], key
 
 
 def test_profile_sampling_counts_and_results(big):
@@ -450,8 +517,8 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
 def test_full_size_kernels_agree():
     """BASELINE cfg 2 size (1,632,803 users): the postings scan (K5), the record-stream scan
     (K1) and the pair kernel (K1') are three independent GPU paths; on the full corpus
-    their top-k ids and FAS bits agree, the top-k is sorted by the reference comparator,
-    and the 2-shard merge equals the single-shard result."""
+    their top-k ids and FAS bits agree, equal the oracle's for two queries, the top-k is
+    sorted by the reference comparator, and the 2-shard merge equals the single-shard result."""
     import torch
     pf = tl.product()
     c = tl.synth.Corpus(n_users=1632803, seed=1, edge_cases=0, threads=16)
@@ -473,6 +540,13 @@ def test_full_size_kernels_agree():
         # K1' rescoring of the same pairs
         again = eng.fas_pairs(np.full(k, u, np.int32), p[0])
         assert np.array_equal(again.view(np.uint32), p[1].view(np.uint32)), u
+    # the oracle on the full corpus (the reference algorithm, one core: ~5 s per query) for two
+    # of the queries: the only oracle anchor at the BASELINE cfg-2 size
+    orc = tl.Oracle(None, desc_ptr=c.desc_ptr())
+    for u, p, r in zip(q[:2], post[:2], orc.interest(q[:2], k, tl.PF_MODE_ALL, 0)):
+        assert list(p[0]) == list(r[0]), u
+        assert np.array_equal(p[1].view(np.uint32), r[1].view(np.uint32)), u
+    orc.close()
     s = torch.cuda.Stream()
     parts = torch.empty((2, len(q), k), dtype=torch.int64, device="cuda")
     for r in range(2):

@@ -93,3 +93,22 @@ def test_oracle_holdout_drivers():
     ref = [float(x) for x in tl.fixture_lines("A", "rectests.txt")[0].split()]
     got = orc.recommendation_tests(m["rectest"], 10)
     assert list(got) == ref
+
+
+@pytest.mark.parametrize("name", ["A", "B"])
+def test_oracle_explicit_idf(name):
+    """A7 and set_tfidf_index: with an explicit idf map that omits columns (raw-count cosine,
+    recommender.cpp:141-163), omits tokens (idf 1.0) and holds an empty map, the oracle's FAS
+    pairs, all-candidates top-50 and recommenders equal the reference's."""
+    c = tl.explicit_idf_corpus(name)
+    orc = tl.Oracle(c)
+    a, b, s = tl.golden_pairs_file(name, "idf_explicit_pairs.txt")
+    got = orc.fas_pairs(a, b).view(np.uint32)
+    assert np.array_equal(got, s), f"{np.count_nonzero(got != s)} of {len(s)} FAS floats differ"
+    for (tag, uid, k, lim), items in tl.golden_lists(name, "idf_explicit_all.txt").items():
+        (ids, sc), = orc.interest([uid], k, tl.PF_MODE_ALL, 0)
+        assert list(ids) == [x for x, _ in items] and list(sc.view(np.uint32)) == [h for _, h in items], uid
+    for (tag, uid, k, lim), items in tl.golden_lists(name, "idf_explicit_recs.txt").items():
+        fn = {"collab": orc.collab, "clubs": orc.clubs}.get(tag)
+        (ids, sc), = fn([uid], k, lim) if fn else orc.interest([uid], k, tl.PF_MODE_FOF, lim)
+        assert list(ids) == [x for x, _ in items] and list(sc.view(np.uint32)) == [h for _, h in items], (tag, uid)

@@ -32,6 +32,12 @@ struct DBuf {
         if (e == hipSuccess) cap = want;
         return e;
     }
+    // per-call workspaces: grow to twice the request (at least 1 MiB), so the sizes of
+    // successive batches settle after a few calls instead of re-allocating (hipFree syncs)
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        return ensure(std::max<size_t>(2 * bytes, 1u << 20));
+    }
     ~DBuf() {
         if (p) (void)hipFree(p);
     }

@@ -391,7 +391,10 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
     if (ru)
         for (int32_t x : *ru) p.F.push_back(node_of(c, x));
     const int64_t L = std::max<int32_t>(Jb.limit, 1);
+    // |row(node)| under the view: the base CSR's length unless an edit or the view covers it
+    const bool plain = c->jb.edited.empty() && !Jb.view.over && !Jb.view.own_row;
     auto rowlen = [&](int32_t node) -> int64_t {
+        if (plain && node >= 0 && node < (int32_t)c->jb.g_len.size()) return c->jb.g_len[node];
         const std::vector<int32_t>* r = Jb.view.row(c->jb.g_uid[node]);
         return r ? (int64_t)r->size() : -1;
     };
@@ -635,7 +638,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
-    HIPCHK(c, J.d_plan.ensure(total));
+    HIPCHK(c, J.d_plan.reserve(total));
     HIPCHK(c, hipMemcpyAsync(J.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
     uint8_t* d = J.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
@@ -650,15 +653,15 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     hl.lap(kHpPack);
     // ---- workspaces
     const size_t nE = (size_t)std::max<int64_t>(E, 1);
-    HIPCHK(c, J.d_slots.ensure(nE * 4));
-    HIPCHK(c, J.d_ids.ensure(nE * 4));
-    HIPCHK(c, J.d_fl.ensure(nE * 4));
-    HIPCHK(c, J.d_ht.ensure((size_t)std::max<int64_t>(HT, 1) * 4));
-    HIPCHK(c, J.d_seq.ensure((size_t)std::max<int64_t>(SEQ, 1) * 4));
-    HIPCHK(c, J.d_img.ensure(std::max<size_t>(ipool, 16)));
-    HIPCHK(c, J.d_scr.ensure((size_t)std::max<int64_t>(scr, 1) * 4));
-    HIPCHK(c, J.d_ncand.ensure(dj.size() * 4));
-    HIPCHK(c, J.d_keys.ensure(dj.size() * (size_t)ktop * 8));
+    HIPCHK(c, J.d_slots.reserve(nE * 4));
+    HIPCHK(c, J.d_ids.reserve(nE * 4));
+    HIPCHK(c, J.d_fl.reserve(nE * 4));
+    HIPCHK(c, J.d_ht.reserve((size_t)std::max<int64_t>(HT, 1) * 4));
+    HIPCHK(c, J.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
+    HIPCHK(c, J.d_img.reserve(std::max<size_t>(ipool, 16)));
+    HIPCHK(c, J.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
+    HIPCHK(c, J.d_ncand.reserve(dj.size() * 4));
+    HIPCHK(c, J.d_keys.reserve(dj.size() * (size_t)ktop * 8));
     HIPCHK(c, J.d_fail.ensure(16));
     HIPCHK(c, hipMemsetAsync(J.d_fail.p, 0, 16, c->stream));
     hl.lap(kHpPlan);  // workspaces
@@ -676,9 +679,12 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     // ---- the stages, in stream order
     HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, J.d_img.as<uint8_t>(),
                              J.d_scr.as<uint32_t>(), J.d_fail.as<int32_t>(), c->stream));
+    int max_sort = 0;
+    for (const DevJob& x : dj)
+        if (x.kind == kDjInterest || x.kind == kDjCollab) max_sort = std::max(max_sort, x.cap);
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
                             J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
-                            J.d_ncand.as<int32_t>(), c->stream));
+                            J.d_ncand.as<int32_t>(), max_sort, c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {

@@ -16,11 +16,9 @@ struct ImgJob {
     int64_t scr_off;
 };
 
-// max_cap: the largest interest / collaborative candidate list of the batch (sizes the
-// slot-order sort's LDS)
 hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
-                         int32_t* ncand, int max_cap, hipStream_t s);
+                         int32_t* ncand, hipStream_t s);
 // images [0, n_lds) are built in LDS (qimage_lds(...) > 0), the next n_glob in global memory
 hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_lds, int n_glob,
                           uint8_t* pool, uint32_t* scratch, int32_t* fail, hipStream_t s);

@@ -119,13 +119,12 @@ __device__ __forceinline__ uint32_t ht_claim(int32_t* keys, uint32_t mask, int32
 }
 
 // one workgroup per job
-// sort_cap: keys of dynamic LDS for the slot-order sort (0 = no sort)
+// slot_shift: slot >> slot_shift < 256 (the length buckets of the candidate grouping)
 __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
                                                              const int32_t* __restrict__ pool, int32_t* __restrict__ ht,
                                                              int32_t* __restrict__ seq, int32_t* __restrict__ cand_slot,
                                                              int32_t* __restrict__ cand_id, int32_t* __restrict__ ncand,
-                                                             const int64_t* __restrict__ pool64, int sort_cap) {
-    extern __shared__ __attribute__((aligned(16))) char sort_lds[];
+                                                             const int64_t* __restrict__ pool64, int slot_shift) {
     __shared__ int wsum[kJobWaves];
     __shared__ int s_count, s_keep, s_done;
     const DevJob J = jobs[blockIdx.x];
@@ -279,36 +278,42 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
         if (s_count >= J.L) break;
     }
     const int nk = s_keep;
-    // The scored candidates in slot order, i.e. longest record first (pf_store.cpp build_store),
-    // so the pair kernel's 64-lane waves walk records of near-equal length instead of waiting on
-    // the longest of 64 random ones.  Their order is free: every later stage keeps slot, id and
-    // score together, and the top-k's total order does not depend on it.  (Raw lists keep the
-    // reference's order.)
-    if (!raw && nk > 1 && sort_cap > 0) {
-        uint32_t np = 2;
-        while ((int)np < nk) np <<= 1;
-        if (np <= (uint32_t)sort_cap) {
-            uint64_t* key = reinterpret_cast<uint64_t*>(sort_lds);
-            __syncthreads();
-            for (uint32_t i = tid; i < np; i += kJobThreads)
-                key[i] = (int)i < nk ? (((uint64_t)(uint32_t)slots[i] << 32) | (uint32_t)ids[i]) : ~0ull;
-            __syncthreads();
-            for (uint32_t k = 2; k <= np; k <<= 1)
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t i = tid; i < np; i += kJobThreads) {
-                        const uint32_t l = i ^ j;
-                        if (l > i) {
-                            const uint64_t a = key[i], b = key[l];
-                            const bool up = (i & k) == 0;
-                            if ((a > b) == up) { key[i] = b; key[l] = a; }
-                        }
-                    }
-                    __syncthreads();
-                }
-            for (int i = tid; i < nk; i += kJobThreads) {
-                slots[i] = (int32_t)(key[i] >> 32);
-                ids[i] = (int32_t)(uint32_t)key[i];
+    // The scored candidates grouped by slot range, i.e. by record length (slots are assigned
+    // longest record first, pf_store.cpp build_store), so the pair kernel's 64-lane waves walk
+    // records of similar length instead of waiting on the longest of 64 random ones: a counting
+    // sort into 256 slot buckets through the (finished) hash table's memory.  The order is free:
+    // every later stage keeps slot, id and score together, and the top-k's total order does not
+    // depend on it.  (Raw lists keep the reference's order.)
+    if (!raw && nk > 64) {
+        __shared__ int hist[256];
+        int2* tmp = reinterpret_cast<int2*>(keys);  // 3 << ht_lg words >= 2 * nk
+        hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < nk; i += kJobThreads) atomicAdd(&hist[slots[i] >> slot_shift], 1);
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan of 256 counts by one wave
+            int v[4], t = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { v[k] = hist[tid * 4 + k]; t += v[k]; }
+            int x = t;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (tid >= o) x += y;
             }
+            int run = x - t;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { hist[tid * 4 + k] = run; run += v[k]; }
+        }
+        __syncthreads();
+        for (int i = tid; i < nk; i += kJobThreads) {
+            const int32_t sl = slots[i];
+            tmp[atomicAdd(&hist[sl >> slot_shift], 1)] = make_int2(sl, ids[i]);
+        }
+        __syncthreads();
+        for (int i = tid; i < nk; i += kJobThreads) {
+            const int2 e = tmp[i];
+            slots[i] = e.x;
+            ids[i] = e.y;
         }
     }
     for (int i = nk + tid; i < J.cap; i += kJobThreads) {
@@ -709,17 +714,12 @@ hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nb
 
 hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
-                         int32_t* ncand, int max_cap, hipStream_t s) {
+                         int32_t* ncand, hipStream_t s) {
     if (njobs <= 0) return hipSuccess;
-    // the slot-order sort runs in LDS for candidate lists up to 16384 (128 KiB of keys)
-    int sort_cap = 0;
-    if (max_cap > 1) {
-        sort_cap = 2;
-        while (sort_cap < max_cap) sort_cap <<= 1;
-        if (sort_cap > 16384) sort_cap = 16384;
-    }
-    hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kJobThreads), (size_t)sort_cap * 8, s, g, v, jobs, pool, ht, seq,
-                       cand_slot, cand_id, ncand, pool64, sort_cap);
+    int shift = 0;
+    while ((g.n >> shift) >= 256) ++shift;
+    hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kJobThreads), 0, s, g, v, jobs, pool, ht, seq, cand_slot,
+                       cand_id, ncand, pool64, shift);
     return hipGetLastError();
 }
 

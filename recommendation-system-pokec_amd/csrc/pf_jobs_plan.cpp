@@ -679,12 +679,9 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     // ---- the stages, in stream order
     HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, J.d_img.as<uint8_t>(),
                              J.d_scr.as<uint32_t>(), J.d_fail.as<int32_t>(), c->stream));
-    int max_sort = 0;
-    for (const DevJob& x : dj)
-        if (x.kind == kDjInterest || x.kind == kDjCollab) max_sort = std::max(max_sort, x.cap);
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
                             J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
-                            J.d_ncand.as<int32_t>(), max_sort, c->stream));
+                            J.d_ncand.as<int32_t>(), c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {

@@ -610,7 +610,8 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 // (later the hit lists, u16[4][256]) | exclusion bits u32[32] | misc u32[4] | QCol[48] |
 // PTok[n_tok] | ranges uint2[n_lists] | prefix u32[n_tok + 1].  The tail merge reuses the
 // tf-byte array.
-constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16 + 16 * kPostMaxCols;
+constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16 + 16 * kPostMaxCols +
+                                   8 * (kNumFixed + kPostMaxCols + 1);
 
 // Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
 // this keeps the compiler from moving accesses across the point).
@@ -700,15 +701,18 @@ struct Group {
 __device__ __forceinline__ void load_group(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
                                            uint32_t f0, Group& g) {
     static_assert(kChunkToks <= 8, "3 bisection steps cover 8 lists");
-    const uint32_t base = gpre[js], total = gpre[js + nj] - base;
+    const int je = js + nj;
+    const uint32_t base = gpre[js], total = gpre[je] - base;
     uint32_t xs[kGroupU];
 #pragma unroll
     for (int u = 0; u < kGroupU; ++u) {
         const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
-        int j = js;  // last list starting at or before fl
-        if (j + 4 < js + nj && gpre[j + 4] - base <= fl) j += 4;
-        if (j + 2 < js + nj && gpre[j + 2] - base <= fl) j += 2;
-        if (j + 1 < js + nj && gpre[j + 1] - base <= fl) j += 1;
+        // last list starting at or before fl, branch-free: a probe past the pass reads
+        // gpre[je] - base = total > fl (the result only matters for fl < total)
+        int j = js;
+        j += gpre[min(j + 4, je)] - base <= fl ? 4 : 0;
+        j += gpre[min(j + 2, je)] - base <= fl ? 2 : 0;
+        j += gpre[min(j + 1, je)] - base <= fl ? 1 : 0;
         g.jj[u] = fl < total ? j - js : -1;
         xs[u] = fl < total ? rng[j].x + (fl - (gpre[j] - base)) : 0u;
     }
@@ -746,11 +750,14 @@ __device__ unsigned long long g_k5t[16];
 #define K5T(slot) do { } while (0)
 #endif
 
+// DBG: the PF_K5_DBG phase switches are compiled in (profiling builds of the launch only)
+template <bool DBG>
 __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-                                                              const int32_t* __restrict__ out_rows, uint32_t dbg) {
+                                                              const int32_t* __restrict__ out_rows, uint32_t dbg_arg) {
+    const uint32_t dbg = DBG ? dbg_arg : 0u;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t* img = pool + img_off[blockIdx.y];
     const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
@@ -769,6 +776,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
     uint32_t* nlist = exb + kBlockCands / 32;
     QCol* scol = reinterpret_cast<QCol*>(nlist + 4);  // the active columns (read at every pass)
+    double* ftab = reinterpret_cast<double*>(scol + kPostMaxCols);  // F = used / (7 + T) by used
     PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
     uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + sizeof(PTok) * H.n_tok);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
@@ -776,6 +784,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     const int nl = H.n_tok + nsets;
     stage(smem, img, sizeof(QConst));
     for (int j = tid; j < H.n_act; j += kPostThreads) scol[j] = cols[j];
+    for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kPostThreads)
+        ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(img)->n_cols);
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
         PTok v;
         v.wq = toks[j].wq;
@@ -983,7 +993,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 const int uk = (int)((used >> (8 * kk)) & 0xFFu);
                 if (uk > 0) {
                     const double S = sum[kk] / (double)uk;
-                    const double F = (double)uk / (double)(kNumFixed + q.n_cols);
+                    const double F = ftab[uk];  // (double)uk / (double)(kNumFixed + q.n_cols)
                     f = (S <= 0.0 && F <= 0.0) ? 0.0f : (float)((2.0 * S * F) / (S + F));
                 }
                 // keyed by idx (idx order = uid order); uids are filled in before the merge
@@ -1149,8 +1159,13 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
                        const int32_t* out_rows, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool, img_off,
-                       blk_begin, blk_end, k, parts, sync, out, out_rows, post_dbg());
+    const uint32_t dbg = post_dbg();
+    if (dbg)
+        hipLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg);
+    else
+        hipLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;
@@ -1176,7 +1191,7 @@ int post_blocks_per_cu(uint32_t var_lds) {
     static thread_local int last_nb = 1;
     if (var_lds == last_key) return last_nb;
     int nb = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel, kPostThreads, post_lds(var_lds));
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel<false>, kPostThreads, post_lds(var_lds));
     last_key = var_lds;
     last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
     return last_nb;

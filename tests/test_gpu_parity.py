@@ -218,6 +218,32 @@ def test_heavy_query_routes_to_stream_scan(hub):
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
+@pytest.fixture(scope="module")
+def wide():
+    """The 20k-user edge-case corpus with a mid-weight user: uid 4242's profile names 3,000
+    friends (3,000 set lists in one K5 workgroup's LDS) and uid 77's adj_list row 3,000 users
+    (an exclusion list far beyond one pass of 256 threads: bisected per block)."""
+    base = tl.synth.Corpus(n_users=20000, seed=77, edge_cases=1)
+    c = tl.corpus_from_desc(base.desc_ptr())
+    c = tl.with_rows(c, user=4242, friends=np.arange(1, 3001, dtype=np.uint32),
+                     adj={77: list(range(19999, 13999, -2)) + [77, 5, 5]})
+    return c, tl.engine(c), tl.Oracle(c)
+
+
+def test_postings_scan_wide_sets_and_long_exclusions(wide):
+    """One K5 call mixing ordinary queries, one with 3,000 friend lists and one with 3,000
+    exclusions spread over many blocks matches the oracle bit for bit, at top-10 and top-64."""
+    c, eng, orc = wide
+    q = [4242, 77, 3, 15000, 4242, 19999, 777]
+    for k in (10, 64):
+        got = eng.recommend_interest_all(q, k)
+        ref = orc.interest(q, k, tl.PF_MODE_ALL, 0)
+        for u, g, r in zip(q, got, ref):
+            assert len(g[0]) == k, u
+            assert list(g[0]) == list(r[0]), (u, k)
+            assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), (u, k)
+
+
 def _hub_queries(c):
     deg = np.diff(c.adj_off)
     return [4242, 999999, 888888, 5] + [int(x) for x in c.adj_uid[np.argsort(-deg)[:3]]]

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 T=$1
 K=${2:-fas_post}
 shift; shift
-B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline $*"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc $*"
 run() { timeout -k 10 120 rocprofv3 --pmc $2 --kernel-include-regex $K -T --output-format csv -d gpurun_out/pmc_$T/$1 -o run -- $B > gpurun_out/pmc_$T/$1.log 2>&1; echo "$1 rc=$?"; }
 mkdir -p gpurun_out/pmc_$T
 run p1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" &&

@@ -603,14 +603,21 @@ def test_batched_sharded_holdout_drivers_equal_sequential():
     eng = pf.FasEngine(ds.desc_ptr(), 0)
     seq = ds.holdout_friends(eng, m["holdout"])
     seq5 = ds.recommendation_tests(eng, m["rectest"], 10)
+    # the reference's own outputs on this corpus (test.cpp:95 prints fixed << setprecision(6);
+    # recommendation_tests.cpp:150-168 the averaged ratios): the batched results are compared
+    # with them directly, not only through the sequential drivers
+    ref = tl.fixture_lines("A", "holdout_friends.txt")
+    ref5 = [float(x) for x in tl.fixture_lines("A", "rectests.txt")[0].split()]
     for nshards, batch in ((1, 64), (3, 1), (3, 64)):
         parts = [ds.eval_holdout_friends(eng, m["holdout"], s, nshards, batch) for s in range(nshards)]
         got = pf.merge_shards(parts)
         assert np.array_equal(got.view(np.uint64), seq.view(np.uint64)), (nshards, batch)
+        assert [f"{v:.6f}" for v in got] == ref, (nshards, batch)
         hp = [ds.eval_recommendation_tests(eng, m["rectest"], 10, s, nshards, batch) for s in range(nshards)]
         hits = pf.merge_shards([h for h, _ in hp])
         club = pf.merge_shards([c for _, c in hp])
         assert (hits >= 0).all()
         assert list(pf.rec_tests_summary(hits, club)) == list(seq5), (nshards, batch)
+        assert list(pf.rec_tests_summary(hits, club)) == ref5, (nshards, batch)
     # the engine's own adjacency is untouched: the sequential driver still matches
     assert np.array_equal(ds.holdout_friends(eng, m["holdout"]).view(np.uint64), seq.view(np.uint64))

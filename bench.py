@@ -13,6 +13,9 @@ generator tools/pokec_synth.cpp, resident in HBM), interest FAS top-10 over ever
          fixed: strong scaling (the north-star ">= 6x at 8 GPUs" is defined on cfg 4).
 --workload cfg2|cfg4 overrides the default (cfg2 at N > 1: N queries per step, one per GPU,
 weak scaling).  value = candidates scored / s over the whole job.
+--workload cfg3 (configs[2]): collaborative FoF top-10, 64 query users per step; value = pair-FAS/s.
+--workload cfg5 (configs[4]): the hold-out evaluation (recommendation_tests.cpp: interest + collab
++ clubs) of 2048 users per step, users split over the ranks; value = hold-out users/s.
 
 Roofline of the dominant kernel (fas_post_kernel, the postings scan, by default;
 fas_scan_kernel, the record-stream scan, with --scan-kernel stream), HIP events around every
@@ -317,6 +320,193 @@ def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s
         dist.destroy_process_group()
 
 
+CFG5_USERS = 2048      # cfg 5 step: one recommendation_tests evaluation of this many sampled users
+CFG5_TOPK = 10
+
+
+def cfg5_dir(users):
+    """The cfg-5 corpus in the reference's on-disk formats (data/, config/; Appendix A), written
+    once per box by rank 0 (the synthetic generator, seed 1) and parsed by every rank."""
+    return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"pf_cfg5_{users}u_seed1")
+
+
+def cpu_baseline_cfg5(ds_dir, users_timed=24):
+    """Oracle run_recommendation_tests_sample (the reference algorithm and its O(N) adj_mod copy
+    per user, recommendation_tests.cpp:68-169) on the SAME full corpus, one core: users/s =
+    (S - 1) extra users / (t(S) - t(1)), the marginal per-user rate without the per-call sampling
+    plan (which favours the CPU: the GPU step pays its plan), plus the whole-call rate."""
+    import torch  # noqa: F401  (loads torch's HIP runtime before the engine's library, as main() does)
+    import pokec_fas as pf
+    import pokec_testlib as tl
+    t0 = time.time()
+    ds = pf.Dataset(ds_dir, 0, cache=os.path.join(ds_dir, "parse_r0.bin"))
+    orc = tl.Oracle(None, desc_ptr=ds.desc_ptr())
+    build_s = time.time() - t0
+    t = time.perf_counter()
+    orc.recommendation_tests(1, CFG5_TOPK)
+    t1 = time.perf_counter() - t
+    orc.fas_calls(True)
+    t = time.perf_counter()
+    orc.recommendation_tests(users_timed, CFG5_TOPK)
+    tn = time.perf_counter() - t
+    calls = orc.fas_calls(True)
+    orc.close()
+    ds.close()
+    marg = (users_timed - 1) / (tn - t1) if tn > t1 else None
+    return {"value": marg, "unit": "hold-out users/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+            "whole_call_users_per_s": users_timed / tn, "pair_fas_per_s": calls / tn, "fas_calls": calls,
+            "sample": f"run_recommendation_tests_sample over {users_timed} users (graph, collaborative, interest, "
+                      f"clubs at limit 5000, top-{CFG5_TOPK}) on the same full corpus, oracle/refcpu.cpp -O3, one "
+                      f"core; value = {users_timed - 1} users / (t({users_timed}) - t(1)) = "
+                      f"{users_timed - 1} / ({tn:.2f} - {t1:.2f}) s; {build_s:.1f}s load + map build untimed"}
+
+
+def run_cfg5(args, world, rank, local):
+    """cfg 5 (BASELINE configs[4]): the full pipeline's hold-out evaluation on the whole corpus.
+    A step = run_recommendation_tests_sample over CFG5_USERS sampled users (recommendation_tests.cpp:
+    68-169: graph = interest FoF, collaborative and clubs at limit 5000, top-10 each, the user's
+    own friend row edited), batched through the device job pipeline (K3 gathers, K6 images, K1'
+    pairs, K4' sums, K7 clubs, K8 top-k), plan entries split over the ranks (i % world == rank;
+    strong scaling), the per-user hits all-gathered and averaged in plan order on rank 0 (the
+    sequential driver's bits).  value = users evaluated / s."""
+    import synth
+    d = cfg5_dir(args.users)
+    marker = os.path.join(d, "written")
+    t0 = time.time()
+    if rank == 0 and not os.path.exists(marker):
+        c = synth.Corpus(n_users=args.users, seed=1, edge_cases=0, threads=16)
+        c.write_reference_files(d)
+        del c
+        with open(marker, "w") as f:
+            f.write("ok\n")
+    while not os.path.exists(marker):  # the other ranks wait for rank 0's files
+        if time.time() - t0 > 900:
+            raise RuntimeError("cfg5 corpus files not written")
+        time.sleep(1.0)
+    write_s = time.time() - t0
+    log(f"[rank {rank}] cfg5 corpus files ready after {write_s:.1f}s")
+    base, pmc, pmc_err = None, None, "not run (N > 1 or --no-pmc)"
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            base = cpu_baseline_cfg5(d)
+            log(f"cpu baseline: {base['value']} users/s ({base['sample']})")
+        if not args.no_pmc:
+            pmc, pmc_err = pmc_pass(args, "fas_pairs_kernel")
+            if pmc_err:
+                log(f"pmc pass: {pmc_err}")
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import pokec_fas as pf
+    t1 = time.time()
+    ds = pf.Dataset(d, 0, cache=os.path.join(d, f"parse_r{rank}.bin"))
+    eng = pf.FasEngine(ds.desc_ptr(), local)
+    open_s = time.time() - t1
+    log(f"[rank {rank}] dataset + engine open {open_s:.1f}s")
+    S, steps, warm = CFG5_USERS, args.steps, args.warmup
+
+    def gather(a):
+        if world == 1:
+            return [a]
+        t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return [p.cpu().numpy() for p in parts]
+
+    def step():
+        hits, club = ds.eval_recommendation_tests(eng, S, CFG5_TOPK, rank, world, 128)
+        hits = pf.merge_shards(gather(hits))
+        club = pf.merge_shards(gather(club))
+        return pf.rec_tests_summary(hits, club), len(hits)
+
+    for _ in range(warm):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    eng.jobs_stats_reset(time_pairs=True, count=False)
+    ts = time.perf_counter()
+    for _ in range(steps):
+        summary, n_eval = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - ts
+    timing = eng.jobs_stats()
+    eng.jobs_stats_reset(time_pairs=False, count=True)
+    step()  # untimed replay: pair and byte counts of one step on this rank
+    st = eng.jobs_stats()
+    eng.jobs_stats_reset(time_pairs=False, count=False)
+    selfcheck = None
+    if world == 1:  # the batched driver against the sequential one on a small sample (untimed)
+        h, c = ds.eval_recommendation_tests(eng, 64, CFG5_TOPK, 0, 1, 128)
+        selfcheck = list(pf.rec_tests_summary(h, c)) == list(ds.recommendation_tests(eng, 64, CFG5_TOPK))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([st["pairs"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        st["pairs"] = float(c.item())
+    launches = timing["pair_launches"]
+    avg_ms = timing["pair_ms"] / launches if launches else None
+    launches_per_step = launches / steps if steps else 0
+    phys = ((st["pair_record_bytes"] + st["pair_image_bytes"]) / launches_per_step
+            if launches_per_step else None)
+    alg_pl = st["pair_alg_bytes"] / launches_per_step if launches_per_step else None
+
+    def rate(b):
+        return None if (b is None or not avg_ms) else b / (avg_ms * 1e-3) / 1e9
+
+    achieved = rate(phys)
+    traffic = pmc["bytes_per_launch"] if pmc else None
+    value = n_eval * steps / elapsed
+    rec = {
+        "metric": METRIC, "value": value, "unit": "hold-out users/s", "n_gpus": world, "steps": steps,
+        "warmup": warm, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded Pokec-shaped corpus in the reference's CSV formats, tools/pokec_synth.cpp; "
+                "no Pokec data offline)",
+        "config": {"workload": f"cfg5: run_recommendation_tests_sample over {S} users per step (graph/interest + "
+                               f"collaborative + clubs, limit 5000, top-{CFG5_TOPK}) on the full {args.users}-user "
+                               f"corpus" + (f", users split over {world} GPUs" if world > 1 else ""),
+                   "workload_key": f"cfg5_rectests_{args.users}users_s{S}_top{CFG5_TOPK}_world{world}",
+                   "n_users": args.users, "users_per_step": S, "topk": CFG5_TOPK, "limit": 5000,
+                   "parallelism": f"hold-out users x{world}" + (" + all_gather" if world > 1 else "")},
+        "rectests_summary": [float(x) for x in summary], "pairs_per_step": st["pairs"],
+        "pair_fas_per_s": st["pairs"] / (elapsed / steps) if elapsed > 0 else None,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "fas_pairs_kernel", "avg_launch_ms": avg_ms, "timed_launches": launches,
+                     "bytes_per_launch": phys,
+                     "bytes_model": "pf_jobs_stats: per scored pair the candidate's 48-B tile-store headers + record "
+                                    "words (K1' walks the record), per 256-pair block the staged query image",
+                     "dram_gbs": rate(traffic),
+                     "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
+                     "traffic_source": pmc if pmc else pmc_err,
+                     "alg_effective_gbs": rate(alg_pl),
+                     "alg_bytes_per_launch": alg_pl,
+                     "pair_kernel_share_of_step": (timing["pair_ms"] / (elapsed * 1e3)) if elapsed > 0 else None},
+        "selfcheck_vs_sequential_64_users": selfcheck, "files_s": write_s, "open_s": open_s,
+    }
+    if rank == 0 and world == 1 and base is not None:
+        rec["cpu_baseline"] = base
+        rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None
+    elif rank == 0:
+        rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    eng.close()
+    ds.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -324,12 +514,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default=None,
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "cfg5"], default=None,
                     help="cfg2: N queries per step (1 per GPU, weak scaling; the default at N = 1); "
                          "cfg3: collaborative FoF top-10, 64 queries per step (limit 10000), query users "
                          "split over the ranks; "
                          "cfg4: a fixed batch of 1024 queries per step over the sharded candidates (strong "
-                         "scaling; the default at N > 1)")
+                         "scaling; the default at N > 1); "
+                         "cfg5: hold-out evaluation (recommendation_tests: interest + collab + clubs) of 2048 "
+                         "users per step, users split over the ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass (traffic = null)")
     ap.add_argument("--time-every", type=int, default=1,
@@ -345,6 +537,8 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
+    if args.workload == "cfg5":
+        return run_cfg5(args, world, rank, local)
     import synth
 
     t0 = time.time()

@@ -1,0 +1,129 @@
+"""The FastAPI wrapper (recommendation-system-pokec_amd/app.py; the reference's python/app.py).
+
+CPU: the wrapper's process handling and routes against a stand-in backend that speaks the
+api_cli protocol (progress lines, READY, one JSON line per input line).
+GPU: the real pokec_api_cli on the golden api corpus; every route answers what the reference
+api_cli printed for the same request (tests/golden/api transcript)."""
+import gzip
+import json
+import os
+import sys
+import textwrap
+
+import pytest
+
+import pokec_testlib as tl
+
+sys.path.insert(0, os.path.join(tl.ROOT, "recommendation-system-pokec_amd"))
+
+FAKE = textwrap.dedent(r'''
+    import json, sys, time
+    print("Loaded 0 users ", flush=True)
+    print("Loaded 3 users total", flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "slow":
+        time.sleep(30)
+    print("READY", flush=True)
+    recs = {"graph": [{"id": i, "score": 1.0 - i / 100} for i in range(1, 31)],
+            "collaborative": [{"id": 7, "score": 0.5}], "interest": [], "clubs": [{"id": 3, "score": 0.25, "name": "x"}]}
+    for line in sys.stdin:
+        p = line.split()
+        if not p:
+            print("{}", flush=True)
+        elif p[0] == "PING":
+            print('{"ok":true}', flush=True)
+        elif p[0] == "EXIT":
+            print('{"ok":true, "exiting":true}', flush=True)
+            break
+        elif p[0] == "USER" and len(p) == 2 and p[1] == "1":
+            print(json.dumps({"profile": {"user_id": 1}, "recommendations": recs}), flush=True)
+        elif p[0] == "USER" and len(p) == 2 and p[1] == "66":
+            print("not json", flush=True)
+        elif p[0] == "USER" and len(p) == 2 and p[1] == "77":
+            time.sleep(3)
+            print("{}", flush=True)
+        elif p[0] == "USER" and len(p) == 2:
+            print(json.dumps({"error": "not found", "user_id": int(p[1])}), flush=True)
+        else:
+            print('{"error":"unknown command"}', flush=True)
+''')
+
+
+@pytest.fixture()
+def fake_cli(tmp_path):
+    p = tmp_path / "fake_cli.py"
+    p.write_text(FAKE)
+    return [sys.executable, str(p)]
+
+
+def test_app_routes_against_protocol_stand_in(fake_cli, tmp_path):
+    from fastapi.testclient import TestClient
+    import app as appmod
+    (tmp_path / "config.yaml").write_text("load_users: 3\nserver:\n  port: 8123\n")
+    a = appmod.create_app(str(tmp_path), cli_cmd=fake_cli, request_timeout=2.0)
+    assert a.state.cli.log == ["Loaded 0 users ", "Loaded 3 users total"]
+    with TestClient(a) as c:
+        assert c.get("/health").json() == {"status": "ok", "load_users": 3}
+        assert "Loaded users: 3" in c.get("/").text
+        j = c.get("/api/user/1").json()
+        assert j["profile"] == {"user_id": 1}
+        assert c.get("/api/user/5").json() == {"error": "not found", "user_id": 5}
+        # /api/recommend/<kind>: recommendations[kind][:topk], topk 20 by default (app.py:122-144)
+        g = c.get("/api/recommend/graph/1").json()
+        assert len(g) == 20 and g[0] == {"id": 1, "score": 0.99}
+        assert len(c.get("/api/recommend/graph/1", params={"topk": 5}).json()) == 5
+        assert c.get("/api/recommend/collab/1").json() == [{"id": 7, "score": 0.5}]
+        assert c.get("/api/recommend/interest/1").json() == []
+        assert c.get("/api/recommend/clubs/1").json() == [{"id": 3, "score": 0.25, "name": "x"}]
+        assert c.get("/api/recommend/graph/5").json() == []  # unknown user: no recommendations key
+        # a line that is not JSON, then a backend slower than the request timeout: 500 each
+        r = c.get("/api/user/66")
+        assert r.status_code == 500 and "invalid JSON" in r.json()["detail"]
+        r = c.get("/api/user/77")
+        assert r.status_code == 500 and "timeout" in r.json()["detail"]
+        # the late answer is skipped, not handed to the next request
+        assert c.get("/api/user/1").json()["profile"] == {"user_id": 1}
+        assert c.get("/api/user/abc").status_code == 422
+    assert a.state.cli.p.poll() is not None  # shutdown ended the backend
+
+
+def test_app_backend_without_ready_fails(fake_cli, tmp_path):
+    import app as appmod
+    with pytest.raises(RuntimeError, match="READY"):
+        appmod.create_app(str(tmp_path), cli_cmd=fake_cli + ["slow"], ready_timeout=1.0)
+    with pytest.raises(RuntimeError, match="READY"):
+        appmod.create_app(str(tmp_path), cli_cmd=[sys.executable, "-c", "print('boom')"], ready_timeout=5.0)
+
+
+def test_app_config_defaults(tmp_path):
+    import app as appmod
+    assert appmod.load_config(str(tmp_path)) == {"load_users": 100000, "host": "0.0.0.0", "port": 8000}
+
+
+@pytest.mark.gpu
+def test_app_over_engine_cli_matches_reference_transcript(tmp_path):
+    """pokec_api_cli (the engine) behind the wrapper: /api/user answers the reference api_cli's
+    JSON line for each USER request of the golden transcript, and /api/recommend/<kind> its
+    recommendation lists."""
+    from fastapi.testclient import TestClient
+    import app as appmod
+    m = tl.manifest()["api_cli"]
+    with gzip.open(os.path.join(tl.GOLDEN, "api", "transcript_stdin.txt.gz"), "rt") as f:
+        cmds = [ln.rstrip("\n") for ln in f]
+    with gzip.open(os.path.join(tl.GOLDEN, "api", "transcript_stdout.txt.gz"), "rt") as f:
+        out = [ln.rstrip("\n") for ln in f]
+    out = out[out.index("READY") + 1:]
+    tl.regen_reference_dir("api", str(tmp_path))
+    a = appmod.create_app(str(tmp_path), load_users=int(m["load_users"]))
+    checked = 0
+    with TestClient(a) as c:
+        for cmd, want in zip(cmds, out):
+            p = cmd.split()
+            if len(p) != 2 or p[0] != "USER" or not p[1].lstrip("-").isdigit() or int(p[1]) < 0:
+                continue  # non-USER lines and negative ids do not map onto the /api/user/{uid} route
+            w = json.loads(want)
+            assert c.get(f"/api/user/{p[1]}").json() == w, cmd
+            if "recommendations" in w:
+                for kind, key in appmod.KINDS.items():
+                    assert c.get(f"/api/recommend/{kind}/{p[1]}").json() == w["recommendations"][key][:20]
+            checked += 1
+    assert checked >= 5

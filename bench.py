@@ -177,7 +177,10 @@ def pmc_pass(args, kernel_name):
                     if row.get("Counter_Name") == "FETCH_SIZE" and kernel_name in row.get("Kernel_Name", ""):
                         vals.append((int(row.get("Dispatch_Id", len(vals))), float(row["Counter_Value"])))
         vals.sort()
-        vals = [v for _, v in vals][-args.steps:]  # the timed launches (the warmup ones come first)
+        if args.workload in ("cfg2", "cfg4"):
+            vals = [v for _, v in vals][-args.steps:]  # the timed launches (the warmup ones come first)
+        else:  # cfg3 / cfg5: several pair launches per step, warmup steps of the same kind: all of them
+            vals = [v for _, v in vals]
         if not vals:
             return None, "no FETCH_SIZE rows"
         mean = sum(vals) / len(vals)

@@ -338,7 +338,6 @@ def cpu_baseline_cfg5(ds_dir, users_timed=24):
     per user, recommendation_tests.cpp:68-169) on the SAME full corpus, one core: users/s =
     (S - 1) extra users / (t(S) - t(1)), the marginal per-user rate without the per-call sampling
     plan (which favours the CPU: the GPU step pays its plan), plus the whole-call rate."""
-    import torch  # noqa: F401  (loads torch's HIP runtime before the engine's library, as main() does)
     import pokec_fas as pf
     import pokec_testlib as tl
     t0 = time.time()

@@ -31,7 +31,10 @@ __device__ __forceinline__ double term_of(const QConst& q, int slot, double s) {
 }
 
 // recommender.cpp:119-128: inter counted over B (with duplicates) / (sqrt|A| sqrt|B|), as float
-__device__ __forceinline__ double set_term(const QConst& q, int slot, int inter, int nb, double sqrt_na) {
+// (out of line, like ratio_term: the fixed-term phase calls them for four candidates per thread,
+// and eight inlined exp + division chains made the scan's hot code larger than the instruction cache)
+static __device__ __attribute__((noinline)) double set_term(const QConst& q, int slot, int inter, int nb,
+                                                             double sqrt_na) {
     const double den = sqrt_na * sqrt((double)nb);
     const double s = den <= 0.0 ? 0.0 : (double)(float)((double)inter / den);
     return term_of(q, slot, s);
@@ -45,7 +48,7 @@ __device__ __forceinline__ double text_term(const QConst& q, int t, double dot, 
 }
 
 // completion / age ratio outside the host table (recommender_similarity.cpp:40-53)
-__device__ __forceinline__ double ratio_term(const QConst& q, int slot, int a, int b) {
+static __device__ __attribute__((noinline)) double ratio_term(const QConst& q, int slot, int a, int b) {
     const int lo = a < b ? a : b, hi = a < b ? b : a;
     return term_of(q, slot, (double)lo / (double)hi);
 }
@@ -166,10 +169,9 @@ __device__ __forceinline__ uint64_t wave_sort64(uint64_t x, int lane) {
 // The wave keeps the 64 smallest keys seen so far, sorted ascending across lanes
 // (lane i = i-th best); a top-k caller reads lanes < k.  Few qualifying keys are
 // inserted one by one; many are merged with a bitonic sort + merge (O(log^2 64)).
-__device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int lane) {
-    uint64_t thr = rdlane64(list, k - 1);
-    uint64_t m = __ballot(x < thr);
-    if (!m) return;
+// Out of line: the scan tails inline dozens of pushes, and only the first test is hot.
+static __device__ __attribute__((noinline)) uint64_t topk_insert(uint64_t list, uint64_t x, uint64_t thr, uint64_t m,
+                                                                  int k, int lane) {
     if (__popcll(m) > 3) {
         uint64_t xs = wave_sort64(x < thr ? x : ~0ull, lane);
         const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)xs, 63 - lane);
@@ -181,8 +183,7 @@ __device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int
             const uint64_t z = shfl_xor64(y, j);
             y = (lane & j) ? (y < z ? z : y) : (y < z ? y : z);
         }
-        list = y;
-        return;
+        return y;
     }
     while (m) {
         const int src = __ffsll((unsigned long long)m) - 1;
@@ -196,6 +197,13 @@ __device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int
             thr = rdlane64(list, k - 1);
         }
     }
+    return list;
+}
+
+__device__ __forceinline__ void topk_push(uint64_t& list, uint64_t x, int k, int lane) {
+    const uint64_t thr = rdlane64(list, k - 1);
+    const uint64_t m = __ballot(x < thr);
+    if (m) list = topk_insert(list, x, thr, m, k, lane);
 }
 
 }  // namespace pf

@@ -691,7 +691,10 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
 // the block's token prefix gpre: a thread finds the list of a flat entry in 3 bisection
 // steps.  One group of 512 flat entries: a thread's two (list - js or -1, entry, norm),
 // loaded together.
-constexpr int kGroupU = 2;  // flat entries per thread in a group (3: 218 us vs 213)
+#ifndef PF_K5_GROUP_U
+#define PF_K5_GROUP_U 2
+#endif
+constexpr int kGroupU = PF_K5_GROUP_U;  // flat entries per thread in a group (3: 218 us vs 213)
 struct Group {
     int jj[kGroupU];
     uint32_t ent[kGroupU];
@@ -799,7 +802,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
 #ifdef PF_K5_TIMERS
-    uint64_t tacc[12] = {0};
+    uint64_t tacc[14] = {0};
     uint64_t tprev = clock64();
     const uint64_t tstart = tprev;
 #endif
@@ -919,6 +922,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                         nrm[p] = nv;
                     }
                 });
+                K5T(12);
                 {  // one load site (copies of in-flight registers at a join would wait for them)
                     int njs = 0, nnj = 0;  // the next pass (none: 0 tokens)
                     if (!last) {
@@ -1019,8 +1023,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
 #ifdef PF_K5_TIMERS
     tacc[11] = clock64() - tstart;
     if (lane == 0) {
-        for (int i = 0; i < 12; ++i) atomicAdd(&g_k5t[i], (unsigned long long)tacc[i]);
-        atomicAdd(&g_k5t[12], 1ull);
+        for (int i = 0; i < 14; ++i) atomicAdd(&g_k5t[i], (unsigned long long)tacc[i]);
+        atomicAdd(&g_k5t[15], 1ull);
     }
 #endif
     // idx -> uid in the wave's list (the same order: uid ascending == idx ascending)
@@ -1172,11 +1176,11 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
         unsigned long long t[16];
         hipStreamSynchronize(s);
         hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k5t), sizeof(t));
-        static const char* nm[12] = {"ranges+hdr", "barriers", "excl+sets", "fixed", "walk", "walk-bar",
-                                     "compact", "dense", "pass-bar", "owner-add", "fas+topk", "total"};
+        static const char* nm[14] = {"ranges+hdr", "barriers", "excl+sets", "fixed", "next-load", "walk-bar",
+                                     "compact", "dense", "pass-bar", "owner-add", "fas+topk", "total", "walk", "-"};
         if (++calls % 10 == 0) {
             fprintf(stderr, "k5t per wave (clock64):");
-            for (int i = 0; i < 12; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[12]);
+            for (int i = 0; i < 13; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[15]);
             fprintf(stderr, "\n");
         }
         const unsigned long long z[16] = {0};

@@ -68,6 +68,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise FasError(f"{LIB_PATH} missing: build it with `make -C {HERE}` (no CPU fallback exists)")
+        # One HIP runtime per process: torch's libraries ask for "libamdhip64.so" (its bundled
+        # copy), this library for "libamdhip64.so.7".  Loaded in that order the engine binds to
+        # torch's copy; the other way round the process ends up with two HIP/HSA runtimes and
+        # whichever initialises second finds no device.  So torch, when present, goes first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         V, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
         L.pf_abi_version.restype = ctypes.c_int

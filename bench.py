@@ -420,7 +420,7 @@ def run_cfg5(args, world, rank, local):
         return [p.cpu().numpy() for p in parts]
 
     def step():
-        hits, club = ds.eval_recommendation_tests(eng, S, CFG5_TOPK, rank, world, 128)
+        hits, club = ds.eval_recommendation_tests(eng, S, CFG5_TOPK, rank, world, args.cfg5_batch)
         hits = pf.merge_shards(gather(hits))
         club = pf.merge_shards(gather(club))
         return pf.rec_tests_summary(hits, club), len(hits)
@@ -524,6 +524,9 @@ def main():
                          "scaling; the default at N > 1); "
                          "cfg5: hold-out evaluation (recommendation_tests: interest + collab + clubs) of 2048 "
                          "users per step, users split over the ranks")
+    ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
+                    help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
+                         "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass (traffic = null)")
     ap.add_argument("--time-every", type=int, default=1,

@@ -97,8 +97,21 @@ struct JobsState {
     size_t view_over_n = 0;
     DevView view{};
     DBuf d_view_node, d_view_ver, d_view_off, d_view_len, d_view_nbr;
-    DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr, d_ncand, d_keys, d_acc, d_touched, d_fail;
-    PinBuf h_plan, h_out;
+    // per-chunk workspaces, double-buffered: chunk i + 1 is planned and launched while chunk i
+    // runs (run_all in pf_jobs_plan.cpp); the clubs accumulators are shared (stream order)
+    struct Ws {
+        DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr, d_ncand, d_keys, d_fail;
+        PinBuf h_plan, h_out;
+        hipEvent_t done = nullptr;  // recorded after the chunk's result copies
+        // what the chunk's unpack needs (host)
+        bool active = false;
+        std::vector<DevJob> dj;
+        std::vector<int32_t> jmap, tpos;
+        std::vector<size_t> full, full_off;
+        size_t o_cnt = 0, o_keys = 0, o_fail = 0;
+        int ktop = 1;
+    } ws[2];
+    DBuf d_acc, d_touched;
     int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
     bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)

@@ -439,11 +439,12 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
             tf = (int32_t)(w >> 24);
             e = make_entry(kTagTok | ((uint32_t)t << kTidBits) | (w & kTidMask), kTokVal | k | ((uint32_t)t << kTidBits));
         } else {
-            tid_ = (int32_t)word_at(st, l, qw, nset + 2 * k);
+            const uint32_t w0 = word_at(st, l, qw, nset + 2 * k);  // tid | col << 26
+            tid_ = (int32_t)(w0 & kWideTidMask);
             const uint32_t w = word_at(st, l, qw, nset + 2 * k + 1);
             t = (int)(w & 0xFFu);
             tf = (int32_t)w >> 8;
-            e = make_entry((uint32_t)tid_, (uint32_t)t | (k << 8)) | (2ull << 62);
+            e = make_entry(w0, (uint32_t)t | (k << 8)) | (2ull << 62);
         }
         const double idf = idf_of(g, t, tid_);
         QVal v;

@@ -25,6 +25,7 @@ namespace {
 constexpr int kDevTopK = kMaxTopK;           // K8 keeps up to 64 keys per job
 constexpr int64_t kChunkElems = 192ll << 20; // element workspace per chunk (x 12 B)
 constexpr int64_t kChunkHt = 128ll << 20;    // gather hash tables per chunk (int32 words)
+constexpr size_t kPipeJobs = 1024;           // calls of this many jobs or more run as pipelined chunks
 constexpr uint32_t kStageLimitJobs = 48 * 1024;  // as pf_api.cpp kStageLimit (LDS-staged tables)
 
 int32_t node_of(const pf_ctx* c, int32_t uid) {
@@ -388,8 +389,10 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
             for (int32_t x : *Jb.view.own_row) p.own.push_back(node_of(c, x));
         }
     }
-    if (ru)
+    if (ru) {
+        p.F.reserve(ru->size());
         for (int32_t x : *ru) p.F.push_back(node_of(c, x));
+    }
     const int64_t L = std::max<int32_t>(Jb.limit, 1);
     // |row(node)| under the view: the base CSR's length unless an edit or the view covers it
     const bool plain = c->jb.edited.empty() && !Jb.view.over && !Jb.view.own_row;
@@ -419,15 +422,32 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
         return;
     }
     // collab / clubs: sim_u_f over the distinct friends with a profile (recommender_graph.cpp:132-136)
-    std::unordered_map<int32_t, int32_t> seen;
-    for (int32_t f : p.F) {
-        if (f < 0 || f >= hc.n) { p.fpos.push_back(-1); continue; }
-        auto it = seen.find(f);
-        if (it == seen.end()) {
-            it = seen.emplace(f, (int32_t)p.fd.size()).first;
-            p.fd.push_back(f);
+    p.fpos.reserve(p.F.size());
+    p.fd.reserve(p.F.size());
+    if (p.F.size() <= 64) {  // the common case: a linear scan beats a hash map's allocations
+        for (int32_t f : p.F) {
+            if (f < 0 || f >= hc.n) { p.fpos.push_back(-1); continue; }
+            int32_t pos = -1;
+            for (size_t r = 0; r < p.fd.size(); ++r)
+                if (p.fd[r] == f) { pos = (int32_t)r; break; }
+            if (pos < 0) {
+                pos = (int32_t)p.fd.size();
+                p.fd.push_back(f);
+            }
+            p.fpos.push_back(pos);
         }
-        p.fpos.push_back(it->second);
+    } else {
+        std::unordered_map<int32_t, int32_t> seen;
+        seen.reserve(p.F.size());
+        for (int32_t f : p.F) {
+            if (f < 0 || f >= hc.n) { p.fpos.push_back(-1); continue; }
+            auto it = seen.find(f);
+            if (it == seen.end()) {
+                it = seen.emplace(f, (int32_t)p.fd.size()).first;
+                p.fd.push_back(f);
+            }
+            p.fpos.push_back(it->second);
+        }
     }
     if (Jb.kind == kJobCollab) {
         p.kind = kDjCollab;
@@ -448,10 +468,12 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
     }
 }
 
-// Runs jobs[b, e) (planned in P) on the device; fills jobs[i].out, or raw lists in raw_out.
-int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, size_t e,
-              std::vector<std::vector<int32_t>>* raw_out) {
+// Launches jobs[b, e) (planned in P) on the device with workspaces W: every stage and the
+// result copies are queued on the context's stream and W.done is recorded after them;
+// finish_chunk waits for it and fills jobs[i].out (or raw lists in raw_out).
+int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, size_t e, JobsState::Ws& W) {
     auto& J = c->jb;
+    W.active = false;
     const HostCorpus& hc = c->hc;
     const bool packed = c->hs.packed;
     HpLap hl;
@@ -479,6 +501,18 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     };
     std::vector<int32_t> jix_collab, jix_clubs, jix_topk;
     int max_cap_collab = 0, ktop = 1;
+    {
+        size_t nb = 0, words = 0;  // the blocks and pool words this chunk appends (one allocation)
+        for (size_t i = b; i < e; ++i) {
+            const JP& p = P[i];
+            if (p.kind < 0) continue;
+            const size_t ch = (size_t)(p.cap + 255) / 256;
+            nb += ch * (1 + p.fd.size()) + 1 + p.fd.size() + (size_t)p.seqlen / 256;
+            words += p.own.size() + p.F.size() + 2 * p.fd.size();
+        }
+        blocks.reserve(nb);
+        pool32.reserve(words + 1);
+    }
     for (size_t i = b; i < e; ++i) {
         JP& p = P[i];
         if (p.kind < 0) continue;
@@ -555,6 +589,7 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         jmap.push_back((int32_t)i);
     }
     if (dj.empty()) return PF_OK;
+    if (W.done == nullptr) HIPCHK(c, hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
     if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
     // ---- images (pf_api.cpp plan_images layout); the ones K6 builds in LDS first
     const uint32_t ntab = packed ? 1u : 3u;
@@ -626,8 +661,8 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
     const size_t total = a16z(o_jt + jix_topk.size() * 4) + 16;
-    HIPCHK(c, J.h_plan.ensure(total));
-    uint8_t* h = J.h_plan.as<uint8_t>();
+    HIPCHK(c, W.h_plan.ensure(total));
+    uint8_t* h = W.h_plan.as<uint8_t>();
     auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(h + o, src, bytes); };
     put(o_dj, dj.data(), dj.size() * sizeof(DevJob));
     put(o_p32, pool32.data(), pool32.size() * 4);
@@ -638,9 +673,9 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
-    HIPCHK(c, J.d_plan.reserve(total));
-    HIPCHK(c, hipMemcpyAsync(J.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
-    uint8_t* d = J.d_plan.as<uint8_t>();
+    HIPCHK(c, W.d_plan.reserve(total));
+    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
+    uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
     const int32_t* d_p32 = reinterpret_cast<const int32_t*>(d + o_p32);
     const int64_t* d_p64 = reinterpret_cast<const int64_t*>(d + o_p64);
@@ -653,17 +688,17 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
     hl.lap(kHpPack);
     // ---- workspaces
     const size_t nE = (size_t)std::max<int64_t>(E, 1);
-    HIPCHK(c, J.d_slots.reserve(nE * 4));
-    HIPCHK(c, J.d_ids.reserve(nE * 4));
-    HIPCHK(c, J.d_fl.reserve(nE * 4));
-    HIPCHK(c, J.d_ht.reserve((size_t)std::max<int64_t>(HT, 1) * 4));
-    HIPCHK(c, J.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
-    HIPCHK(c, J.d_img.reserve(std::max<size_t>(ipool, 16)));
-    HIPCHK(c, J.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
-    HIPCHK(c, J.d_ncand.reserve(dj.size() * 4));
-    HIPCHK(c, J.d_keys.reserve(dj.size() * (size_t)ktop * 8));
-    HIPCHK(c, J.d_fail.ensure(16));
-    HIPCHK(c, hipMemsetAsync(J.d_fail.p, 0, 16, c->stream));
+    HIPCHK(c, W.d_slots.reserve(nE * 4));
+    HIPCHK(c, W.d_ids.reserve(nE * 4));
+    HIPCHK(c, W.d_fl.reserve(nE * 4));
+    HIPCHK(c, W.d_ht.reserve((size_t)std::max<int64_t>(HT, 1) * 4));
+    HIPCHK(c, W.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
+    HIPCHK(c, W.d_img.reserve(std::max<size_t>(ipool, 16)));
+    HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
+    HIPCHK(c, W.d_ncand.reserve(dj.size() * 4));
+    HIPCHK(c, W.d_keys.reserve(dj.size() * (size_t)ktop * 8));
+    HIPCHK(c, W.d_fail.ensure(16));
+    HIPCHK(c, hipMemsetAsync(W.d_fail.p, 0, 16, c->stream));
     hl.lap(kHpPlan);  // workspaces
     if (!jix_clubs.empty()) {
         const int64_t want = (int64_t)jix_clubs.size();
@@ -677,11 +712,11 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         }
     }
     // ---- the stages, in stream order
-    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, J.d_img.as<uint8_t>(),
-                             J.d_scr.as<uint32_t>(), J.d_fail.as<int32_t>(), c->stream));
-    HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, J.d_ht.as<int32_t>(),
-                            J.d_seq.as<int32_t>(), J.d_slots.as<int32_t>(), J.d_ids.as<int32_t>(),
-                            J.d_ncand.as<int32_t>(), c->stream));
+    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
+                             W.d_scr.as<uint32_t>(), W.d_fail.as<int32_t>(), c->stream));
+    HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
+                            W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
+                            W.d_ncand.as<int32_t>(), c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {
@@ -695,14 +730,14 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         ++J.stat_used;
         HIPCHK(c, hipEventRecord(pe0, c->stream));
     }
-    HIPCHK(c, launch_pairs(c->ds, J.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(),
-                           J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
+    HIPCHK(c, launch_pairs(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(),
+                           W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
     if (pe1) {
         HIPCHK(c, hipEventRecord(pe1, c->stream));
         ++J.st_launches;
     }
     if (J.stats_count && !blocks.empty()) {
-        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), J.d_slots.as<int32_t>(),
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(),
                                     J.d_stats.as<unsigned long long>(), c->stream));
         for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
             const QImageRef& r = refs[pb.qimg];
@@ -712,13 +747,13 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
-    HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, J.d_fl.as<float>(),
-                            J.d_slots.as<int32_t>(), J.d_fl.as<float>(), c->stream));
-    HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, J.d_fl.as<float>(),
-                           J.d_acc.as<double>(), J.d_touched.as<int32_t>(), J.d_fl.as<float>(), J.d_ids.as<int32_t>(),
-                           J.d_ncand.as<int32_t>(), (int64_t)J.js.n_club_ids, c->stream));
-    HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), J.d_fl.as<float>(), J.d_ids.as<int32_t>(),
-                              J.d_slots.as<int32_t>(), J.d_ncand.as<int32_t>(), J.d_keys.as<uint64_t>(), ktop,
+    HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
+                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
+    HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
+                           J.d_acc.as<double>(), J.d_touched.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
+                           W.d_ncand.as<int32_t>(), (int64_t)J.js.n_club_ids, c->stream));
+    HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
+                              W.d_slots.as<int32_t>(), W.d_ncand.as<int32_t>(), W.d_keys.as<uint64_t>(), ktop,
                               c->stream));
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
@@ -732,24 +767,51 @@ int run_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b, s
         full_off.push_back(ob);
         ob += a16z((size_t)std::max(dj[x].cap, dj[x].kind == kDjClubs ? J.js.n_club_ids : 0) * 12);
     }
-    HIPCHK(c, J.h_out.ensure(ob));
-    uint8_t* ho = J.h_out.as<uint8_t>();
+    HIPCHK(c, W.h_out.ensure(ob));
+    uint8_t* ho = W.h_out.as<uint8_t>();
     const size_t o_cnt = 0, o_keys = a16z(dj.size() * 4), o_fail = o_keys + a16z(dj.size() * (size_t)ktop * 8);
-    HIPCHK(c, hipMemcpyAsync(ho + o_cnt, J.d_ncand.p, dj.size() * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ho + o_keys, J.d_keys.p, dj.size() * (size_t)ktop * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ho + o_fail, J.d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho + o_cnt, W.d_ncand.p, dj.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho + o_keys, W.d_keys.p, dj.size() * (size_t)ktop * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho + o_fail, W.d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
     for (size_t q = 0; q < full.size(); ++q) {
         const DevJob& x = dj[full[q]];
         const size_t cnt = (size_t)std::max(x.cap, x.kind == kDjClubs ? J.js.n_club_ids : 0);
         uint8_t* dst = ho + full_off[q];
-        HIPCHK(c, hipMemcpyAsync(dst, J.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, J.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, J.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
+        HIPCHK(c, hipMemcpyAsync(dst, W.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, W.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, W.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
                                  c->stream));
     }
+    HIPCHK(c, hipEventRecord(W.done, c->stream));
     hl.lap(kHpStage2);  // launches issued
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    W.active = true;
+    W.o_cnt = o_cnt;
+    W.o_keys = o_keys;
+    W.o_fail = o_fail;
+    W.ktop = ktop;
+    W.dj.swap(dj);
+    W.jmap.swap(jmap);
+    W.tpos.swap(tpos);
+    W.full.swap(full);
+    W.full_off.swap(full_off);
+    return PF_OK;
+}
+
+int finish_chunk(pf_ctx* c, std::vector<Job>& jobs, JobsState::Ws& W, std::vector<std::vector<int32_t>>* raw_out) {
+    if (!W.active) return PF_OK;
+    W.active = false;
+    auto& J = c->jb;
+    HpLap hl;
+    HIPCHK(c, hipEventSynchronize(W.done));
     hl.lap(kHpGpu);
+    const uint8_t* ho = W.h_out.as<uint8_t>();
+    const std::vector<DevJob>& dj = W.dj;
+    const std::vector<int32_t>& jmap = W.jmap;
+    const std::vector<int32_t>& tpos = W.tpos;
+    const std::vector<size_t>& full = W.full;
+    const std::vector<size_t>& full_off = W.full_off;
+    const size_t o_cnt = W.o_cnt, o_keys = W.o_keys, o_fail = W.o_fail;
+    const int ktop = W.ktop;
     if (*reinterpret_cast<const int32_t*>(ho + o_fail))
         return c->fail(PF_EINTERNAL, "device query table build did not converge");
     const int32_t* cnt = reinterpret_cast<const int32_t*>(ho + o_cnt);
@@ -815,26 +877,53 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     rc = sync_view(c, over);
     if (rc != PF_OK) return rc;
     HpLap hl;
-    std::vector<JP> P(jobs.size());
-    // 1-hop planning is a few microseconds per job: threads only for large batches (spawning
-    // them costs more than planning a 64-user step)
-    par_jobs(jobs.size(), [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 256);
-    hl.lap(kHpPrep);
-    hl.skip();
+    const size_t n = jobs.size();
+    std::vector<JP> P(n);
+    // Chunks of at most chunk_jobs jobs (and the element budgets), double-buffered: chunk i + 1
+    // is planned and launched while chunk i runs on the device, then chunk i is unpacked.
+    // Only large calls are cut: splitting a 64-user cfg-3 step into four chunks made it slower
+    // (1.09 -> 1.50 ms: four times the launches, each too small to fill the GPU; r2n).
+    const size_t chunk_jobs = n < kPipeJobs ? n : std::max<size_t>(kPipeJobs / 2, (n + 2) / 3);
+    int slot = 0;
+    JobsState::Ws* pending = nullptr;
+    auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
+        (void)hipStreamSynchronize(c->stream);
+        J.ws[0].active = J.ws[1].active = false;
+        return code;
+    };
     size_t b = 0;
-    while (b < jobs.size()) {
+    while (b < n) {
+        const size_t lim = std::min(n, b + chunk_jobs);
+        // 1-hop planning is a few microseconds per job: threads only for large chunks
+        // (spawning them costs more than planning a 64-user step)
+        par_jobs(lim - b, [&](size_t i) { if (P[b + i].u < 0 && P[b + i].kind < 0) plan_job(c, jobs[b + i], P[b + i], raw); },
+                 256);
+        hl.lap(kHpPrep);
         size_t e = b;
         int64_t el = 0, ht = 0;
-        while (e < jobs.size()) {
+        while (e < lim) {
             const JP& p = P[e];
             if (e > b && (el + p.elems > kChunkElems || ht + p.ht_words > kChunkHt)) break;
             el += p.elems;
             ht += p.ht_words;
             ++e;
         }
-        rc = run_chunk(c, jobs, P, b, e, raw_out);
-        if (rc != PF_OK) return rc;
+        hl.skip();
+        JobsState::Ws& W = J.ws[slot];
+        rc = launch_chunk(c, jobs, P, b, e, W);
+        if (rc != PF_OK) return drain(rc);
+        if (pending) {
+            rc = finish_chunk(c, jobs, *pending, raw_out);
+            if (rc != PF_OK) return drain(rc);
+        }
+        pending = &W;
+        slot ^= 1;
         b = e;
+        hl.skip();
+    }
+    if (pending) {
+        rc = finish_chunk(c, jobs, *pending, raw_out);
+        if (rc != PF_OK) return drain(rc);
     }
     return PF_OK;
 }

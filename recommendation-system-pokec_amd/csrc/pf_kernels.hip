@@ -38,7 +38,8 @@ struct Walk {
 
 // A token hit is stored as its T2 val plus the candidate's tf:
 //   packed: one word  vi | col << 18 | tf << 24        (the walk's only LDS write)
-//   wide:   two words {col | vi << 8, tf << 8 | col}
+//   wide:   two words {col | vi << 8, tf << 8 | col}; the record's token words are
+//           {tid | col << 26, tf << 8 | col}, the first being the table key
 template <bool PACKED>
 struct HitT;
 template <>

@@ -121,69 +121,11 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
             if (!hc.has_idf[t] || !d->idf_off) continue;
             for (int64_t k = d->idf_off[t]; k < d->idf_off[t + 1]; ++k) hc.idf[t][d->idf_tid[k]] = d->idf_val[k];
         }
-    } else {
-        // recommender.cpp:43-66: df = #profiles whose column map holds the token;
-        // idf = logf(1 + N/(1+df)) in float32, N = number of loaded profiles.
-        const float N = (float)n;
-        std::vector<std::thread> ts;
-        for (int t = 0; t < T; ++t) {
-            ts.emplace_back([&, t]() {
-                int32_t mx = -1, mn = 0;
-                for (int i = 0; i < n; ++i)
-                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) {
-                        mx = std::max(mx, hc.tid[k]);
-                        mn = std::min(mn, hc.tid[k]);
-                    }
-                auto& m = hc.idf[t];
-                if (mn >= 0 && mx < (1 << 22)) {
-                    std::vector<int32_t> df((size_t)mx + 1, 0);
-                    for (int i = 0; i < n; ++i)
-                        for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) ++df[hc.tid[k]];
-                    for (int32_t k = 0; k <= mx; ++k)
-                        if (df[k]) m[k] = logf(1.0f + N / (1.0f + (float)df[k]));
-                } else {
-                    std::unordered_map<int32_t, int32_t> df;
-                    for (int i = 0; i < n; ++i)
-                        for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k) ++df[hc.tid[k]];
-                    for (auto& e : df) m[e.first] = logf(1.0f + N / (1.0f + (float)e.second));
-                }
-            });
-            if ((int)ts.size() >= 16) { for (auto& x : ts) x.join(); ts.clear(); }
-        }
-        for (auto& x : ts) x.join();
     }
-    // ---- candidate norms sqrt(sum (tf*idf)^2) per (user, col) row --------
-    hc.sqrt_nb.assign((size_t)n * T, 0.0);
-    {
-        // dense idf lookup tables where possible (the norm pass touches every token)
-        std::vector<std::vector<float>> dense(T);
-        for (int t = 0; t < T; ++t) {
-            if (!hc.has_idf[t]) continue;
-            int32_t mx = -1;
-            bool ok = true;
-            for (auto& e : hc.idf[t]) { if (e.first < 0 || e.first >= (1 << 22)) { ok = false; break; } mx = std::max(mx, e.first); }
-            if (!ok) continue;
-            dense[t].assign((size_t)mx + 1, 1.0f);
-            for (auto& e : hc.idf[t]) dense[t][e.first] = e.second;
-        }
-        par_for(n, [&](int64_t lo, int64_t hi) {
-            for (int64_t i = lo; i < hi; ++i)
-                for (int t = 0; t < T; ++t) {
-                    size_t r = (size_t)i * T + t;
-                    double nb = 0.0;
-                    for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
-                        double idf;
-                        if (!hc.has_idf[t]) idf = 1.0;
-                        else if (!dense[t].empty() || hc.idf[t].empty())
-                            idf = (hc.tid[k] >= 0 && hc.tid[k] < (int32_t)dense[t].size()) ? dense[t][hc.tid[k]] : 1.0f;
-                        else idf = hc.idf_of(t, hc.tid[k]);
-                        double w = (double)hc.tf[k] * idf;
-                        nb += w * w;
-                    }
-                    hc.sqrt_nb[r] = std::sqrt(nb);
-                }
-        });
-    }
+    // ---- df / idf (profiles mode) and the candidate norms sqrt(sum (tf*idf)^2) per (user,
+    // col) row: on the device (F3, pf_idf.hip)
+    const int rc = device_idf_norms(hc, d->idf_mode != PF_IDF_EXPLICIT, err);
+    if (rc != PF_OK) return rc;
     // ---- normalisers -----------------------------------------------------
     const int K = kNumFixed + T;
     hc.npres.assign(K, 0); hc.nmean.assign(K, 0.f); hc.nsd.assign(K, 0.f);
@@ -224,8 +166,10 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     for (size_t k = 0; k < hc.clubs.size() && packed; ++k) packed = hc.clubs[k] < kIdLimit;
     for (size_t k = 0; k < hc.friends.size() && packed; ++k) packed = hc.friends[k] < kIdLimit;
     if (!packed)
-        for (size_t k = 0; k < hc.tf.size(); ++k)
+        for (size_t k = 0; k < hc.tf.size(); ++k) {
             if (hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23)) { err = "token count outside [-2^23, 2^23)"; return PF_EUNSUPP; }
+            if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kWideTidMask) { err = "token id outside [0, 2^26)"; return PF_EUNSUPP; }
+        }
     hs.packed = packed;
     // record length in words: clubs, friends, tokens
     std::vector<uint32_t> len(n), ncols(n);
@@ -315,7 +259,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                     if (packed) {
                         w.push_back(((uint32_t)hc.tf[k] << 24) | ((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k]);
                     } else {
-                        w.push_back((uint32_t)hc.tid[k]);
+                        w.push_back((uint32_t)hc.tid[k] | ((uint32_t)t << kWideTidBits));
                         w.push_back(((uint32_t)hc.tf[k] << 8) | (uint32_t)t);
                     }
                 }
@@ -482,7 +426,7 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
             if (packed)
                 items[2].push_back(make_entry(kTagTok | ((uint32_t)t << kTidBits) | (uint32_t)hc.tid[k],
                                               kTokVal | vi | ((uint32_t)t << kTidBits)));
-            else items[2].push_back(make_entry((uint32_t)hc.tid[k], (uint32_t)t | (vi << 8)));
+            else items[2].push_back(make_entry((uint32_t)hc.tid[k] | ((uint32_t)t << kWideTidBits), (uint32_t)t | (vi << 8)));
             out.vals.push_back(v);
         }
     }

@@ -72,6 +72,10 @@ struct HostPost {
 };
 
 int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err);
+// F3 on the device (pf_idf.hip): with from_profiles, df per (column, tid) and hc.idf (host
+// logf over the distinct pairs); then hc.sqrt_nb for every (user, column) row.  Needs the
+// current HIP device; hc.has_idf (and, explicit mode, hc.idf) set by the caller.
+int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err);
 // fills hp (hp.ok = false with hp.why when the corpus is outside the encoding)
 void build_postings(const HostCorpus& hc, HostPost& hp);
 // Postings query image of candidate idx (pf_types.h layout); excl = uids to exclude

@@ -39,6 +39,10 @@ constexpr uint32_t kTagClub = 0x80000000u;
 constexpr uint32_t kTagTok = 0x40000000u;
 constexpr uint32_t kTokVal = 0x01000000u;
 constexpr uint32_t kIdLimit = 0x40000000u;        // packed: club / friend ids below 2^30
+// wide: a token's first word is tid | col << 26 (the query tables' key: one entry per (column,
+// tid), as a tid can sit in several columns), so wide corpora need 0 <= tid < 2^26
+constexpr uint32_t kWideTidBits = 26;
+constexpr uint32_t kWideTidMask = (1u << kWideTidBits) - 1;
 constexpr uint32_t kPadWord = 0xFFFFFFFFu;        // stream padding
 
 // Record stream (per candidate, tile-interleaved in 16-B steps):

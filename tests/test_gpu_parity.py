@@ -621,3 +621,43 @@ def test_batched_sharded_holdout_drivers_equal_sequential():
         assert list(pf.rec_tests_summary(hits, club)) == ref5, (nshards, batch)
     # the engine's own adjacency is untouched: the sequential driver still matches
     assert np.array_equal(ds.holdout_friends(eng, m["holdout"]).view(np.uint64), seq.view(np.uint64))
+
+
+def test_device_df_idf_norms_and_wide_token_ids():
+    """F3 on the device (pf_idf.hip): df by radix sort + run-length encoding and the candidate
+    norms by per-row bisection, on a corpus whose token ids pass the packed limit (2^18 - 1),
+    so the record-stream scan and the pair kernel use the wide format, where a token's key is
+    tid | col << 26 (a tid in several of the query's columns is one entry per column).  idf
+    bits equal the oracle's float32 logf (recommender.cpp:43-66) for every (column, tid), and
+    the scores that depend on the norms and the wide tables are bit-exact.  Token ids outside
+    [0, 2^26) are refused at open (the reference's encoder writes vocabulary indices)."""
+    base = tl.synth.Corpus(n_users=6000, seed=11, edge_cases=1)
+    c = tl.corpus_from_desc(base.desc_ptr())
+    t = c.tok_tid.astype(np.int64)
+    c.tok_tid[:] = ((t * 1048573) % 2**26).astype(np.int32)  # a bijection of [0, 2^26)
+    eng = tl.engine(c.desc_ptr())
+    assert not eng.layout().packed_tokens
+    orc = tl.Oracle(c)
+    T = c.n_cols
+    rows = np.repeat(np.arange(len(c.tok_off) - 1) % T, np.diff(c.tok_off))
+    pairs = np.unique(np.stack([rows, c.tok_tid.astype(np.int64)]), axis=1)
+    assert (pairs[1] > 2**25).any()
+    for col, tid in pairs.T[:: max(1, pairs.shape[1] // 3000)]:
+        g, r = np.float32(eng.idf(int(col), int(tid))), np.float32(orc.idf(int(col), int(tid)))
+        assert g.view(np.uint32) == r.view(np.uint32), (col, tid)
+    rng = np.random.default_rng(3)
+    a = rng.integers(1, 6001, 20000).astype(np.int32)
+    b = rng.integers(1, 6001, 20000).astype(np.int32)
+    assert np.array_equal(eng.fas_pairs(a, b).view(np.uint32), orc.fas_pairs(a, b).view(np.uint32))
+    q = [1, 8, 77, 1500, 5999]
+    for u, gq, rq in zip(q, eng.recommend_interest_all(q, 10), orc.interest(q, 10, tl.PF_MODE_ALL, 0)):
+        assert list(gq[0]) == list(rq[0]), u
+        assert np.array_equal(gq[1].view(np.uint32), rq[1].view(np.uint32)), u
+    for u, gq, rq in zip(q, eng.recommend_collaborative(q, 10, 1000), orc.collab(q, 10, 1000)):
+        assert list(gq[0]) == list(rq[0]), u
+        assert np.array_equal(gq[1].view(np.uint32), rq[1].view(np.uint32)), u
+    eng.close()
+    orc.close()
+    c.tok_tid[int(np.nonzero(c.tok_tid != 0)[0][0])] = -5
+    with pytest.raises(tl.product().FasError, match="outside"):
+        tl.engine(c.desc_ptr())

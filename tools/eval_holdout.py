@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--holdout", type=int, default=2000)
     ap.add_argument("--rectests", type=int, default=1000)
     ap.add_argument("--topk", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=2048, help="users per device pass (large passes run as pipelined chunks)")
     ap.add_argument("--sequential", action="store_true")
     args = ap.parse_args()
     if args.make_data:

@@ -192,6 +192,53 @@ def pmc_pass(args, kernel_name):
         shutil.rmtree(d, ignore_errors=True)
 
 
+class Comm:
+    """The collectives bench.py uses, named like torch.distributed's: RCCL ("nccl", one rank
+    per GPU, device tensors) or gloo through host memory (--dist-backend gloo: N ranks may share
+    one GPU, a correctness rehearsal of the N > 1 path on a one-GPU box; its timings are not
+    scaling numbers)."""
+
+    def __init__(self, backend, local):
+        import torch
+        import torch.distributed as dist
+        self.dist, self.torch, self.gloo = dist, torch, backend == "gloo"
+        self.ReduceOp = dist.ReduceOp
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if self.gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def all_reduce(self, t, op):
+        if self.gloo:
+            h = t.cpu()
+            self.dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            self.dist.all_reduce(t, op=op)
+
+    def all_gather(self, parts, t):
+        if self.gloo:
+            hp = [self.torch.empty_like(t, device="cpu") for _ in parts]
+            self.dist.all_gather(hp, t.cpu())
+            for d, h in zip(parts, hp):
+                d.copy_(h)
+        else:
+            self.dist.all_gather(parts, t)
+
+    def all_gather_into_tensor(self, out, t):
+        if self.gloo:
+            self.all_gather(list(out.unbind(0)), t)
+        else:
+            self.dist.all_gather_into_tensor(out, t)
+
+    def destroy_process_group(self):
+        self.dist.destroy_process_group()
+
+
 CFG3_QUERIES = 64      # cfg 3 step: a batch of seeded query users
 CFG3_LIMIT = 10000     # recommend_collaborative's default candidate_limit (include/recommender.h)
 
@@ -397,12 +444,9 @@ def run_cfg5(args, world, rank, local):
             if pmc_err:
                 log(f"pmc pass: {pmc_err}")
     import torch
+    local = local % max(1, torch.cuda.device_count())  # --dist-backend gloo: ranks may share a GPU
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = Comm(args.dist_backend, local) if world > 1 else None
     import pokec_fas as pf
     t1 = time.time()
     ds = pf.Dataset(d, 0, cache=os.path.join(d, f"parse_r{rank}.bin"))
@@ -527,6 +571,9 @@ def main():
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1 collectives: nccl (RCCL over xGMI, one rank per GPU) or gloo through host memory "
+                         "(ranks may share one GPU: a correctness rehearsal of the multi-GPU path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass (traffic = null)")
     ap.add_argument("--time-every", type=int, default=1,
@@ -565,12 +612,9 @@ def main():
                 log(f"pmc pass: {pmc_err}")
 
     import torch
+    local = local % max(1, torch.cuda.device_count())  # --dist-backend gloo: ranks may share a GPU
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = Comm(args.dist_backend, local) if world > 1 else None
     import pokec_fas as pf
 
     t2 = time.time()

@@ -131,3 +131,53 @@ def test_gloo_eval_shards_merge_to_plan_order(world):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert ret.get(timeout=10) is True
+
+
+def _comm_worker(rank, world, port, k, ret):
+    """bench.py's own collectives object (Comm, gloo): the per-shard top-k keys all-gathered
+    into [world][nq][k] exactly as the bench's step does, then merged; the step time's max
+    over ranks and the pair counts' sum as the bench reduces them."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
+    import bench
+    comm = bench.Comm("gloo", 0)
+    rng = np.random.default_rng(11)
+    nq, n = 4, 1000
+    scores = rng.random((nq, n)).astype(np.float32)
+    scores[:, 100:140] = 0.25  # ties broken by uid
+    shard = np.array_split(np.arange(n), world)[rank]
+    local = np.full((nq, k), np.iinfo(np.uint64).max, np.uint64)
+    for qi in range(nq):
+        keys = sorted(_key(scores[qi, j], j + 1) for j in shard)[:k]
+        local[qi, :len(keys)] = keys
+    gathered = torch.empty((world, nq, k), dtype=torch.int64)
+    comm.all_gather_into_tensor(gathered, torch.from_numpy(local.view(np.int64)))
+    t = torch.tensor([float(rank + 1), float(len(shard))], dtype=torch.float64)
+    tm = t[:1].clone()
+    comm.all_reduce(t, op=comm.ReduceOp.SUM)
+    comm.all_reduce(tm, op=comm.ReduceOp.MAX)
+    ok = float(tm.item()) == float(world) and float(t[1]) == float(n)
+    g = gathered.numpy().view(np.uint64)
+    for qi in range(nq):
+        merged = np.sort(g[:, qi, :].reshape(-1))[:k]
+        ref = np.array(sorted(_key(scores[qi, j], j + 1) for j in range(n))[:k], np.uint64)
+        ok = ok and bool(np.array_equal(merged, ref))
+    ret.put(bool(ok))
+    comm.barrier()
+    comm.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_comm_gloo_exchange(world):
+    ctx = mp.get_context("spawn")
+    ret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, 10, ret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ret.get(timeout=10) is True for _ in range(world))

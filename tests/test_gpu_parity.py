@@ -661,3 +661,23 @@ def test_device_df_idf_norms_and_wide_token_ids():
     c.tok_tid[int(np.nonzero(c.tok_tid != 0)[0][0])] = -5
     with pytest.raises(tl.product().FasError, match="outside"):
         tl.engine(c.desc_ptr())
+
+
+def test_pipelined_job_chunks_equal_small_calls(big):
+    """A call of >= 1024 jobs runs as double-buffered chunks (chunk i + 1 planned and launched
+    while chunk i runs): its results equal 64-user calls (one chunk each) bit for bit, and the
+    oracle on a sample, for the collaborative and clubs recommenders."""
+    c, eng, orc = big
+    rng = np.random.default_rng(8)
+    q = [int(x) for x in rng.integers(1, 20001, 1200)]
+    for fn, ofn in ((eng.recommend_collaborative, orc.collab), (eng.recommend_clubs_collab, orc.clubs)):
+        whole = fn(q, 10, 1000)
+        parts = []
+        for i in range(0, len(q), 64):
+            parts += fn(q[i:i + 64], 10, 1000)
+        for u, a, b in zip(q, whole, parts):
+            assert list(a[0]) == list(b[0]), u
+            assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), u
+        for u, a, r in zip(q[:24], whole[:24], ofn(q[:24], 10, 1000)):
+            assert list(a[0]) == list(r[0]), u
+            assert np.array_equal(a[1].view(np.uint32), r[1].view(np.uint32)), u

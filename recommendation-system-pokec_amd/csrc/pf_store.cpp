@@ -489,10 +489,20 @@ void radix_sort_u64(std::vector<uint64_t>& a, int bits) {
     }
 }
 
-// cell width 2^shift: the smallest >= one wave block holding ~<= 32 of the list's entries
+// cell width 2^shift: the smallest >= one wave block holding ~<= cell_entries() of the list's
+// entries.  A block reads whole cells, so a short list costs up to a cell of entries per block
+// for the few that fall in it.  PF_CELL_ENTRIES overrides it (profiling only).
+uint64_t cell_entries() {
+    static const uint64_t v = [] {
+        const char* e = getenv("PF_CELL_ENTRIES");
+        const long x = e ? strtol(e, nullptr, 0) : 0;
+        return x > 0 ? (uint64_t)x : (uint64_t)32;
+    }();
+    return v;
+}
 uint32_t list_shift(uint64_t len, int32_t n) {
     uint32_t s = kPostMinShift;
-    while (s < 30 && (len << (s + 1)) <= 32ull * (uint64_t)n) ++s;
+    while (s < 30 && (len << (s + 1)) <= cell_entries() * (uint64_t)n) ++s;
     return s;
 }
 

@@ -195,8 +195,8 @@ int pf_set_scan_kernel(pf_ctx* ctx, int32_t kind);
 /*
  * Device-resident all-candidates scan for the multi-GPU bench: scores the
  * queries against this context's shard and writes, per query, `topk` packed
- * 64-bit keys to DEVICE memory d_keys[nq*topk] on `stream` (a hipStream_t;
- * NULL = the context's stream).  Key = (~orderable(score) << 32) | (uid ^
+ * 64-bit keys to DEVICE memory d_keys[nq*topk] on `stream` (a hipStream_t).
+ * Key = (~orderable(score) << 32) | (uid ^
  * 0x80000000): ascending key = (score desc, uid asc); unused slots are
  * UINT64_MAX.  `stream` is used as given (NULL = the HIP null stream, not the
  * context's stream), so the caller's collectives on that stream are ordered

@@ -678,13 +678,13 @@ __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const Pair
     const PairBlock b = blocks[blockIdx.x];
     const int i = threadIdx.x;
     unsigned long long v[3] = {0ull, 0ull, 0ull};
-    if (i < b.count) {
-        const int p = slots[b.begin + i];
+    for (int x = i; x < b.count; x += 256) {
+        const int p = slots[b.begin + x];
         if (p >= 0) {
             const uint4 h2 = st.hdr2[p];
-            v[0] = 1ull;
-            v[1] = 32ull + 4ull * (h2.y + h2.z) + 8ull * h2.w;
-            v[2] = 48ull + 4ull * record_words(h2, PACKED);
+            v[0] += 1ull;
+            v[1] += 32ull + 4ull * (h2.y + h2.z) + 8ull * h2.w;
+            v[2] += 48ull + 4ull * record_words(h2, PACKED);
         }
     }
 #pragma unroll

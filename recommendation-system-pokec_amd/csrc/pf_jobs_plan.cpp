@@ -59,6 +59,19 @@ hipError_t up(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 }
 
 int a16(int64_t x) { return (int)((x + 15) & ~15ll); }
+
+// candidates per collaborative pair block (a multiple of 256): one staged image per block.
+// 256 measured best (r2r, cfg 3 pair kernel: 256 -> 360 us, 512 -> 367, 1024 -> 391, 2048 ->
+// 433: wider blocks stage fewer images but balance worse).  PF_PAIR_SPAN overrides it
+// (profiling only).
+int64_t pair_span() {
+    static const int64_t v = [] {
+        const char* e = getenv("PF_PAIR_SPAN");
+        const long x = e ? strtol(e, nullptr, 0) : 0;
+        return x >= 256 ? (int64_t)(x / 256 * 256) : (int64_t)256;
+    }();
+    return v;
+}
 size_t a16z(size_t x) { return (x + 15) & ~(size_t)15; }
 
 int pow2_lg(int64_t n) {
@@ -567,13 +580,15 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                 E += (int64_t)d.nfd * p.cap;
                 const int32_t iu = img(p.u);
                 add_blocks(iu, d.sim_off, d.nfd, d.sim_off);
-                // candidate-chunk major: the friends' blocks of one 256-candidate chunk are
-                // consecutive, so they run together and share the chunk's records in cache
+                // candidate-chunk major: the friends' blocks of one candidate chunk are
+                // consecutive, so they run together and share the chunk's records in cache;
+                // a block scores span() candidates against one staged friend image
+                const int64_t span = pair_span();
                 std::vector<int32_t> fimg(d.nfd);
                 for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
-                for (int64_t x = 0; x < p.cap; x += 256)
+                for (int64_t x = 0; x < p.cap; x += span)
                     for (int r = 0; r < d.nfd; ++r)
-                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), (int32_t)std::min<int64_t>(256, p.cap - x),
+                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), (int32_t)std::min<int64_t>(span, p.cap - x),
                                                    (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
                 jix_collab.push_back(jn);
                 max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);

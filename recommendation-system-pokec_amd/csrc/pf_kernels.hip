@@ -1083,12 +1083,16 @@ __global__ __launch_bounds__(256) void fas_pairs_kernel(DevStore st, const uint8
     const PairBlock b = blocks[blockIdx.x];
     char* scratch;
     const QView v = stage_query<GTAB>(smem, pool, refs[b.qimg], &scratch);
-    const int i = (int)threadIdx.x;
-    int p = i < b.count ? slots[b.begin + i] : -1;
-    const bool active = p >= 0;
-    if (!active) p = 0;
-    const float f = fas_slot<PACKED>(st, v, p, active);
-    if (active) out[b.out + i] = f;
+    // a block scores b.count pairs (a multiple of 256 except the last of a run) against the
+    // one staged image, 256 at a time: wider blocks stage the image fewer times
+    for (int base = 0; base < b.count; base += 256) {
+        const int i = base + (int)threadIdx.x;
+        int p = i < b.count ? slots[b.begin + i] : -1;
+        const bool active = p >= 0;
+        if (!active) p = 0;
+        const float f = fas_slot<PACKED>(st, v, p, active);
+        if (active) out[b.out + i] = f;
+    }
 }
 
 // ---------------------------------------------------------------- K4: collaborative sum

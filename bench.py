@@ -13,7 +13,8 @@ generator tools/pokec_synth.cpp, resident in HBM), interest FAS top-10 over ever
          fixed: strong scaling (the north-star ">= 6x at 8 GPUs" is defined on cfg 4).
 --workload cfg2|cfg4 overrides the default (cfg2 at N > 1: N queries per step, one per GPU,
 weak scaling).  value = candidates scored / s over the whole job.
---workload cfg3 (configs[2]): collaborative FoF top-10, 64 query users per step; value = pair-FAS/s.
+--workload cfg3 (configs[2]): collaborative FoF top-10, 64 query users per step; value = pair-FAS/s;
+three engine contexts per GPU by default, steps dealt round-robin to their host threads.
 --workload cfg5 (configs[4]): the hold-out evaluation (recommendation_tests.cpp: interest + collab
 + clubs) of 2048 users per step, users split over the ranks; value = hold-out users/s.
 
@@ -164,7 +165,8 @@ def pmc_pass(args, kernel_name):
     cmd = [prof, "--pmc", "FETCH_SIZE", "--kernel-include-regex", kernel_name, "-T", "--output-format", "csv",
            "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--gpus", "1",
            "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-pmc",
-           "--workload", args.workload, "--scan-kernel", args.scan_kernel, "--users", str(args.users)]
+           "--workload", args.workload, "--scan-kernel", args.scan_kernel, "--users", str(args.users),
+           "--contexts", str(args.contexts), "--cfg5-batch", str(args.cfg5_batch)]
     try:
         r = subprocess.run(["timeout", "-s", "KILL", "240"] + cmd, capture_output=True, text=True,
                            env={**os.environ, "TMPDIR": os.environ.get("TMPDIR", "/tmp")})
@@ -277,13 +279,18 @@ def cpu_baseline_collab(desc_ptr, n_queries=16, seconds_budget=10.0):
                       f"by the oracle, {el:.1f}s timed, {build_s:.1f}s map build untimed)"}
 
 
-def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s):
+def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s):
     """cfg 3 (BASELINE configs[2]): collaborative FoF propagation top-10 on the full corpus.  A
     step = recommend_collaborative(u, 10, 10000) for a batch of 64 seeded users (this rank's share
     of them at N > 1: query users split, strong scaling), through the device job pipeline
     (K3 gather, K6 images, K1' pairs, K4' sums, K8 top-k) and back to the host.  value =
-    FAS pairs scored / s (SURVEY D3's cfg-3 unit, |F| + |F|.|C| per user)."""
+    FAS pairs scored / s (SURVEY D3's cfg-3 unit, |F| + |F|.|C| per user).
+    --contexts C > 1: C engine contexts on the GPU (each its own stream and workspaces, a full
+    replica), step i on context i % C from its own host thread, so one context's host planning
+    overlaps another's device work (ctypes releases the GIL during the calls)."""
     Q = CFG3_QUERIES
+    eng = engs[0]
+    C = len(engs)
     steps, warm = args.steps, args.warmup
     rng = np.random.default_rng(4)
     qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
@@ -295,17 +302,34 @@ def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s
         dist.barrier()
     # timed region: the pair kernel timed by HIP events (the launch roofline); the pair and byte
     # counts come from an untimed replay of the same steps (the counting kernel stays out of it)
-    eng.jobs_stats_reset(time_pairs=True, count=False)
+    for e in engs:
+        e.jobs_stats_reset(time_pairs=True, count=False)
+
+    def run_steps(t):  # context t: steps warm + t, warm + t + C, ...
+        n = 0
+        for i in range(warm + t, warm + steps, C):
+            out = engs[t].recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
+            n += sum(len(o[0]) for o in out)
+        return n
+
     t0 = time.perf_counter()
-    nres = 0
-    for i in range(warm, warm + steps):
-        out = eng.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
-        nres += sum(len(o[0]) for o in out)
+    if C == 1:
+        nres = run_steps(0)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(C) as ex:
+            nres = sum(ex.map(run_steps, range(C)))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timing = eng.jobs_stats()
+    timing = {"pair_ms": 0.0, "pair_launches": 0}
+    for e in engs:
+        tm_ = e.jobs_stats()
+        timing["pair_ms"] += tm_["pair_ms"]
+        timing["pair_launches"] += tm_["pair_launches"]
+        if e is not eng:
+            e.jobs_stats_reset(time_pairs=False, count=False)
     eng.jobs_stats_reset(time_pairs=False, count=True)
     for i in range(warm, warm + steps):
         eng.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
@@ -339,7 +363,7 @@ def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s
                                f"per step (limit {CFG3_LIMIT})" + (f", split over {world} GPUs" if world > 1 else ""),
                    "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{Q}_limit{CFG3_LIMIT}_world{world}",
                    "n_users": args.users, "queries_per_step": Q, "topk": TOPK, "limit": CFG3_LIMIT,
-                   "parallelism": f"query-users x{world}"},
+                   "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")},
         "candidates_per_s": cands / elapsed, "queries_per_s": Q * steps / elapsed,
         "pairs_per_step": pairs / steps, "candidates_per_step": cands / steps, "results": nres,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -364,7 +388,8 @@ def run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s
         rec["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    eng.close()
+    for e in engs:
+        e.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -568,6 +593,9 @@ def main():
                          "scaling; the default at N > 1); "
                          "cfg5: hold-out evaluation (recommendation_tests: interest + collab + clubs) of 2048 "
                          "users per step, users split over the ranks")
+    ap.add_argument("--contexts", type=int, default=3,
+                    help="cfg3: engine contexts per GPU, each driven by its own host thread (r2s: 1 -> 1.1e9, "
+                         "2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 pair-FAS/s; each context is a full replica)")
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
@@ -621,7 +649,8 @@ def main():
     eng = pf.FasEngine(desc, local)
     t3 = time.time()
     if args.workload == "cfg3":
-        return run_cfg3(args, eng, pf, torch, dist, world, rank, base, pmc, pmc_err, t3 - t2)
+        engs = [eng] + [pf.FasEngine(desc, local) for _ in range(max(1, args.contexts) - 1)]
+        return run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, time.time() - t2)
     eng.set_shard(rank, world)
     eng.set_scan_kernel({"auto": pf.PF_SCAN_AUTO, "stream": pf.PF_SCAN_STREAM, "postings": pf.PF_SCAN_POSTINGS}
                         [args.scan_kernel])

@@ -475,10 +475,22 @@ def run_cfg5(args, world, rank, local):
     import pokec_fas as pf
     t1 = time.time()
     ds = pf.Dataset(d, 0, cache=os.path.join(d, f"parse_r{rank}.bin"))
-    eng = pf.FasEngine(ds.desc_ptr(), local)
+    C = max(1, args.contexts)  # engine contexts on this GPU, one host thread each
+    engs = [pf.FasEngine(ds.desc_ptr(), local) for _ in range(C)]
+    eng = engs[0]
     open_s = time.time() - t1
-    log(f"[rank {rank}] dataset + engine open {open_s:.1f}s")
+    log(f"[rank {rank}] dataset + {C} engine context(s) open {open_s:.1f}s")
     S, steps, warm = CFG5_USERS, args.steps, args.warmup
+    nsh = world * C  # plan shards: entry i belongs to shard i % nsh = rank * C + context
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(C) if C > 1 else None
+
+    def sum_stats(fn):
+        tot = {}
+        for e in engs:
+            for key, v in fn(e).items():
+                tot[key] = tot.get(key, 0) + v
+        return tot
 
     def gather(a):
         if world == 1:
@@ -489,9 +501,13 @@ def run_cfg5(args, world, rank, local):
         return [p.cpu().numpy() for p in parts]
 
     def step():
-        hits, club = ds.eval_recommendation_tests(eng, S, CFG5_TOPK, rank, world, args.cfg5_batch)
-        hits = pf.merge_shards(gather(hits))
-        club = pf.merge_shards(gather(club))
+        def part(t):
+            return ds.eval_recommendation_tests(engs[t], S, CFG5_TOPK, rank * C + t, nsh, args.cfg5_batch)
+        parts = [part(0)] if pool is None else list(pool.map(part, range(C)))
+        hs = gather(np.stack([h for h, _ in parts]))  # per rank [C, entries, 3]
+        cs = gather(np.stack([c for _, c in parts]))
+        hits = pf.merge_shards([h[t] for h in hs for t in range(C)])  # shard order rank * C + t
+        club = pf.merge_shards([c[t] for c in cs for t in range(C)])
         return pf.rec_tests_summary(hits, club), len(hits)
 
     for _ in range(warm):
@@ -499,7 +515,8 @@ def run_cfg5(args, world, rank, local):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    eng.jobs_stats_reset(time_pairs=True, count=False)
+    for e in engs:
+        e.jobs_stats_reset(time_pairs=True, count=False)
     ts = time.perf_counter()
     for _ in range(steps):
         summary, n_eval = step()
@@ -507,11 +524,13 @@ def run_cfg5(args, world, rank, local):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - ts
-    timing = eng.jobs_stats()
-    eng.jobs_stats_reset(time_pairs=False, count=True)
+    timing = sum_stats(lambda e: e.jobs_stats())
+    for e in engs:
+        e.jobs_stats_reset(time_pairs=False, count=True)
     step()  # untimed replay: pair and byte counts of one step on this rank
-    st = eng.jobs_stats()
-    eng.jobs_stats_reset(time_pairs=False, count=False)
+    st = sum_stats(lambda e: e.jobs_stats())
+    for e in engs:
+        e.jobs_stats_reset(time_pairs=False, count=False)
     selfcheck = None
     if world == 1:  # the batched driver against the sequential one on a small sample (untimed)
         h, c = ds.eval_recommendation_tests(eng, 64, CFG5_TOPK, 0, 1, 128)
@@ -547,7 +566,8 @@ def run_cfg5(args, world, rank, local):
                                f"corpus" + (f", users split over {world} GPUs" if world > 1 else ""),
                    "workload_key": f"cfg5_rectests_{args.users}users_s{S}_top{CFG5_TOPK}_world{world}",
                    "n_users": args.users, "users_per_step": S, "topk": CFG5_TOPK, "limit": 5000,
-                   "parallelism": f"hold-out users x{world}" + (" + all_gather" if world > 1 else "")},
+                   "parallelism": f"hold-out users x{world}" + (" + all_gather" if world > 1 else "")
+                                  + (f", {C} engine contexts per GPU" if C > 1 else "")},
         "rectests_summary": [float(x) for x in summary], "pairs_per_step": st["pairs"],
         "pair_fas_per_s": st["pairs"] / (elapsed / steps) if elapsed > 0 else None,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -571,7 +591,10 @@ def run_cfg5(args, world, rank, local):
         rec["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    eng.close()
+    if pool is not None:
+        pool.shutdown()
+    for e in engs:
+        e.close()
     ds.close()
     if dist:
         dist.barrier()
@@ -593,9 +616,10 @@ def main():
                          "scaling; the default at N > 1); "
                          "cfg5: hold-out evaluation (recommendation_tests: interest + collab + clubs) of 2048 "
                          "users per step, users split over the ranks")
-    ap.add_argument("--contexts", type=int, default=3,
-                    help="cfg3: engine contexts per GPU, each driven by its own host thread (r2s: 1 -> 1.1e9, "
-                         "2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 pair-FAS/s; each context is a full replica)")
+    ap.add_argument("--contexts", type=int, default=None,
+                    help="cfg3 / cfg5: engine contexts per GPU, each a full replica driven by its own host "
+                         "thread; default 3 for cfg3 (r2s: 1 -> 1.1e9, 2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 "
+                         "pair-FAS/s) and 2 for cfg5 (r2t: 1 -> 28.3k, 2 -> 39.8k, 3 -> 35.4k users/s)")
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
@@ -617,6 +641,8 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
+    if args.contexts is None:
+        args.contexts = {"cfg3": 3, "cfg5": 2}.get(args.workload, 1)
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local)
     import synth

@@ -681,3 +681,28 @@ def test_pipelined_job_chunks_equal_small_calls(big):
         for u, a, r in zip(q[:24], whole[:24], ofn(q[:24], 10, 1000)):
             assert list(a[0]) == list(r[0]), u
             assert np.array_equal(a[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def test_two_contexts_from_two_threads(big):
+    """Engine contexts are independent (own stream, workspaces, replica): two contexts on one
+    device driven from two host threads at once (bench.py --contexts) give the results of one
+    context used alone, for the job pipeline and the all-candidates scan."""
+    from concurrent.futures import ThreadPoolExecutor
+    c, eng, orc = big
+    eng2 = tl.engine(c.desc_ptr())
+    rng = np.random.default_rng(12)
+    qs = [[int(x) for x in rng.integers(1, 20001, 48)] for _ in range(6)]
+    want = [(eng.recommend_collaborative(q, 10, 2000), eng.recommend_interest_all(q[:4], 10)) for q in qs]
+
+    def run(t):
+        e = (eng, eng2)[t]
+        return [(i, e.recommend_collaborative(qs[i], 10, 2000), e.recommend_interest_all(qs[i][:4], 10))
+                for i in range(t, len(qs), 2)]
+
+    with ThreadPoolExecutor(2) as ex:
+        got = [r for part in ex.map(run, range(2)) for r in part]
+    for i, col, alls in got:
+        for a, b in zip(col + alls, want[i][0] + want[i][1]):
+            assert list(a[0]) == list(b[0]), i
+            assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), i
+    eng2.close()

@@ -250,6 +250,17 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 // Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
 // launch the caller passes timed = false, or that sampling skips, records nothing and clears
 // last_ev0/last_ev1, so pf_last_scan_ms never reports another launch's time.
+// Blocks per workgroup of a batched postings scan (each workgroup stages its query's tables
+// once for them).  PF_K5_BATCH_SPAN overrides it (profiling only).
+int batch_blocks_per_wg() {
+    static const int v = [] {
+        const char* e = getenv("PF_K5_BATCH_SPAN");
+        const int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 1;
+    }();
+    return v;
+}
+
 int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
     e0 = c->ev0;
     e1 = c->ev1;
@@ -307,7 +318,8 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // queries at a time and share their lists and cells in L2; with a few workgroups per
     // query looping over the range instead, 256 queries run at once and L2 hits collapse
     // (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
-    const int blocks = nq == 1 ? std::max(1, std::min(nwb, c->num_cus * per_cu)) : std::max(1, nwb);
+    const int blocks = nq == 1 ? std::max(1, std::min(nwb, c->num_cus * per_cu))
+                               : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);

@@ -745,8 +745,8 @@ def main():
     n_cand = eng.num_users - 1  # candidates per query: every profile but the query (minus adj[q])
     value = Q * n_cand * steps / elapsed
     # bytes per launch by the kernel's access pattern, over the queries timed (this rank's shard)
-    timed_q = qstream[warm:warm + steps].reshape(-1)
-    phys = eng.scan_bytes(timed_q)
+    # one call per step: the byte model counts the image staging of a launch of Q queries
+    phys = np.concatenate([eng.scan_bytes(qstream[i]) for i in range(warm, warm + steps)])
     timed_steps = list(range(0, steps, max(args.time_every, 1)))[:launches] if launches else []
     phys_per_launch = (float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in timed_steps]))
                        if timed_steps else None)

@@ -237,8 +237,10 @@ int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
  * cell words per query list and every entry of each list's cell range (4 B;
  * token entries also their 8-B norm), the exclusion list, and the staged query
  * image per workgroup; K1 = the shard's record stream and headers.  0 for an
- * unknown uid.  (A query alone in its launch is assumed; in a batch each
- * workgroup stages its query's image once per block.) */
+ * unknown uid.  The nq queries are taken as ONE launch, as pf_recommend_interest
+ * runs them: nq = 1 is the single-query scan (one resident round of workgroups,
+ * each staging the image once); nq > 1 a batch (each workgroup stages its query's
+ * image once for its four blocks). */
 int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* out_bytes);
 
 /* Statistics of the recommenders' device job pipeline (pf_recommend_collab / _clubs /

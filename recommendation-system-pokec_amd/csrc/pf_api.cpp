@@ -885,7 +885,10 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
         pf::build_query_post(c->hc, c->hp, x, ex, img);
         const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(img.data() + sizeof(pf::QConst));
         const uint32_t wl = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
-        const int wgs = nq == 1 ? c->num_cus * pf::post_blocks_per_cu(wl) : 1;
+        // workgroups that stage this query's image, as the launch of these nq queries runs
+        const int nwb = c->wb_end - c->wb_begin;
+        const int wgs = nq == 1 ? c->num_cus * pf::post_blocks_per_cu(wl)
+                                : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
         out[i] = post_query_bytes(c, img, wgs);
     }, 1);
     return PF_OK;

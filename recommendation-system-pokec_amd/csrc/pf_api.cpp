@@ -254,6 +254,19 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
 // candidates/s.  PF_K5_BATCH_SPAN overrides it (profiling only).
+// K5 block hand-out of a one-query launch (profiling knob PF_K5_DYN): 1 dynamic (each
+// workgroup's first block, then the next unclaimed one; the default), 0 static (workgroup w
+// takes blocks w, w + grid, ...).  r2fb A/B: 205.3 / 205.6 us vs 206.9 / 206.9 us per cfg-2
+// launch; batches (one block per workgroup in L2-sharing order) stay static (cfg 4 9.83e9
+// dynamic vs 9.88e9 static).
+int post_dynamic() {
+    static const int v = [] {
+        const char* e = getenv("PF_K5_DYN");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 int batch_blocks_per_wg() {
     static const int v = [] {
         const char* e = getenv("PF_K5_BATCH_SPAN");
@@ -344,7 +357,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
                               nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
                               reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
-                              reinterpret_cast<const int32_t*>(base + offs_b), s));
+                              reinterpret_cast<const int32_t*>(base + offs_b), nq == 1 ? post_dynamic() : 0, s));
     if (timed) {
         HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;

@@ -760,7 +760,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-                                                              const int32_t* __restrict__ out_rows, uint32_t dbg_arg) {
+                                                              const int32_t* __restrict__ out_rows, uint32_t dbg_arg,
+                                                              int32_t dyn) {
     const uint32_t dbg = DBG ? dbg_arg : 0u;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t* img = pool + img_off[blockIdx.y];
@@ -778,8 +779,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kBlockCands * 24);
     uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
-    uint32_t* nlist = exb + kBlockCands / 32;
-    QCol* scol = reinterpret_cast<QCol*>(nlist + 4);  // the active columns (read at every pass)
+    uint32_t* misc = exb + kBlockCands / 32;  // [0]: the next block (dynamic hand-out)
+    QCol* scol = reinterpret_cast<QCol*>(misc + 4);  // the active columns (read at every pass)
     double* ftab = reinterpret_cast<double*>(scol + kPostMaxCols);  // F = used / (7 + T) by used
     PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
     uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + sizeof(PTok) * H.n_tok);
@@ -807,7 +808,11 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint64_t tprev = clock64();
     const uint64_t tstart = tprev;
 #endif
-    for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end; blk += (int)gridDim.x) {
+    // Blocks: the workgroup's own first block, then either every gridDim.x-th block (static)
+    // or (dyn) the next unclaimed block of the query from a counter in its ScanSync, so the
+    // blocks past the first resident round go to the workgroups that finish first.
+    unsigned int* next_blk = &sync[blockIdx.y].next;
+    for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end;) {
         const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
@@ -1020,6 +1025,14 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         }
         K5T(10);
+        if (dyn) {
+            // misc[0] was last read before this block's first barrier
+            if (tid == 0) misc[0] = (uint32_t)blk_begin + gridDim.x + atomicAdd(next_blk, 1u);
+            __syncthreads();
+            blk = (int)misc[0];
+        } else {
+            blk += (int)gridDim.x;
+        }
     }
 #ifdef PF_K5_TIMERS
     tacc[11] = clock64() - tstart;
@@ -1166,15 +1179,15 @@ uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFix
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                       const int32_t* out_rows, hipStream_t s) {
+                       const int32_t* out_rows, int dyn, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const uint32_t dbg = post_dbg();
     if (dbg)
         hipLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg);
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, dyn);
     else
         hipLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u);
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, dyn);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;

@@ -121,11 +121,14 @@ struct QImageRef {
     uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 
-// Per-query rendezvous of one scan launch: blocks finished, and the tail tile counters.
-// Zeroed by the host before every launch (it rides in the query upload).
+// Per-query rendezvous of one scan launch: blocks finished, K5's block hand-out counter,
+// and the tail tile counters.  Zeroed by the host before every launch (it rides in the
+// query upload).
 struct ScanSync {
     unsigned int done;
-    unsigned int pad[31];
+    unsigned int pad0[15];
+    unsigned int next;  // K5 dynamic hand-out: blocks claimed past the first gridDim.x, 64 B from done
+    unsigned int pad[15];
     unsigned int xcd_next[8 * 16];  // tail tile counter per XCD, 64 B apart
 };
 

@@ -267,6 +267,9 @@ int post_dynamic() {
     return v;
 }
 
+// K5 mode word: bit 0 dynamic hand-out (one-query launches only)
+uint32_t post_mode(int nq) { return nq == 1 && post_dynamic() ? 1u : 0u; }
+
 int batch_blocks_per_wg() {
     static const int v = [] {
         const char* e = getenv("PF_K5_BATCH_SPAN");
@@ -357,7 +360,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
                               nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
                               reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
-                              reinterpret_cast<const int32_t*>(base + offs_b), nq == 1 ? post_dynamic() : 0, s));
+                              reinterpret_cast<const int32_t*>(base + offs_b), post_mode(nq), s));
     if (timed) {
         HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;

@@ -761,7 +761,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
                                                               const int32_t* __restrict__ out_rows, uint32_t dbg_arg,
-                                                              int32_t dyn) {
+                                                              uint32_t mode) {
     const uint32_t dbg = DBG ? dbg_arg : 0u;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t* img = pool + img_off[blockIdx.y];
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     const uint64_t tstart = tprev;
 #endif
     // Blocks: the workgroup's own first block, then either every gridDim.x-th block (static)
-    // or (dyn) the next unclaimed block of the query from a counter in its ScanSync, so the
+    // or (mode bit 0) the next unclaimed block of the query from a counter in its ScanSync, so the
     // blocks past the first resident round go to the workgroups that finish first.
     unsigned int* next_blk = &sync[blockIdx.y].next;
     for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end;) {
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         }
         K5T(10);
-        if (dyn) {
+        if (mode & 1u) {
             // misc[0] was last read before this block's first barrier
             if (tid == 0) misc[0] = (uint32_t)blk_begin + gridDim.x + atomicAdd(next_blk, 1u);
             __syncthreads();
@@ -1179,15 +1179,15 @@ uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFix
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                       const int32_t* out_rows, int dyn, hipStream_t s) {
+                       const int32_t* out_rows, uint32_t mode, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const uint32_t dbg = post_dbg();
     if (dbg)
         hipLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, dyn);
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, mode);
     else
         hipLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, dyn);
+                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, mode);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;

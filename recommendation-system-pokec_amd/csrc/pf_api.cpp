@@ -301,8 +301,8 @@ int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
                 return PF_OK;
             }
             hipEvent_t a, b;
-            HIPCHK(c, hipEventCreate(&a));
-            HIPCHK(c, hipEventCreate(&b));
+            HIPCHK(c, pf::timing_event(&a));
+            HIPCHK(c, pf::timing_event(&b));
             c->prof_ev.emplace_back(a, b);
         }
         e0 = c->prof_ev[c->prof_used].first;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <thread>
@@ -228,6 +229,19 @@ inline void par_jobs(size_t n, F f, size_t grain = 4) {
         hipError_t _e = (expr);                             \
         if (_e != hipSuccess) return (ctx)->hip_fail(_e, #expr); \
     } while (0)
+
+// A timing event of the profiling pools (pf_profile_*, the job statistics).  Created without
+// the system-scope fence (hipEventDisableSystemFence): every read of these events follows a
+// stream or device synchronisation, and the fence's L2 write-back and invalidation would
+// otherwise run between the timed kernels and perturb them.  PF_EV_FENCE=1 restores the
+// default flags (A/B knob).
+inline hipError_t timing_event(hipEvent_t* e) {
+    static const unsigned flags = [] {
+        const char* v = getenv("PF_EV_FENCE");
+        return (v && atoi(v)) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
+    }();
+    return hipEventCreateWithFlags(e, flags);
+}
 
 template <class T>
 inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {

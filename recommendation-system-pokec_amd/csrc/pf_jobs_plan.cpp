@@ -736,8 +736,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {
             hipEvent_t a, b2;
-            HIPCHK(c, hipEventCreate(&a));
-            HIPCHK(c, hipEventCreate(&b2));
+            HIPCHK(c, timing_event(&a));
+            HIPCHK(c, timing_event(&b2));
             J.stat_ev.emplace_back(a, b2);
         }
         pe0 = J.stat_ev[J.stat_used].first;

@@ -356,13 +356,21 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     hipEvent_t e0, e1;
     int rc = scan_events(c, timed, e0, e1);
     if (rc != PF_OK) return rc;
-    if (timed) HIPCHK(c, hipEventRecord(e0, s));
+    // timed: the events ride in the kernel's dispatch (its own start / end), or, with the
+    // A/B knob PF_EV_MARKERS=1, are two marker packets recorded around it
+    static const bool markers = [] {
+        const char* v = getenv("PF_EV_MARKERS");
+        return v && atoi(v);
+    }();
+    if (timed && markers) HIPCHK(c, hipEventRecord(e0, s));
+    const bool in_dispatch = timed && !markers;
     HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
                               nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
                               reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
-                              reinterpret_cast<const int32_t*>(base + offs_b), post_mode(nq), s));
+                              reinterpret_cast<const int32_t*>(base + offs_b), post_mode(nq),
+                              in_dispatch ? e0 : nullptr, in_dispatch ? e1 : nullptr, s));
     if (timed) {
-        HIPCHK(c, hipEventRecord(e1, s));
+        if (markers) HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;
         c->last_ev1 = e1;
     }

@@ -27,7 +27,7 @@ uint32_t post_var_lds(int n_tok, int n_lists);
 uint32_t post_lds(uint32_t var_lds);
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                       const int32_t* out_rows, uint32_t mode, hipStream_t s);
+                       const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s);
 int post_blocks_per_cu(uint32_t var_lds);
 // plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,

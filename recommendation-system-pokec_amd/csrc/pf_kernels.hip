@@ -15,6 +15,7 @@
 // LDS list of column dot products.  All sigmoid work and the reference's summation
 // order (recommender_similarity.cpp:38-113: public, gender, completion, age, region,
 // clubs, friends, columns ascending) live in a per-candidate epilogue.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -1179,15 +1180,17 @@ uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFix
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                       const int32_t* out_rows, uint32_t mode, hipStream_t s) {
+                       const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const uint32_t dbg = post_dbg();
+    // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
+    // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
     if (dbg)
-        hipLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, mode);
+        hipExtLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0, e1,
+                              0u, ps, pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, mode);
     else
-        hipLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, ps, pool,
-                           img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, mode);
+        hipExtLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0,
+                              e1, 0u, ps, pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, mode);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;

@@ -549,9 +549,30 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
 }
 
 // ---------------------------------------------------------------- K7: clubs
-// recommender_clubs.cpp:34-66 with club_scores[c] += ... in the reference's sequence: every
-// lane of the job's wave walks the same contributions in order and adds only the clubs it
-// owns (dense index % 64 == lane), so each club's double sum is the reference's.
+// recommender_clubs.cpp:34-66: club_scores[c] += ... in the reference's sequence.  One wave per
+// job.  The contribution stream (phase 1: friends in order, each friend's clubs in order;
+// phase 2: friends in order, their rows in order, each fof's clubs in order) is generated 64
+// stream items at a time, one per lane, into an LDS buffer in sequence order (a prefix sum of
+// the lanes' club counts places them); the buffer is then bucketed, stably, by owner lane
+// (dense club index % 64), and every lane adds its own bucket in order.  A club's
+// contributions all go to one lane and keep their sequence order, so each club's double sum
+// is the reference's.  acc[d] == 0.0 marks an untouched club (every contribution is > 0).
+constexpr int kClubBuf = 512;  // contributions per round (LDS: 2 x 12 B each)
+#ifndef PF_CLUBS_SERIAL
+#define PF_CLUBS_SERIAL 0  // 1: the former one-contribution-at-a-time walk (A/B)
+#endif
+
+__device__ __forceinline__ int wave_excl_prefix(int x, int lane, int& total) {
+    int v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    total = __shfl(v, 63);
+    return v - x;
+}
+
 __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
                                                    const int32_t* __restrict__ jix, const int32_t* __restrict__ pool,
                                                    const int64_t* __restrict__ pool64, const float* __restrict__ pout,
@@ -577,7 +598,8 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
             if (g.club_dense[k] == d) return true;
         return false;
     };
-    int32_t* list = ids + J.out_off;  // dense indices of the touched clubs, in touch order
+    int32_t* list = ids + J.out_off;  // dense indices of the touched clubs
+#if PF_CLUBS_SERIAL
     auto add = [&](int32_t d, double v) {
         if ((d & 63) != lane) return;
         if (!touched[d]) {
@@ -586,7 +608,6 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         }
         acc[d] += v;
     };
-    // phase 1 (:34-44): friends in order, w > 0, their clubs not in user_clubs
     for (int j = 0; j < J.nf; ++j) {
         const int r = fpos[j];
         if (r < 0) continue;
@@ -598,7 +619,6 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
             if (!own_club(d)) add(d, w);
         }
     }
-    // phase 2 (:46-66): friends in order with a row, a profile and w > 0; fof in row order
     for (int j = 0; j < J.nf; ++j) {
         const int r = fpos[j];
         if (r < 0) continue;
@@ -622,7 +642,6 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         }
     }
     __syncthreads();
-    // scored list (score, club id); the accumulators go back to zero for the next job
     const int n = s_n;
     for (int i = lane; i < n; i += 64) {
         const int32_t d = list[i];
@@ -631,6 +650,134 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         touched[d] = 0;
         list[i] = g.club_id[d];
     }
+#else
+    (void)touched;
+    __shared__ int32_t bd[kClubBuf];  // a round's contributions in sequence order (-1: own club)
+    __shared__ double bv[kClubBuf];
+    __shared__ int32_t sd[kClubBuf];  // the same bucketed by owner lane, stable
+    __shared__ double sv[kClubBuf];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // one stream item per lane: weight v for the clubs club_dense[cb .. ce) (nothing if !valid)
+    auto chunk = [&](bool valid, double v, int64_t cb, int64_t ce) {
+        const int nc = valid ? (int)(ce - cb) : 0;
+        int total;
+        const int pre = wave_excl_prefix(nc, lane, total);
+        for (int r0 = 0; r0 < total; r0 += kClubBuf) {
+            const int T = min(total - r0, kClubBuf);
+            for (int i = max(pre, r0); i < min(pre + nc, r0 + T); ++i) {
+                const int32_t d = g.club_dense[cb + (i - pre)];
+                bd[i - r0] = own_club(d) ? -1 : d;
+                bv[i - r0] = v;
+            }
+            __syncthreads();
+            // bucket sizes: lane b counts the contributions of bucket b
+            int cnt = 0;
+            for (int i0 = 0; i0 < T; i0 += 64) {
+                const int i = i0 + lane;
+                const int d = i < T ? bd[i] : -1;
+                uint64_t mine = __ballot(d >= 0);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const uint64_t B = __ballot((d >> j) & 1);
+                    mine &= ((lane >> j) & 1) ? B : ~B;
+                }
+                cnt += __popcll(mine);
+            }
+            int placed;
+            const int base = wave_excl_prefix(cnt, lane, placed);
+            // stable placement: a contribution goes after the earlier ones of its bucket
+            int fill = base;
+            for (int i0 = 0; i0 < T; i0 += 64) {
+                const int i = i0 + lane;
+                const int d = i < T ? bd[i] : -1;
+                const uint64_t V = __ballot(d >= 0);
+                uint64_t peers = V, mine = V;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const uint64_t B = __ballot((d >> j) & 1);
+                    peers &= ((d >> j) & 1) ? B : ~B;
+                    mine &= ((lane >> j) & 1) ? B : ~B;
+                }
+                const int at = __shfl(fill, d & 63) + __popcll(peers & lt);
+                if (d >= 0) {
+                    sd[at] = d;
+                    sv[at] = bv[i];
+                }
+                fill += __popcll(mine);
+            }
+            __syncthreads();
+            // every lane adds its bucket in order; a run of one club stays in a register
+            for (int m = base; m < base + cnt;) {
+                const int32_t d = sd[m];
+                double a = acc[d];
+                if (a == 0.0) list[atomicAdd(&s_n, 1)] = d;
+                a += sv[m++];
+                while (m < base + cnt && sd[m] == d) a += sv[m++];
+                acc[d] = a;
+            }
+            __syncthreads();
+        }
+    };
+    // phase 1 (:34-44): friends in order, w > 0, their clubs not in user_clubs
+    for (int j0 = 0; j0 < J.nf; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        double w = 0.0;
+        int64_t cb = 0, ce = 0;
+        if (j < J.nf) {
+            const int r = fpos[j];
+            if (r >= 0) {
+                w = (double)sim[r];
+                if (!(w <= 0.0)) {  // the serial walk's test, NaN included
+                    const int32_t f = frow[j];
+                    cb = g.club_off[f];
+                    ce = g.club_off[f + 1];
+                    ok = true;
+                }
+            }
+        }
+        chunk(ok, w, cb, ce);
+    }
+    // phase 2 (:46-66): friends in order with a row, a profile and w > 0; fof in row order
+    for (int j = 0; j < J.nf; ++j) {
+        const int r = fpos[j];
+        if (r < 0) continue;
+        const int32_t f = frow[j];
+        int32_t len;
+        const int32_t* row = row_of(g, vw, J, pool, f, len);
+        if (len < 0) continue;
+        const double w = (double)sim[r];
+        if (w <= 0.0) continue;
+        const float* S = pout + sreg[r];
+        for (int k0 = 0; k0 < len; k0 += 64) {
+            const int k = k0 + lane;
+            bool ok = false;
+            double contrib = 0.0;
+            int64_t cb = 0, ce = 0;
+            if (k < len) {
+                const int32_t x = row[k];
+                if (x != u && x >= 0 && x < g.n) {
+                    const double sx = (double)S[k];
+                    if (!(sx <= 0.0)) {
+                        contrib = w * sx;
+                        cb = g.club_off[x];
+                        ce = g.club_off[x + 1];
+                        ok = true;
+                    }
+                }
+            }
+            chunk(ok, contrib, cb, ce);
+        }
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int i = lane; i < n; i += 64) {
+        const int32_t d = list[i];
+        score[J.out_off + i] = (float)acc[d];
+        acc[d] = 0.0;
+        list[i] = g.club_id[d];
+    }
+#endif
     if (lane == 0) ncand[jix[slot]] = n;
 }
 

@@ -619,7 +619,8 @@ def main():
     ap.add_argument("--contexts", type=int, default=None,
                     help="cfg3 / cfg5: engine contexts per GPU, each a full replica driven by its own host "
                          "thread; default 3 for cfg3 (r2s: 1 -> 1.1e9, 2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 "
-                         "pair-FAS/s) and 2 for cfg5 (r2t: 1 -> 28.3k, 2 -> 39.8k, 3 -> 35.4k users/s)")
+                         "pair-FAS/s) and 3 for cfg5 (with the bucketed clubs kernel, r2fk: 1 -> 39.7k, 2 -> 51.5k, "
+                         "3 -> 61.7k users/s; r2t, before it: 1 -> 28.3k, 2 -> 39.8k, 3 -> 35.4k)")
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
@@ -642,7 +643,7 @@ def main():
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
     if args.contexts is None:
-        args.contexts = {"cfg3": 3, "cfg5": 2}.get(args.workload, 1)
+        args.contexts = {"cfg3": 3, "cfg5": 3}.get(args.workload, 1)
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local)
     import synth

@@ -738,28 +738,59 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         }
         chunk(ok, w, cb, ce);
     }
-    // phase 2 (:46-66): friends in order with a row, a profile and w > 0; fof in row order
-    for (int j = 0; j < J.nf; ++j) {
-        const int r = fpos[j];
-        if (r < 0) continue;
-        const int32_t f = frow[j];
-        int32_t len;
-        const int32_t* row = row_of(g, vw, J, pool, f, len);
-        if (len < 0) continue;
-        const double w = (double)sim[r];
-        if (w <= 0.0) continue;
-        const float* S = pout + sreg[r];
-        for (int k0 = 0; k0 < len; k0 += 64) {
-            const int k = k0 + lane;
+    // phase 2 (:46-66): friends in order with a row, a profile and w > 0; fof in row order.
+    // 64 friends at a time: their rows flattened into one stream (a prefix of the row
+    // lengths), 64 items per chunk, so short rows share chunks.
+    __shared__ int32_t f_off[64];
+    __shared__ const int32_t* f_row[64];
+    __shared__ const float* f_S[64];
+    __shared__ double f_w[64];
+    for (int j0 = 0; j0 < J.nf; j0 += 64) {
+        const int j = j0 + lane;
+        int32_t len = 0;
+        const int32_t* row = nullptr;
+        const float* S = nullptr;
+        double w = 0.0;
+        if (j < J.nf) {
+            const int r = fpos[j];
+            if (r >= 0) {
+                int32_t l;
+                const int32_t* rw = row_of(g, vw, J, pool, frow[j], l);
+                if (l >= 0) {
+                    w = (double)sim[r];
+                    if (!(w <= 0.0)) {
+                        len = l;
+                        row = rw;
+                        S = pout + sreg[r];
+                    }
+                }
+            }
+        }
+        int total;
+        const int off = wave_excl_prefix(len, lane, total);
+        f_off[lane] = off;
+        f_row[lane] = row;
+        f_S[lane] = S;
+        f_w[lane] = w;
+        __syncthreads();
+        for (int t0 = 0; t0 < total; t0 += 64) {
+            const int t = t0 + lane;
             bool ok = false;
             double contrib = 0.0;
             int64_t cb = 0, ce = 0;
-            if (k < len) {
-                const int32_t x = row[k];
+            if (t < total) {
+                // the friend whose row holds item t: the last one starting at or before t
+                // (friends without items start where the next one does, so they are passed over)
+                int fi = 0;
+#pragma unroll
+                for (int h = 32; h > 0; h >>= 1)
+                    if (f_off[fi + h] <= t) fi += h;
+                const int k = t - f_off[fi];
+                const int32_t x = f_row[fi][k];
                 if (x != u && x >= 0 && x < g.n) {
-                    const double sx = (double)S[k];
+                    const double sx = (double)f_S[fi][k];
                     if (!(sx <= 0.0)) {
-                        contrib = w * sx;
+                        contrib = f_w[fi] * sx;
                         cb = g.club_off[x];
                         ce = g.club_off[x + 1];
                         ok = true;
@@ -768,6 +799,7 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
             }
             chunk(ok, contrib, cb, ce);
         }
+        __syncthreads();
     }
     __syncthreads();
     const int n = s_n;

@@ -96,54 +96,125 @@ def _oracle_worker(args):
     return cands, el
 
 
-def cpu_baseline(desc_ptr, seconds_budget=12.0, all_cores_seconds=6.0):
-    """Oracle (reference algorithm, unordered_map per profile/column) over a bounded prefix of
-    the same corpus: all-candidates interest top-10 per query.  value = candidates per query /
-    the median single-core query time; all_cores = one oracle per host core
-    (context only, not the x100 denominator)."""
-    import pokec_testlib as tl
-    t0 = time.time()
-    orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=desc_ptr)
-    build_s = time.time() - t0
+def _pinned_oracle_child(conn, desc_ptr, core, cfg2_queries, cfg3_users, cfg3_budget):
+    """Forked child (no GPU): pinned to `core`, the oracle (the reference algorithm with its
+    unordered_map data structures, oracle/refcpu.cpp -O3) on the FULL corpus: per-query times of
+    all-candidates interest top-10 (cfg 2) and recommend_collaborative(u, 10, 10000) (cfg 3),
+    then the former 150k-prefix figure; results through the pipe."""
+    try:
+        os.sched_setaffinity(0, {core})
+        import pokec_testlib as tl
+        out = {}
+        t0 = time.time()
+        orc = tl.Oracle(None, desc_ptr=desc_ptr)
+        out["build_s"] = time.time() - t0
+        out["n_users"] = int(orc.L.ro_num_users(orc.h))
+        per = []
+        for q in cfg2_queries:
+            t = time.perf_counter()
+            orc.interest([int(q)], TOPK, tl.PF_MODE_ALL, 0)
+            per.append(time.perf_counter() - t)
+        out["cfg2_query_s"] = per
+        if cfg3_users is not None:
+            calls, el, n = 0, 0.0, 0
+            for q in cfg3_users:
+                if n >= 16 and el >= cfg3_budget:
+                    break
+                orc.fas_calls(True)
+                t = time.perf_counter()
+                orc.collab([int(q)], TOPK, CFG3_LIMIT)
+                dt = time.perf_counter() - t
+                c = orc.fas_calls(True)
+                if c == 0:
+                    continue
+                calls, el, n = calls + c, el + dt, n + 1
+            out["cfg3"] = {"fas_calls": calls, "seconds": el, "queries": n}
+        orc.close()
+        # the former figure, kept for comparison: the median query over a 150k-user prefix
+        orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=desc_ptr)
+        npre = int(orc.L.ro_num_users(orc.h))
+        rng = np.random.default_rng(123)
+        per, el = [], 0.0
+        while el < 6.0 and len(per) < 64:
+            q = int(rng.integers(1, npre + 1))
+            t = time.perf_counter()
+            orc.interest([q], TOPK, tl.PF_MODE_ALL, 0)
+            dt = time.perf_counter() - t
+            per.append(dt)
+            el += dt
+        out["prefix_query_s"] = per
+        out["prefix_n_users"] = npre
+        orc.close()
+        conn.send(out)
+    except Exception as e:  # reported, never fatal to the bench
+        conn.send({"error": repr(e)[:300]})
+    finally:
+        conn.close()
+
+
+def cpu_baselines(desc_ptr, n_users, cfg3_users=None, cfg3_budget=10.0, all_cores_seconds=6.0):
+    """the oracle timed on this box's host, one core pinned (os.sched_setaffinity in a
+    forked child, before this process touches the GPU), on the FULL corpus the GPU line scores:
+    cfg 2 = the median of 3 all-candidates interest top-10 queries (candidates / s); cfg 3 (when
+    cfg3_users is given) = pair-FAS/s over >= 16 recommend_collaborative(u, 10, 10000) queries and
+    about cfg3_budget seconds.  The former 150k-user-prefix median and an all-cores context figure
+    (one oracle process per core on that prefix) ride along as second fields."""
+    import multiprocessing as mp
+    core = min(os.sched_getaffinity(0))
     rng = np.random.default_rng(123)
-    per, el = [], 0.0
-    while el < seconds_budget and len(per) < 64:
-        q = int(rng.integers(1, SAMPLE_USERS + 1))
-        t = time.perf_counter()
-        orc.interest([q], TOPK, tl.PF_MODE_ALL, 0)
-        dt = time.perf_counter() - t
-        per.append(dt)
-        el += dt
-    n_cand = orc.L.ro_num_users(orc.h) - 1
-    orc.close()
-    med = float(np.median(per))
-    out = {"value": n_cand / med, "unit": "candidates/s", "cores": 1, "kind": "port",
-           "cpu_model": cpu_model(), "median_query_s": med, "queries": len(per),
-           "mean_rate": n_cand * len(per) / el,
-           "sample": f"{len(per)} all-candidates interest top-10 queries over the first {SAMPLE_USERS} users of the "
-                     f"same synthetic corpus (oracle/refcpu.cpp -O3, single thread, median of the per-query times, "
-                     f"{el:.1f}s timed, {build_s:.1f}s map build untimed)"}
-    # all-cores context: one oracle process per core (the box's CPU share is 16)
+    q2 = [int(x) for x in rng.integers(1, n_users + 1, 3)]
+    ctx = mp.get_context("fork")
+    a, b = ctx.Pipe(duplex=False)
+    p = ctx.Process(target=_pinned_oracle_child, args=(b, desc_ptr, core, q2, cfg3_users, cfg3_budget))
+    t0 = time.time()
+    p.start()
+    b.close()
+    res = a.recv()
+    p.join()
+    wall = time.time() - t0
+    if "error" in res:
+        return {"value": None, "error": res["error"]}, None
+    n_cand = res["n_users"] - 1
+    med = float(np.median(res["cfg2_query_s"]))
+    pre = res["prefix_query_s"]
+    pmed = float(np.median(pre))
+    base2 = {"value": n_cand / med, "unit": "candidates/s", "cores": 1, "kind": "port", "pinned_core": core,
+             "cpu_model": cpu_model(), "median_query_s": med, "query_s": res["cfg2_query_s"], "queries": len(q2),
+             "sample": f"{len(q2)} all-candidates interest top-10 queries (seed 123) over the full {res['n_users']}-user "
+                       f"corpus the GPU line scores (oracle/refcpu.cpp -O3, one thread pinned to core {core}, median of "
+                       f"the per-query times; {res['build_s']:.1f}s map build untimed, {wall:.0f}s wall)",
+             "prefix": {"value": (res["prefix_n_users"] - 1) / pmed, "median_query_s": pmed, "queries": len(pre),
+                        "n_users": res["prefix_n_users"],
+                        "note": "the round-2 figure: the same oracle on the first 150,000 users only"}}
     global _DESC
     _DESC = desc_ptr
     try:
-        import multiprocessing as mp
         ncores = min(16, len(os.sched_getaffinity(0)))
-        ctx = mp.get_context("fork")
         with ctx.Pool(ncores) as pool:
-            res = pool.map(_oracle_worker, [(1000 + i, all_cores_seconds) for i in range(ncores)])
-        out["all_cores"] = {"value": sum(c for c, _ in res) / max(e for _, e in res), "cores": ncores,
-                            "note": "one oracle process per core, each on the same 150k-user prefix; context only"}
+            r = pool.map(_oracle_worker, [(1000 + i, all_cores_seconds) for i in range(ncores)])
+        base2["all_cores"] = {"value": sum(c for c, _ in r) / max(e for _, e in r), "cores": ncores,
+                              "note": "one oracle process per core, each on the 150k-user prefix; context only"}
     except Exception as e:  # context figure only
-        out["all_cores"] = {"value": None, "error": str(e)[:200]}
-    return out
+        base2["all_cores"] = {"value": None, "error": str(e)[:200]}
+    base3 = None
+    if cfg3_users is not None and res.get("cfg3", {}).get("seconds"):
+        c3 = res["cfg3"]
+        base3 = {"value": c3["fas_calls"] / c3["seconds"], "unit": "pair-FAS/s", "cores": 1, "kind": "port",
+                 "pinned_core": core, "cpu_model": cpu_model(), "queries": c3["queries"], "fas_calls": c3["fas_calls"],
+                 "sample": f"{c3['queries']} recommend_collaborative(u, 10, {CFG3_LIMIT}) queries (the GPU line's first "
+                           f"query users) over the full {res['n_users']}-user corpus (oracle/refcpu.cpp -O3, one thread "
+                           f"pinned to core {core}; profile_similarity calls counted by the oracle, "
+                           f"{c3['seconds']:.1f}s timed)"}
+    return base2, base3
 
 
-def pmc_pass(args, kernel_name):
-    """HBM bytes per timed launch of the scan kernel from a rocprofv3 --pmc FETCH_SIZE pass of
-    this same command, run as a child before this process touches the GPU.  FETCH_SIZE (KiB)
-    x 1024 x the gfx950 factor (profiles/fetch_calib_r2.json: the factor measured on known
-    byte counts of the kernel's load widths; MI355X_MICROARCH.md HBM section)."""
+def pmc_pass(args, select):
+    """HBM bytes per timed launch of each kernel in `select` (name -> a function picking the timed
+    launches from that kernel's FETCH_SIZE values in dispatch order) from one rocprofv3 --pmc
+    FETCH_SIZE pass of this same command, run as a child before this process touches the GPU.
+    FETCH_SIZE (KiB) x 1024 x the gfx950 factor (profiles/fetch_calib_r2.json: the factor measured
+    on known byte counts of the kernel's load widths; MI355X_MICROARCH.md HBM section).
+    Returns {name: (info or None, error or None)}."""
     import csv
     import glob
     import shutil
@@ -151,45 +222,55 @@ def pmc_pass(args, kernel_name):
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
-        return None, "rocprofv3 not found"
-    factor, fsrc = 2.0, "MI355X_MICROARCH.md (16-B/lane streams)"
-    cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
-    if os.path.exists(cal) and kernel_name == "fas_post_kernel":  # 4/8-B loads; K1 / K1' read 16-B steps
-        try:
-            with open(cal) as f:
-                c = json.load(f)
-            factor, fsrc = float(c["k5_factor"]), "profiles/fetch_calib_r2.json"
-        except Exception:
-            pass
+        return {k: (None, "rocprofv3 not found") for k in select}
+    factors = {}
+    for k in select:
+        factor, fsrc = 2.0, "MI355X_MICROARCH.md (16-B/lane streams)"
+        cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
+        if os.path.exists(cal) and k == "fas_post_kernel":  # 4/8-B loads; K1 / K1' read 16-B steps
+            try:
+                with open(cal) as f:
+                    c = json.load(f)
+                factor, fsrc = float(c["k5_factor"]), "profiles/fetch_calib_r2.json"
+            except Exception:
+                pass
+        factors[k] = (factor, fsrc)
     d = tempfile.mkdtemp(prefix="pf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    cmd = [prof, "--pmc", "FETCH_SIZE", "--kernel-include-regex", kernel_name, "-T", "--output-format", "csv",
+    cmd = [prof, "--pmc", "FETCH_SIZE", "--kernel-include-regex", "|".join(select), "-T", "--output-format", "csv",
            "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--gpus", "1",
            "--steps", str(args.steps), "--warmup", str(args.warmup), "--no-cpu-baseline", "--no-pmc",
            "--workload", args.workload, "--scan-kernel", args.scan_kernel, "--users", str(args.users),
-           "--contexts", str(args.contexts), "--cfg5-batch", str(args.cfg5_batch)]
+           "--contexts", str(args.contexts), "--cfg5-batch", str(args.cfg5_batch),
+           "--cfg3-steps", str(args.cfg3_steps)]
+    if args.no_cfg3:
+        cmd.append("--no-cfg3")
     try:
         r = subprocess.run(["timeout", "-s", "KILL", "240"] + cmd, capture_output=True, text=True,
                            env={**os.environ, "TMPDIR": os.environ.get("TMPDIR", "/tmp")})
         if r.returncode != 0:
-            return None, f"rocprofv3 pass rc={r.returncode}: {r.stderr[-300:]}"
-        vals = []
+            return {k: (None, f"rocprofv3 pass rc={r.returncode}: {r.stderr[-300:]}") for k in select}
+        vals = {k: [] for k in select}
         for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(p) as f:
                 for row in csv.DictReader(f):
-                    if row.get("Counter_Name") == "FETCH_SIZE" and kernel_name in row.get("Kernel_Name", ""):
-                        vals.append((int(row.get("Dispatch_Id", len(vals))), float(row["Counter_Value"])))
-        vals.sort()
-        if args.workload in ("cfg2", "cfg4"):
-            vals = [v for _, v in vals][-args.steps:]  # the timed launches (the warmup ones come first)
-        else:  # cfg3 / cfg5: several pair launches per step, warmup steps of the same kind: all of them
-            vals = [v for _, v in vals]
-        if not vals:
-            return None, "no FETCH_SIZE rows"
-        mean = sum(vals) / len(vals)
-        return {"bytes_per_launch": mean * 1024 * factor, "fetch_size_kib_mean": mean, "launches": len(vals),
-                "factor": factor, "factor_source": fsrc}, None
+                    if row.get("Counter_Name") != "FETCH_SIZE":
+                        continue
+                    for k in select:
+                        if k in row.get("Kernel_Name", ""):
+                            vals[k].append((int(row.get("Dispatch_Id", len(vals[k]))), float(row["Counter_Value"])))
+        out = {}
+        for k, pick in select.items():
+            v = pick([x for _, x in sorted(vals[k])])
+            if not v:
+                out[k] = (None, "no FETCH_SIZE rows")
+                continue
+            mean = sum(v) / len(v)
+            factor, fsrc = factors[k]
+            out[k] = ({"bytes_per_launch": mean * 1024 * factor, "fetch_size_kib_mean": mean, "launches": len(v),
+                       "factor": factor, "factor_source": fsrc}, None)
+        return out
     except Exception as e:
-        return None, str(e)[:300]
+        return {k: (None, str(e)[:300]) for k in select}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -245,58 +326,26 @@ CFG3_QUERIES = 64      # cfg 3 step: a batch of seeded query users
 CFG3_LIMIT = 10000     # recommend_collaborative's default candidate_limit (include/recommender.h)
 
 
-def cpu_baseline_collab(desc_ptr, n_queries=16, seconds_budget=10.0):
-    """Oracle recommend_collaborative (reference algorithm, one core) over a bounded prefix of the
-    same corpus: pair-FAS/s = the oracle's profile_similarity evaluations / time, over at least 16
-    seeded queries with friends inside the prefix (the 16-query set for cfg 3) and
-    about 10 s of CPU work."""
-    import pokec_testlib as tl
-    t0 = time.time()
-    orc = tl.Oracle(None, max_users=SAMPLE_USERS, desc_ptr=desc_ptr)
-    build_s = time.time() - t0
-    rng = np.random.default_rng(44)
-    per, calls, el = [], 0, 0.0
-    tried = 0
-    while (len(per) < n_queries or el < seconds_budget) and tried < 5000:
-        tried += 1
-        q = int(rng.integers(1, SAMPLE_USERS + 1))
-        orc.fas_calls(True)
-        t = time.perf_counter()
-        orc.collab([q], TOPK, CFG3_LIMIT)
-        dt = time.perf_counter() - t
-        nc = orc.fas_calls(True)
-        if nc == 0:  # no friend with a profile inside the prefix
-            continue
-        per.append(nc / dt)
-        calls += nc
-        el += dt
-    orc.close()
-    return {"value": calls / el if el > 0 else None, "unit": "pair-FAS/s", "cores": 1, "kind": "port",
-            "cpu_model": cpu_model(), "median_query_rate": float(np.median(per)) if per else None,
-            "queries": len(per), "fas_calls": calls,
-            "sample": f"{len(per)} recommend_collaborative(u, 10, {CFG3_LIMIT}) queries over the first {SAMPLE_USERS} "
-                      f"users of the same corpus (oracle/refcpu.cpp -O3, one core; profile_similarity calls counted "
-                      f"by the oracle, {el:.1f}s timed, {build_s:.1f}s map build untimed)"}
+def cfg3_queries(users, warm, steps, rank=0, world=1):
+    """cfg 3's query users: per step a batch of CFG3_QUERIES seeded uids (seed 4), this rank's
+    share of each at N > 1."""
+    rng = np.random.default_rng(4)
+    qstream = rng.integers(1, users + 1, size=(warm + steps, CFG3_QUERIES)).astype(np.int32)
+    return [qs[rank::world] for qs in qstream]
 
 
-def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, open_s):
+def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None):
     """cfg 3 (BASELINE configs[2]): collaborative FoF propagation top-10 on the full corpus.  A
     step = recommend_collaborative(u, 10, 10000) for a batch of 64 seeded users (this rank's share
-    of them at N > 1: query users split, strong scaling), through the device job pipeline
-    (K3 gather, K6 images, K1' pairs, K4' sums, K8 top-k) and back to the host.  value =
-    FAS pairs scored / s (SURVEY D3's cfg-3 unit, |F| + |F|.|C| per user).
-    --contexts C > 1: C engine contexts on the GPU (each its own stream and workspaces, a full
-    replica), step i on context i % C from its own host thread, so one context's host planning
-    overlaps another's device work (ctypes releases the GIL during the calls)."""
-    Q = CFG3_QUERIES
+    at N > 1), through the device job pipeline (K3 gather, K6 images, K1' pairs, K4' sums, K8
+    top-k) and back to the host.  Returns the timing and counters: pair-FAS scored (SURVEY D3's
+    cfg-3 unit, |F| + |F|.|C| per user) and the pair kernel's HIP-event time per launch (its
+    roofline).  With C = len(engs) > 1 contexts, step i runs on context i % C from its own host
+    thread (ctypes releases the GIL), so one context's host planning overlaps another's device work."""
     eng = engs[0]
     C = len(engs)
-    steps, warm = args.steps, args.warmup
-    rng = np.random.default_rng(4)
-    qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
-    mine = [qs[rank::world] for qs in qstream]
     for i in range(warm):
-        eng.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
+        engs[i % C].recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -336,16 +385,20 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, open_
     st = eng.jobs_stats()
     eng.jobs_stats_reset(time_pairs=False, count=False)
     st["pair_ms"], st["pair_launches"] = timing["pair_ms"], timing["pair_launches"]
-    pairs, cands = st["pairs"], st["candidates"]
+    st["elapsed"], st["results"] = elapsed, nres
     if dist:
-        t = torch.tensor([elapsed, pairs, cands], dtype=torch.float64, device="cuda")
+        t = torch.tensor([st["pairs"], st["candidates"]], dtype=torch.float64, device="cuda")
         tm = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        pairs, cands, elapsed = float(t[1]), float(t[2]), float(tm.item())
-    value = pairs / elapsed
-    ms = st["pair_ms"]
-    launches = st["pair_launches"]
+        st["pairs"], st["candidates"], st["elapsed"] = float(t[0]), float(t[1]), float(tm.item())
+    return st
+
+
+def cfg3_fields(st, steps, pmc):
+    """value + roofline fields of a cfg-3 measurement (measure_cfg3)."""
+    elapsed = st["elapsed"]
+    ms, launches = st["pair_ms"], st["pair_launches"]
     avg_ms = ms / launches if launches else None
     phys = (st["pair_record_bytes"] + st["pair_image_bytes"]) / launches if launches else None
 
@@ -354,36 +407,51 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, open_
 
     achieved = rate(phys)
     alg_pl = st["pair_alg_bytes"] / launches if launches else None
-    traffic = pmc["bytes_per_launch"] if pmc else None
-    rec = {
-        "metric": METRIC, "value": value, "unit": "pair-FAS/s", "n_gpus": world, "steps": steps, "warmup": warm,
-        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
-        "config": {"workload": f"cfg3: collaborative FoF top-10 on the full {args.users}-user corpus, {Q} query users "
-                               f"per step (limit {CFG3_LIMIT})" + (f", split over {world} GPUs" if world > 1 else ""),
-                   "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{Q}_limit{CFG3_LIMIT}_world{world}",
-                   "n_users": args.users, "queries_per_step": Q, "topk": TOPK, "limit": CFG3_LIMIT,
-                   "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")},
-        "candidates_per_s": cands / elapsed, "queries_per_s": Q * steps / elapsed,
-        "pairs_per_step": pairs / steps, "candidates_per_step": cands / steps, "results": nres,
+    traffic = pmc[0]["bytes_per_launch"] if pmc and pmc[0] else None
+    return {
+        "value": st["pairs"] / elapsed, "unit": "pair-FAS/s", "ms_per_step": elapsed * 1e3 / steps,
+        "candidates_per_s": st["candidates"] / elapsed, "queries_per_s": CFG3_QUERIES * steps / elapsed,
+        "pairs_per_step": st["pairs"] / steps, "candidates_per_step": st["candidates"] / steps,
+        "results": st["results"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "fas_pairs_kernel", "avg_launch_ms": avg_ms, "timed_launches": launches,
                      "bytes_per_launch": phys,
                      "bytes_model": "pf_jobs_stats: per scored pair the candidate's 48-B tile-store headers + record "
-                                    "words (K1' walks the record), per 256-pair block the staged query image",
+                                    "words (K1' walks the record), per pair block the staged query image",
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
-                     "traffic_source": pmc if pmc else pmc_err,
+                     "traffic_source": (pmc[0] if pmc and pmc[0] else (pmc[1] if pmc else "not run")),
                      "alg_effective_gbs": rate(alg_pl),
                      "alg_effective_frac": None if rate(alg_pl) is None else rate(alg_pl) / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_pl,
                      "pair_kernel_share_of_step": (ms / (elapsed * 1e3)) if elapsed > 0 else None},
-        "open_s": open_s,
+    }
+
+
+def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, open_s):
+    """--workload cfg3: the cfg-3 measurement as the bench line (query users split over the ranks:
+    strong scaling); value = FAS pairs scored / s."""
+    steps, warm = args.steps, args.warmup
+    mine = cfg3_queries(args.users, warm, steps, rank, world)
+    st = measure_cfg3(engs, mine, warm, steps, dist, torch)
+    C = len(engs)
+    f = cfg3_fields(st, steps, pmc)
+    rec = {
+        "metric": METRIC, "value": f.pop("value"), "unit": f.pop("unit"), "n_gpus": world, "steps": steps,
+        "warmup": warm, "ms_per_step": f.pop("ms_per_step"), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
+        "config": {"workload": f"cfg3: collaborative FoF top-10 on the full {args.users}-user corpus, {CFG3_QUERIES} "
+                               f"query users per step (limit {CFG3_LIMIT})" + (f", split over {world} GPUs" if world > 1 else ""),
+                   "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{CFG3_QUERIES}_limit{CFG3_LIMIT}_world{world}",
+                   "n_users": args.users, "queries_per_step": CFG3_QUERIES, "topk": TOPK, "limit": CFG3_LIMIT,
+                   "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")},
+        **f, "open_s": open_s,
     }
     if rank == 0 and world == 1 and base is not None:
         rec["cpu_baseline"] = base
-        rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None
+        rec["speedup_vs_cpu"] = rec["value"] / base["value"] if base.get("value") else None
     elif rank == 0:
         rec["cpu_baseline"] = None
     if rank == 0:
@@ -405,11 +473,43 @@ def cfg5_dir(users):
     return os.path.join(os.environ.get("TMPDIR", "/tmp"), f"pf_cfg5_{users}u_seed1")
 
 
-def cpu_baseline_cfg5(ds_dir, users_timed=24):
+def _pinned_call(fn, *a):
+    """fn(*a) in a forked child pinned to one core (the CPU baseline single-threaded and
+    pinned), before this process touches the GPU; returns (result, core)."""
+    import multiprocessing as mp
+    core = min(os.sched_getaffinity(0))
+    ctx = mp.get_context("fork")
+    rd, wr = ctx.Pipe(duplex=False)
+
+    def child():
+        try:
+            os.sched_setaffinity(0, {core})
+            wr.send(fn(*a))
+        except Exception as e:
+            wr.send({"value": None, "error": repr(e)[:300]})
+        finally:
+            wr.close()
+    p = ctx.Process(target=child)
+    p.start()
+    wr.close()
+    res = rd.recv()
+    p.join()
+    return res, core
+
+
+def cpu_baseline_cfg5(ds_dir, users_timed=101):
     """Oracle run_recommendation_tests_sample (the reference algorithm and its O(N) adj_mod copy
     per user, recommendation_tests.cpp:68-169) on the SAME full corpus, one core: users/s =
     (S - 1) extra users / (t(S) - t(1)), the marginal per-user rate without the per-call sampling
     plan (which favours the CPU: the GPU step pays its plan), plus the whole-call rate."""
+    res, core = _pinned_call(_cpu_baseline_cfg5, ds_dir, users_timed)
+    if res.get("value") is not None:
+        res["pinned_core"] = core
+        res["sample"] += f"; pinned to core {core}"
+    return res
+
+
+def _cpu_baseline_cfg5(ds_dir, users_timed):
     import pokec_fas as pf
     import pokec_testlib as tl
     t0 = time.time()
@@ -464,8 +564,8 @@ def run_cfg5(args, world, rank, local):
         if not args.no_cpu_baseline:
             base = cpu_baseline_cfg5(d)
             log(f"cpu baseline: {base['value']} users/s ({base['sample']})")
-        if not args.no_pmc:
-            pmc, pmc_err = pmc_pass(args, "fas_pairs_kernel")
+        if not args.no_pmc:  # every pair launch (several per step, warmup steps of the same kind)
+            pmc, pmc_err = pmc_pass(args, {"fas_pairs_kernel": lambda v: v})["fas_pairs_kernel"]
             if pmc_err:
                 log(f"pmc pass: {pmc_err}")
     import torch
@@ -633,6 +733,11 @@ def main():
                     help="HIP-event timing on every n-th scan launch of the timed region (1 = all)")
     ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
                     help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
+    ap.add_argument("--no-cfg3", action="store_true",
+                    help="cfg2 at N = 1: skip the cfg-3 sub-record (collaborative FoF top-10, 64 users per step)")
+    ap.add_argument("--cfg3-steps", type=int, default=20, help="timed steps of the cfg-3 sub-record")
+    ap.add_argument("--n1-steps", type=int, default=5,
+                    help="N > 1: steps rank 0 times the same workload unsharded on its own GPU (n1_same_workload)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -652,19 +757,37 @@ def main():
     corpus = synth.Corpus(n_users=args.users, seed=1, edge_cases=0, threads=16)
     desc = corpus.desc_ptr()
     t1 = time.time()
-    # rank 0 at N = 1, before this process touches the GPU: the CPU baseline (its all-cores part
-    # forks oracle workers) and the rocprofv3 PMC pass (a child running this same command)
+    # the cfg-3 sub-record of the default N = 1 line (the north star's FoF half, BASELINE cfg 3)
+    sub3 = args.workload == "cfg2" and world == 1 and not args.no_cfg3
+    W3 = 3
+    # rank 0 at N = 1, before this process touches the GPU: the CPU baselines (forked, pinned
+    # children) and the rocprofv3 PMC pass (a child running this same command)
     want_kernel = "fas_scan_kernel" if args.scan_kernel == "stream" else "fas_post_kernel"
-    if args.workload == "cfg3":
-        want_kernel = "fas_pairs_kernel"
-    base, pmc, pmc_err = None, None, "not run (N > 1 or --no-pmc)"
+    base, base3, pmcs = None, None, {}
     if rank == 0 and world == 1:
+        if args.workload == "cfg3" or sub3:
+            steps3 = args.steps if args.workload == "cfg3" else args.cfg3_steps
+            warm3 = args.warmup if args.workload == "cfg3" else W3
+            users3 = [int(u) for qs in cfg3_queries(args.users, warm3, steps3)[warm3:] for u in qs]
         if not args.no_cpu_baseline:
-            base = cpu_baseline_collab(desc) if args.workload == "cfg3" else cpu_baseline(desc)
+            base, base3 = cpu_baselines(desc, args.users, users3 if (args.workload == "cfg3" or sub3) else None)
+            if args.workload == "cfg3":
+                base = base3
+            log(f"cpu baseline: {base}")
         if not args.no_pmc:
-            pmc, pmc_err = pmc_pass(args, want_kernel)
-            if pmc_err:
-                log(f"pmc pass: {pmc_err}")
+            sel = {}
+            if args.workload in ("cfg2", "cfg4"):
+                sel[want_kernel] = lambda v, k=args.steps: v[len(v) - k:] if len(v) >= k else []
+            if args.workload == "cfg3":
+                sel["fas_pairs_kernel"] = lambda v: v  # warmup and timed steps alike
+            elif sub3:
+                # pair launches: the top-k self-check (1), cfg 3's warmup (W3), its timed steps, the
+                # counting replay; the timed ones
+                sel["fas_pairs_kernel"] = lambda v, w=W3, k=args.cfg3_steps: v[1 + w:1 + w + k]
+            pmcs = pmc_pass(args, sel)
+            for k, (_, e) in pmcs.items():
+                if e:
+                    log(f"pmc pass {k}: {e}")
 
     import torch
     local = local % max(1, torch.cuda.device_count())  # --dist-backend gloo: ranks may share a GPU
@@ -677,13 +800,15 @@ def main():
     t3 = time.time()
     if args.workload == "cfg3":
         engs = [eng] + [pf.FasEngine(desc, local) for _ in range(max(1, args.contexts) - 1)]
-        return run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, pmc_err, time.time() - t2)
+        return run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmcs.get("fas_pairs_kernel"),
+                        time.time() - t2)
     eng.set_shard(rank, world)
     eng.set_scan_kernel({"auto": pf.PF_SCAN_AUTO, "stream": pf.PF_SCAN_STREAM, "postings": pf.PF_SCAN_POSTINGS}
                         [args.scan_kernel])
     lay = eng.layout()
     kernel_name = "fas_post_kernel" if lay.scan_kernel == pf.PF_SCAN_POSTINGS else "fas_scan_kernel"
-    if kernel_name != want_kernel:
+    pmc, pmc_err = pmcs.get(kernel_name, (None, "not run (N > 1 or --no-pmc)"))
+    if rank == 0 and world == 1 and not args.no_pmc and kernel_name != want_kernel:
         pmc, pmc_err = None, f"the pass profiled {want_kernel}, the engine runs {kernel_name}"
     log(f"[rank {rank}] corpus {t1 - t0:.1f}s, engine open {t3 - t2:.1f}s, stream {lay.stream_bytes / 1e9:.3f} GB, "
         f"alg {lay.alg_bytes / 1e9:.3f} GB, packed={lay.packed_tokens}")
@@ -709,6 +834,28 @@ def main():
         eng.scan_keys_async(qstream[i], k, local_keys.data_ptr(), sptr)
         dist.all_gather_into_tensor(gathered, local_keys)
         eng.merge_keys_async(gathered.data_ptr(), world, Q, k, final.data_ptr(), sptr)
+
+    n_cand = eng.num_users - 1  # candidates per query: every profile but the query (minus adj[q])
+    # N > 1: rank 0 first runs the same workload unsharded on its own GPU (the like-for-like N = 1
+    # point of the driver's scaling curve); the other ranks wait at the barrier
+    n1 = None
+    if world > 1:
+        if rank == 0:
+            eng.set_shard(0, 1)
+            for i in range(min(warm, 2)):
+                eng.scan_keys_async(qstream[i], k, final.data_ptr(), sptr)
+            torch.cuda.synchronize()
+            ns = max(1, min(args.n1_steps, steps))
+            ta = time.perf_counter()
+            for i in range(warm, warm + ns):
+                eng.scan_keys_async(qstream[i], k, final.data_ptr(), sptr)
+            torch.cuda.synchronize()
+            el1 = time.perf_counter() - ta
+            n1 = {"value": Q * n_cand * ns / el1, "unit": "candidates/s", "steps": ns, "ms_per_step": el1 * 1e3 / ns,
+                  "note": "rank 0 alone, the same queries over the whole corpus (unsharded, no collective), timed "
+                          "before the sharded steps: the like-for-like N = 1 point for this line's value"}
+            eng.set_shard(rank, world)
+        dist.barrier()
 
     for i in range(warm):
         step(i)
@@ -743,7 +890,6 @@ def main():
     chk = eng.fas_pairs(np.full(len(uids), qstream[warm + steps - 1][0], np.int32), uids)
     consistent = bool(len(uids) == k and np.array_equal(chk.view(np.uint32), scores.view(np.uint32)))
 
-    n_cand = eng.num_users - 1  # candidates per query: every profile but the query (minus adj[q])
     value = Q * n_cand * steps / elapsed
     # bytes per launch by the kernel's access pattern, over the queries timed (this rank's shard)
     # one call per step: the byte model counts the image staging of a launch of Q queries
@@ -806,11 +952,27 @@ def main():
                               "postings scan reads only the query's lists, so that effective rate can pass the peak)")},
         "topk_selfcheck": consistent,
     }
+    if n1 is not None:
+        rec["n1_same_workload"] = n1
     if rank == 0 and world == 1 and base is not None:
         rec["cpu_baseline"] = base
-        rec["speedup_vs_cpu"] = value / base["value"]
+        rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None
     elif rank == 0:
         rec["cpu_baseline"] = None
+    if sub3:
+        # cfg 3 (BASELINE configs[2]) on the same engine: recommend_collaborative(u, 10, 10000) for
+        # 64 seeded users per step, one engine context (the default line's own replica)
+        ta = time.perf_counter()
+        mine = cfg3_queries(args.users, W3, args.cfg3_steps)
+        st = measure_cfg3([eng], mine, W3, args.cfg3_steps, None, torch)
+        f3 = cfg3_fields(st, args.cfg3_steps, pmcs.get("fas_pairs_kernel"))
+        f3.update({"steps": args.cfg3_steps, "warmup": W3, "contexts": 1,
+                   "workload": f"cfg3: recommend_collaborative(u, {TOPK}, {CFG3_LIMIT}) for {CFG3_QUERIES} seeded users "
+                               f"per step on the full {args.users}-user corpus, one engine context",
+                   "cpu_baseline": base3,
+                   "speedup_vs_cpu": f3["value"] / base3["value"] if base3 and base3.get("value") else None,
+                   "wall_s": time.perf_counter() - ta})
+        rec["cfg3"] = f3
     if rank == 0:
         print(json.dumps(rec), flush=True)
     eng.close()

@@ -36,6 +36,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "pokec_fas.h"
 
@@ -112,6 +113,38 @@ int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, d
  * interest_hit_rate, avg_club_prec_at_k, avg_club_recall_at_k}. */
 int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5);
 
+/* Result digest of one recommender call (a parity probe): FNV-1a over the 32-bit words of
+ * every returned (id, score bits) pair in result order, then the count.  Two runs returned the
+ * same list, ids and score bits, iff (practically) their digests are equal. */
+static inline uint64_t pf_result_digest(const int32_t* ids, const float* scores, int32_t n) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int32_t i = 0; i < n; ++i) {
+        uint32_t w[2];
+        w[0] = (uint32_t)ids[i];
+        memcpy(&w[1], &scores[i], 4);
+        for (int k = 0; k < 2; ++k) {
+            h ^= w[k];
+            h *= 0x100000001b3ull;
+        }
+    }
+    h ^= (uint32_t)n;
+    h *= 0x100000001b3ull;
+    return h;
+}
+
+/* The two drivers with every tested user's results as digests (parity probes of the
+ * drivers' adjacency handling; the metrics alone cannot see most of a wrong list, e.g.
+ * recommend_clubs_collab never returns the user's own clubs, so the club precision of
+ * recommendation_tests.cpp:140-153 is always 0):
+ *   pf_holdout_friends_digest:      out_digest[i] = user i's collaborative list;
+ *   pf_recommendation_tests_digest: out_digest[4i .. 4i+3] = graph, collaborative, interest,
+ *                                   clubs lists of user i.
+ * *n_out = users tested.  The batched forms below have _digest twins in plan order. */
+int pf_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, uint64_t* out_digest,
+                              int32_t cap, int32_t* n_out);
+int pf_recommendation_tests_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                   uint64_t* out_digest, int32_t cap, int32_t* n_out);
+
 /* Batched, shardable forms of the two drivers (BASELINE cfg 5).  The plan
  * (sampled users and their held-out friends, in the sequential driver's rng order) is computed
  * up front; each user's query reads the adjacency it would have seen (test.cpp: every earlier
@@ -129,6 +162,13 @@ int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
 int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
                                  int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
                                  double* out_club, int32_t cap, int32_t* n_plan);
+/* digests of the plan entries this shard evaluates (layout as the sequential _digest forms) */
+int pf_eval_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard,
+                                   int32_t nshards, int32_t batch, uint64_t* out_digest, int32_t cap,
+                                   int32_t* n_plan);
+int pf_eval_recommendation_tests_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                        int32_t shard, int32_t nshards, int32_t batch, uint64_t* out_digest,
+                                        int32_t cap, int32_t* n_plan);
 
 #ifdef __cplusplus
 }

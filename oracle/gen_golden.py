@@ -36,9 +36,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # name -> generator params + writer options + harness options
 CORPORA = {
     "A": dict(n_users=2500, seed=11, edge_cases=1, normalizers=1, median=1,
-              npairs=60000, pair_seed=7, holdout=12, rectest=6),
+              npairs=60000, pair_seed=7, holdout=12, rectest=6, digest_holdout=60, digest_rectest=120),
     "B": dict(n_users=1200, seed=23, edge_cases=1, normalizers=0, median=0,
-              npairs=20000, pair_seed=9, holdout=0, rectest=0),
+              npairs=20000, pair_seed=9, holdout=0, rectest=0, digest_holdout=0, digest_rectest=0),
 }
 # config 1 plumbing (BASELINE.json configs[0]): api_cli with load_users=10000
 API_CORPUS = dict(n_users=10000, seed=31, edge_cases=0, normalizers=1, median=1)
@@ -48,7 +48,8 @@ def run_harness(work, out, c):
     exe = os.path.join(HERE, "_ref", "ref_fixture")
     with open(os.path.join(out, "harness_stdout.txt"), "w") as so:
         subprocess.run([exe, work, out, str(c["npairs"]), str(c["pair_seed"]),
-                        str(c["holdout"]), str(c["rectest"])], check=True, stdout=so)
+                        str(c["holdout"]), str(c["rectest"]), str(c["digest_holdout"]), str(c["digest_rectest"])],
+                       check=True, stdout=so)
     os.remove(os.path.join(out, "harness_stdout.txt"))
 
 

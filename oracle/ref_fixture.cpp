@@ -10,7 +10,7 @@
 // exactly what the reference's own CLI would compute on the same data/ dir.
 //
 // usage: ref_fixture <workdir-with-data-and-config> <outdir> <npairs> <seed>
-//                    <holdout_samples> <rectest_samples>
+//                    <holdout_samples> <rectest_samples> [<digest_holdout> <digest_rectest>]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +31,8 @@
 #include "test.h"
 #include "recommendation_tests.h"
 
+#include "pokec_io.h"  // pf_result_digest (the engine's parity-probe hash; plain C, no engine code)
+
 static uint32_t fbits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
 static void dump_list(FILE* f, const char* tag, int uid, int a, int b,
@@ -46,6 +48,7 @@ int main(int argc, char** argv) {
     int npairs = atoi(argv[3]);
     unsigned seed = (unsigned)atoi(argv[4]);
     int holdout_n = atoi(argv[5]), rectest_n = atoi(argv[6]);
+    const int digest_holdout = argc > 7 ? atoi(argv[7]) : 0, digest_rectest = argc > 8 ? atoi(argv[8]) : 0;
     if (chdir(work.c_str()) != 0) { perror("chdir"); return 1; }
 
     // ---- api_cli start-up (api_cli.cpp:93-167), minus vocab/lemmatiser ----
@@ -299,6 +302,87 @@ int main(int argc, char** argv) {
         f = open("rectests.txt");
         fprintf(f, "%.17g %.17g %.17g %.17g %.17g\n", m.graph_hit_rate, m.collab_hit_rate, m.interest_hit_rate,
                 m.avg_club_prec_at_k, m.avg_club_recall_at_k);
+        fclose(f);
+    }
+
+    // ---- A19 per-user result digests: the two drivers' loops replayed over the real
+    //      Recommender with the drivers' own construction and mutation sequence, each returned
+    //      list hashed (pf_result_digest).  The drivers print only averages; these pin every
+    //      list they produce under the edited adjacency (clubs included, whose precision the
+    //      averages always report as 0).
+    auto digest = [](const std::vector<std::pair<int, float>>& v) {
+        std::vector<int32_t> ids;
+        std::vector<float> sc;
+        for (auto& p : v) { ids.push_back(p.first); sc.push_back(p.second); }
+        return (unsigned long long)pf_result_digest(ids.data(), sc.data(), (int32_t)ids.size());
+    };
+    if (digest_holdout > 0) {  // test.cpp:20-89: one adj_mod, edits accumulate
+        std::vector<int> cand;
+        for (auto& kv : profiles) {
+            auto it = adj.find(kv.first);
+            if (it != adj.end() && (int)it->second.size() >= 20) cand.push_back(kv.first);
+        }
+        std::mt19937 rng(1234567);
+        std::shuffle(cand.begin(), cand.end(), rng);
+        std::unordered_map<int, std::vector<int>> adj_mod = adj;
+        Recommender r2(&profiles, &adj_mod);
+        r2.set_field_normalizers(rec.field_normalizers);
+        r2.set_column_normalizers(rec.column_normalizers);
+        r2.set_text_columns(cols);
+        r2.set_tfidf_index(rec.idf_per_col);
+        f = open("holdout_digest.txt");
+        int taken = 0;
+        for (int uid : cand) {
+            if (taken >= digest_holdout) break;
+            const std::vector<int>& fr = adj.at(uid);
+            const int F = (int)fr.size();
+            if (F < 2 || F / 5 <= 0) continue;
+            const int hold = F / 5;
+            std::vector<int> idx(F);
+            for (int i = 0; i < F; ++i) idx[i] = i;
+            std::shuffle(idx.begin(), idx.end(), rng);
+            std::unordered_set<int> held;
+            for (int i = 0; i < hold; ++i) held.insert(fr[idx[i]]);
+            std::vector<int> kept;
+            for (int x : fr) if (!held.count(x)) kept.push_back(x);
+            adj_mod[uid] = std::move(kept);
+            fprintf(f, "%d %016llx\n", uid, digest(r2.recommend_collaborative(uid, hold, 1000)));
+            ++taken;
+        }
+        fclose(f);
+    }
+    if (digest_rectest > 0) {  // recommendation_tests.cpp:79-156: a fresh adj_mod and Recommender per user
+        std::vector<int> all;
+        for (auto& kv : profiles) all.push_back(kv.first);
+        std::mt19937 rng(1234567);
+        std::shuffle(all.begin(), all.end(), rng);
+        f = open("rectests_digest.txt");
+        int taken = 0;
+        for (int uid : all) {
+            if (taken >= digest_rectest) break;
+            auto it = adj.find(uid);
+            if (it == adj.end() || it->second.size() < 4) continue;
+            const std::vector<int>& fr = it->second;
+            const int hold = std::max(1, (int)fr.size() / 4);
+            std::vector<int> idx(fr.size());
+            for (size_t i = 0; i < fr.size(); ++i) idx[i] = (int)i;
+            std::shuffle(idx.begin(), idx.end(), rng);
+            std::unordered_set<int> held;
+            for (int i = 0; i < hold; ++i) held.insert(fr[idx[i]]);
+            std::unordered_map<int, std::vector<int>> adj_mod = adj;
+            std::vector<int> kept;
+            for (int x : fr) if (!held.count(x)) kept.push_back(x);
+            adj_mod[uid] = kept;
+            Recommender r3(&profiles, &adj_mod);
+            r3.set_field_normalizers(rec.field_normalizers);
+            r3.set_column_normalizers(rec.column_normalizers);
+            r3.set_text_columns(cols);
+            r3.set_tfidf_index(rec.idf_per_col);
+            fprintf(f, "%d %016llx %016llx %016llx %016llx\n", uid, digest(r3.recommend_graph_registration(uid, 10, 5000)),
+                    digest(r3.recommend_collaborative(uid, 10, 5000)), digest(r3.recommend_by_interest(uid, 10, 5000)),
+                    digest(r3.recommend_clubs_collab(uid, 10, 5000)));
+            ++taken;
+        }
         fclose(f);
     }
     return 0;

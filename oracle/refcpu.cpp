@@ -6,6 +6,8 @@
 // arithmetic order (and therefore every float) and the timing profile match.
 #include "refcpu.h"
 
+#include "pokec_io.h"  // pf_result_digest (a plain hash; no engine code)
+
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -332,6 +334,17 @@ int emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc) 
     return n;
 }
 
+// pf_result_digest (pokec_io.h) of a ranked list
+uint64_t ranked_digest(const Ranked& r) {
+    std::vector<int32_t> ids;
+    std::vector<float> sc;
+    for (const auto& p : r) {
+        ids.push_back(p.first);
+        sc.push_back(p.second);
+    }
+    return pf_result_digest(ids.data(), sc.data(), (int32_t)ids.size());
+}
+
 }  // namespace
 
 extern "C" {
@@ -454,8 +467,13 @@ int ro_profile_order(const ro_ctx* h, int32_t* out, int32_t cap) {
     return i;
 }
 
-// test.cpp:13-105 — 20% of each eligible user's friends held out, cumulative adj edits
-int ro_holdout_friends(ro_ctx* h, int32_t sample, double* ratios, int32_t cap, int32_t* n) {
+}  // extern "C"
+
+namespace {
+
+// test.cpp:13-105 — 20% of each eligible user's friends held out, cumulative adj edits.
+// digest (may be null): per tested user the pf_result_digest of its collaborative list.
+int holdout_friends(ro_ctx* h, int32_t sample, double* ratios, uint64_t* digest, int32_t cap, int32_t* n) {
     std::vector<int> elig;
     for (const auto& kv : h->prof) {
         const std::vector<int>* fr = h->nbrs(kv.first);
@@ -485,7 +503,8 @@ int ro_holdout_friends(ro_ctx* h, int32_t sample, double* ratios, int32_t cap, i
         Ranked pred = h->rec_collab(u, hold, 1000);
         int hits = 0;
         for (size_t i = 0; i < pred.size() && (int)i < hold; ++i) hits += held.count(pred[i].first) ? 1 : 0;
-        if (taken < cap) ratios[taken] = (double)hits / (double)hold;
+        if (ratios && taken < cap) ratios[taken] = (double)hits / (double)hold;
+        if (digest && taken < cap) digest[taken] = ranked_digest(pred);
         ++taken;
     }
     h->adj = std::move(original);
@@ -493,9 +512,12 @@ int ro_holdout_friends(ro_ctx* h, int32_t sample, double* ratios, int32_t cap, i
     return PF_OK;
 }
 
-// recommendation_tests.cpp:68-169 — per-user fresh adjacency copy, four recommenders
-int ro_recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* metrics) {
+// recommendation_tests.cpp:68-169 — per-user fresh adjacency copy, four recommenders.
+// digest (may be null): per tested user i, digest[4i .. 4i+3] = graph, collab, interest, clubs.
+int recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* metrics, uint64_t* digest, int32_t cap,
+                         int32_t* n) {
     for (int k = 0; k < 5; ++k) metrics[k] = 0.0;
+    if (n) *n = 0;
     if (h->prof.empty() || h->adj.empty()) return PF_OK;
     std::vector<int> all;
     for (const auto& kv : h->prof) all.push_back(kv.first);
@@ -524,10 +546,18 @@ int ro_recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* met
             for (auto& p : r) if (held.count(p.first)) return true;
             return false;
         };
-        hg += any_hit(h->rec_graph(u, topk, 5000));
-        hc += any_hit(h->rec_collab(u, topk, 5000));
-        hi += any_hit(h->rec_graph(u, topk, 5000));
+        const Ranked rg = h->rec_graph(u, topk, 5000), rc = h->rec_collab(u, topk, 5000), ri = h->rec_graph(u, topk, 5000);
+        hg += any_hit(rg);
+        hc += any_hit(rc);
+        hi += any_hit(ri);
         Ranked cp = h->rec_clubs(u, topk, 5000);
+        if (digest && taken < cap) {
+            uint64_t* d = digest + 4 * (size_t)taken;
+            d[0] = ranked_digest(rg);
+            d[1] = ranked_digest(rc);
+            d[2] = ranked_digest(ri);
+            d[3] = ranked_digest(cp);
+        }
         std::unordered_set<int> own;
         for (uint32_t c : h->prof.at(u).clubs) own.insert((int)c);
         if (!own.empty()) {
@@ -549,7 +579,27 @@ int ro_recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* met
         metrics[3] = prec / club_users;
         metrics[4] = rec / club_users;
     }
+    if (n) *n = taken;
     return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ro_holdout_friends(ro_ctx* h, int32_t sample, double* ratios, int32_t cap, int32_t* n) {
+    return holdout_friends(h, sample, ratios, nullptr, cap, n);
+}
+int ro_holdout_friends_digest(ro_ctx* h, int32_t sample, uint64_t* digest, int32_t cap, int32_t* n) {
+    return holdout_friends(h, sample, nullptr, digest, cap, n);
+}
+int ro_recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* metrics) {
+    return recommendation_tests(h, sample, topk, metrics, nullptr, 0, nullptr);
+}
+int ro_recommendation_tests_digest(ro_ctx* h, int32_t sample, int32_t topk, uint64_t* digest, int32_t cap,
+                                   int32_t* n) {
+    double m[5];
+    return recommendation_tests(h, sample, topk, m, digest, cap, n);
 }
 
 }  // extern "C"

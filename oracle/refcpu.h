@@ -41,6 +41,11 @@ int   ro_profile_order(const ro_ctx* h, int32_t* out, int32_t cap);
 int   ro_holdout_friends(ro_ctx* h, int32_t sample, double* ratios, int32_t cap, int32_t* n);
 /* recommendation_tests.cpp:68-169; metrics[5] = graph, collab, interest hit rates, club P@k, R@k */
 int   ro_recommendation_tests(ro_ctx* h, int32_t sample, int32_t topk, double* metrics);
+/* the same drivers with per-user result digests (pokec_io.h pf_result_digest): holdout one per
+ * user (collaborative list), rectests four per user (graph, collab, interest, clubs) */
+int   ro_holdout_friends_digest(ro_ctx* h, int32_t sample, uint64_t* digest, int32_t cap, int32_t* n);
+int   ro_recommendation_tests_digest(ro_ctx* h, int32_t sample, int32_t topk, uint64_t* digest, int32_t cap,
+                                     int32_t* n);
 #ifdef __cplusplus
 }
 #endif

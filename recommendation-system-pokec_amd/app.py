@@ -176,12 +176,14 @@ def create_app(root, cli_cmd=None, load_users=None, ready_timeout=120.0, request
         except Exception as e:
             raise HTTPException(status_code=500, detail="invalid JSON from backend: " + str(e) + " output: " + out)
 
+    # plain `def` routes: FastAPI runs them in its threadpool, so a request blocked on the
+    # backend (cli.send waits up to request_timeout) never stalls the event loop (/health etc.)
     @app.get("/api/user/{uid}")
-    async def api_user(uid: int):
+    def api_user(uid: int):
         return JSONResponse(user_json(uid))
 
     def recommend(kind):
-        async def route(uid: int, topk: int = 20):
+        def route(uid: int, topk: int = 20):
             return user_json(uid).get("recommendations", {}).get(KINDS[kind], [])[:topk]
         route.__name__ = f"api_recommend_{kind}"
         return route

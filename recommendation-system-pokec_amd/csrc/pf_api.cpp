@@ -688,7 +688,7 @@ const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : g_open_
 int32_t pf_num_users(const pf_ctx* c) { return c ? c->hc.n : 0; }
 float pf_idf(const pf_ctx* c, int32_t col, int32_t tid) {
     if (!c || col < 0 || col >= c->hc.T) return NAN;
-    return c->hc.idf_of(col, tid);
+    return c->hc.idf_of_tid(col, tid);
 }
 
 int pf_fas_pairs(pf_ctx* c, const int32_t* a, const int32_t* b, int64_t n, float* out) {
@@ -806,10 +806,7 @@ int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, in
 
 int pf_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
     if (!c || (n > 0 && !nbrs)) return PF_EINVAL;
-    if (n < 0) c->hc.adj.erase(uid);
-    else c->hc.adj[uid].assign(nbrs, nbrs + n);
-    pf::jobs_note_edit(c, uid);  // the device graph sees the edit at the next job batch
-    return PF_OK;
+    return pf::jobs_set_adj(c, uid, nbrs, n);
 }
 
 int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {
@@ -890,30 +887,43 @@ int pf_jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) { return (c && o) ? pf::jobs
 int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     if (!c || nq < 0 || (nq && (!q || !out))) return PF_EINVAL;
     (void)hipSetDevice(c->device);
-    if (!c->use_post()) {  // K1: one pass over the shard's tiles and headers, whatever the query
-        const int64_t tiles = c->tile_end - c->tile_begin;
-        int64_t sb = 0;
-        for (int32_t t = c->tile_begin; t < c->tile_end; ++t) sb += (int64_t)c->hs.tile_steps[t] * pf::kTileSlots * 16;
-        const int64_t hdr = tiles * pf::kTileSlots * 48;
-        for (int i = 0; i < nq; ++i) out[i] = c->hc.idx_of(q[i]) < 0 ? 0 : sb + hdr;
+    // K1: one pass over the shard's tiles and headers, whatever the query
+    int64_t k1 = 0;
+    for (int32_t t = c->tile_begin; t < c->tile_end; ++t) k1 += (int64_t)c->hs.tile_steps[t] * pf::kTileSlots * 16;
+    k1 += (int64_t)(c->tile_end - c->tile_begin) * pf::kTileSlots * 48;
+    if (!c->use_post()) {
+        for (int i = 0; i < nq; ++i) out[i] = c->hc.idx_of(q[i]) < 0 ? 0 : k1;
         return PF_OK;
     }
+    // K5 serves the queries whose lists fit one workgroup's LDS; the others go to K1 in a launch
+    // of their own (scan_all's routing): the K5 launch holds only the fitting queries
+    std::vector<std::vector<uint8_t>> imgs((size_t)nq);
+    std::vector<int8_t> kind((size_t)nq, 0);  // 0 unknown uid, 1 K5, 2 K1
     par_jobs((size_t)nq, [&](size_t i) {
         const int32_t x = c->hc.idx_of(q[i]);
-        if (x < 0) { out[i] = 0; return; }
+        if (x < 0) return;
         std::vector<int32_t> ex;
         auto it = c->hc.adj.find(q[i]);
         if (it != c->hc.adj.end()) ex = it->second;
         ex.push_back(q[i]);
-        std::vector<uint8_t> img;
-        pf::build_query_post(c->hc, c->hp, x, ex, img);
-        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(img.data() + sizeof(pf::QConst));
-        const uint32_t wl = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
-        // workgroups that stage this query's image, as the launch of these nq queries runs
-        const int nwb = c->wb_end - c->wb_begin;
-        const int wgs = nq == 1 ? c->num_cus * pf::post_blocks_per_cu(wl)
-                                : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
-        out[i] = post_query_bytes(c, img, wgs);
+        pf::build_query_post(c->hc, c->hp, x, ex, imgs[i]);
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[i].data() + sizeof(pf::QConst));
+        kind[i] = pf::post_lds(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend)) <= kK5LdsCap ? 1 : 2;
+    }, 1);
+    int nfit = 0, max_tok = 0, max_lists = 0;
+    for (int i = 0; i < nq; ++i) {
+        if (kind[i] != 1) continue;
+        ++nfit;
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[i].data() + sizeof(pf::QConst));
+        max_tok = std::max(max_tok, h->n_tok);
+        max_lists = std::max(max_lists, h->n_tok + h->n_club + h->n_friend);
+    }
+    // workgroups that stage a query's image, as scan_post launches the fitting queries
+    const int nwb = c->wb_end - c->wb_begin;
+    const int wgs = nfit == 1 ? c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists))
+                              : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
+    par_jobs((size_t)nq, [&](size_t i) {
+        out[i] = kind[i] == 0 ? 0 : (kind[i] == 2 ? k1 : post_query_bytes(c, imgs[i], wgs));
     }, 1);
     return PF_OK;
 }

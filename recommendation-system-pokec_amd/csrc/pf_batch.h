@@ -75,6 +75,8 @@ struct HpLap {
 // Runs every job on the device job pipeline (pf_jobs_plan.cpp): one chain of device stages per
 // chunk of jobs.  0 = OK, else a PF_* status.
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs);
+// A batched driver call (its versioned edit set) starts or ends (pf_jobs_plan.cpp).
+void jobs_view_scope(pf_ctx* c);
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c);
 
 }  // namespace pf

@@ -83,19 +83,22 @@ struct JobsState {
     bool ok = false;
     std::string why;
     DevJobsStore js{};
-    DBuf d_tmpl, d_sigreg, d_comp_vals, d_comp_rows, d_age_vals, d_age_rows, d_idf_off, d_idf_tid, d_idf_val,
+    DBuf d_tmpl, d_sigreg, d_comp_vals, d_comp_rows, d_age_vals, d_age_rows,
         d_idf_doff, d_idf_dlen, d_idf_dense,
-        d_has_idf, d_slot_of, d_goff, d_glen, d_gnbr, d_guid, d_club_off, d_club_dense, d_club_id;
+        d_slot_of, d_goff, d_glen, d_gnbr, d_guid, d_club_off, d_club_dense, d_club_id;
     std::unordered_map<int32_t, int32_t> xnode;  // uid -> node for adj_list uids without a profile
     std::vector<int32_t> dense_node;             // uid -> node (-1 none) when the uids are dense
     std::vector<int32_t> g_uid, g_len;           // host mirrors (new uids from pf_set_adj append nodes)
     bool nodes_dirty = false;
     std::vector<uint8_t> img_lg;                 // per idx: query-table log2 (0 = outside the device limits)
     std::vector<int32_t> img_nset;               // per idx: clubs + friends words of the record
-    std::unordered_set<int32_t> edited;          // uids whose adj_list row pf_set_adj changed
+    std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
+    // open-time row of each edited uid (present, row): an edit back to it drops the override
+    std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;
     uint64_t edit_gen = 1, view_gen = 0;         // the uploaded edit table is current when equal
     const void* view_over = nullptr;             // the batched drivers' versioned edits last uploaded
     size_t view_over_n = 0;
+    uint64_t call_gen = 0, view_call = 0;        // batched driver calls (jobs_view_scope)
     DevView view{};
     DBuf d_view_node, d_view_ver, d_view_off, d_view_len, d_view_nbr;
     // per-chunk workspaces, double-buffered: chunk i + 1 is planned and launched while chunk i
@@ -254,7 +257,7 @@ inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 
 // the device job pipeline (pf_jobs.cpp)
 int jobs_open(pf_ctx* c);                            // after the tile store is on the device
-void jobs_note_edit(pf_ctx* c, int32_t uid);         // pf_set_adj changed uid's row
+int jobs_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n);  // pf_set_adj
 int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out);
 int jobs_stats_reset(pf_ctx* c, int enable);
 int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o);

@@ -959,14 +959,11 @@ struct Topk {
     explicit Topk(int k) : uid(std::max(k, 1)), score(std::max(k, 1)) {}
 };
 
-}  // namespace
-
-extern "C" {
-
-// run_friends_holdout_test (test.cpp:13-105); adj_mod accumulates over users
-int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, double* out_ratios, int32_t cap,
-                       int32_t* n_out) {
-    if (!ctx || !ds || !n_out || (cap > 0 && !out_ratios)) return PF_EINVAL;
+// run_friends_holdout_test (test.cpp:13-105); adj_mod accumulates over users.  digest (may be
+// null): per tested user the pf_result_digest of its collaborative list.
+int holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, double* out_ratios, uint64_t* digest,
+                    int32_t cap, int32_t* n_out) {
+    if (!ctx || !ds || !n_out || (cap > 0 && !out_ratios && !digest)) return PF_EINVAL;
     *n_out = 0;
     std::vector<int> candidates;
     for (auto& kv : ds->profiles) {
@@ -1006,6 +1003,7 @@ int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, d
         int hits = 0;
         for (int i = 0; i < t.n && i < hold_k; ++i)
             if (held.find(t.uid[i]) != held.end()) ++hits;
+        if (digest && taken < cap) digest[taken] = pf_result_digest(t.uid.data(), t.score.data(), t.n);
         results.push_back((double)hits / (double)hold_k);
         ++taken;
     }
@@ -1016,15 +1014,20 @@ int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, d
     }
     if (rc != PF_OK) return rc;
     const int32_t n = (int32_t)results.size();
-    for (int32_t i = 0; i < n && i < cap; ++i) out_ratios[i] = results[i];
+    for (int32_t i = 0; i < n && i < cap && out_ratios; ++i) out_ratios[i] = results[i];
     *n_out = n;
     return PF_OK;
 }
 
-// run_recommendation_tests_sample (recommendation_tests.cpp:68-169); a fresh adj_mod per user
-int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5) {
-    if (!ctx || !ds || !out5) return PF_EINVAL;
+// run_recommendation_tests_sample (recommendation_tests.cpp:68-169); a fresh adj_mod per user.
+// digest (may be null): per tested user i, digest[4i .. 4i+3] = pf_result_digest of its graph,
+// collaborative, interest and clubs lists; *n_out = users tested.
+int recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5,
+                         uint64_t* digest, int32_t cap, int32_t* n_out) {
+    double scratch[5];
+    if (!out5) out5 = scratch;
     for (int i = 0; i < 5; ++i) out5[i] = 0.0;
+    if (n_out) *n_out = 0;
     if (ds->profiles.empty() || ds->adj_list.empty()) return PF_OK;
     std::vector<int> all;
     for (auto& kv : ds->profiles) all.push_back(kv.first);
@@ -1060,6 +1063,13 @@ int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
         const int r2 = pf_set_adj(ctx, uid, friends.data(), (int32_t)friends.size());
         if (rc != PF_OK) return rc;
         if (r2 != PF_OK) return r2;
+        if (digest && taken < cap) {
+            uint64_t* d = digest + 4 * (size_t)taken;
+            d[0] = pf_result_digest(g.uid.data(), g.score.data(), g.n);
+            d[1] = pf_result_digest(c.uid.data(), c.score.data(), c.n);
+            d[2] = pf_result_digest(in.uid.data(), in.score.data(), in.n);
+            d[3] = pf_result_digest(cl.uid.data(), cl.score.data(), cl.n);
+        }
         auto any_held = [&](const Topk& t) {
             for (int i = 0; i < t.n; ++i)
                 if (held.find(t.uid[i]) != held.end()) return true;
@@ -1090,7 +1100,33 @@ int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
         out5[3] = club_prec / (double)club_users;
         out5[4] = club_rec / (double)club_users;
     }
+    if (n_out) *n_out = taken;
     return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, double* out_ratios, int32_t cap,
+                       int32_t* n_out) {
+    return holdout_friends(ctx, ds, sample_size, out_ratios, nullptr, cap, n_out);
+}
+
+int pf_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, double* out5) {
+    if (!ctx || !ds || !out5) return PF_EINVAL;
+    return recommendation_tests(ctx, ds, sample_size, topk, out5, nullptr, 0, nullptr);
+}
+
+int pf_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, uint64_t* out_digest,
+                              int32_t cap, int32_t* n_out) {
+    return holdout_friends(ctx, ds, sample_size, nullptr, out_digest, cap, n_out);
+}
+
+int pf_recommendation_tests_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                   uint64_t* out_digest, int32_t cap, int32_t* n_out) {
+    if (!ctx || !ds || !n_out || (cap > 0 && !out_digest)) return PF_EINVAL;
+    return recommendation_tests(ctx, ds, sample_size, topk, nullptr, out_digest, cap, n_out);
 }
 
 }  // extern "C"
@@ -1172,18 +1208,34 @@ std::vector<PlanEntry> plan_rec(const pf_dataset* ds, int32_t sample_size) {
     return plan;
 }
 
+// The versioned edit set of a driver call lives on the call's stack: the engine forgets it when
+// the call starts and ends (pf_jobs_plan.cpp jobs_view_scope).
+struct ViewScope {
+    pf_ctx* c;
+    explicit ViewScope(pf_ctx* x) : c(x) { pf::jobs_view_scope(c); }
+    ~ViewScope() { pf::jobs_view_scope(c); }
+};
+
 bool bad_shard(int32_t shard, int32_t nshards, int32_t batch) {
     return nshards < 1 || shard < 0 || shard >= nshards || batch < 1;
 }
 
-}  // namespace
+uint64_t job_digest(const pf::Job& J) {
+    std::vector<int32_t> ids;
+    std::vector<float> sc;
+    for (const auto& kv : J.out) {
+        ids.push_back(kv.first);
+        sc.push_back(kv.second);
+    }
+    return pf_result_digest(ids.data(), sc.data(), (int32_t)ids.size());
+}
 
-extern "C" {
-
-int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard, int32_t nshards,
-                            int32_t batch, double* out_ratio, int32_t cap, int32_t* n_plan) {
-    if (!ctx || !ds || !n_plan || (cap > 0 && !out_ratio) || bad_shard(shard, nshards, batch)) return PF_EINVAL;
+int eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard, int32_t nshards,
+                         int32_t batch, double* out_ratio, uint64_t* digest, int32_t cap, int32_t* n_plan) {
+    if (!ctx || !ds || !n_plan || (cap > 0 && !out_ratio && !digest) || bad_shard(shard, nshards, batch))
+        return PF_EINVAL;
     pf::HpLap hl;
+    ViewScope scope(ctx);
     const std::vector<PlanEntry> plan = plan_friends(ds, sample_size);
     hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
@@ -1215,18 +1267,21 @@ int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
             int hits = 0;
             for (int i = 0; i < (int)out.size() && i < pe.hold_k; ++i)
                 if (pe.held.find(out[i].first) != pe.held.end()) ++hits;
-            if (mine[x] < cap) out_ratio[mine[x]] = (double)hits / (double)pe.hold_k;
+            if (mine[x] >= cap) continue;
+            if (out_ratio) out_ratio[mine[x]] = (double)hits / (double)pe.hold_k;
+            if (digest) digest[mine[x]] = job_digest(jobs[x - b]);
         }
     }
     return PF_OK;
 }
 
-int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
-                                 int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, int32_t cap,
-                                 int32_t* n_plan) {
-    if (!ctx || !ds || !n_plan || (cap > 0 && (!out_hits || !out_club)) || bad_shard(shard, nshards, batch))
+int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
+                              int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, uint64_t* digest,
+                              int32_t cap, int32_t* n_plan) {
+    if (!ctx || !ds || !n_plan || (cap > 0 && !digest && (!out_hits || !out_club)) || bad_shard(shard, nshards, batch))
         return PF_EINVAL;
     pf::HpLap hl;
+    ViewScope scope(ctx);
     const std::vector<PlanEntry> plan = plan_rec(ds, sample_size);
     hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
@@ -1262,6 +1317,13 @@ int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t samp
                 return false;
             };
             const pf::Job& g = jobs[3 * (x - b)];
+            if (digest) {
+                uint64_t* d = digest + 4 * (size_t)i;
+                d[0] = d[2] = job_digest(g);  // recommend_by_interest = recommend_graph_registration
+                d[1] = job_digest(jobs[3 * (x - b) + 1]);
+                d[3] = job_digest(jobs[3 * (x - b) + 2]);
+            }
+            if (!out_hits) continue;
             out_hits[3 * (size_t)i] = (int8_t)any_held(g);
             out_hits[3 * (size_t)i + 1] = (int8_t)any_held(jobs[3 * (x - b) + 1]);
             out_hits[3 * (size_t)i + 2] = (int8_t)any_held(g);
@@ -1281,6 +1343,38 @@ int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t samp
         }
     }
     return PF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard, int32_t nshards,
+                            int32_t batch, double* out_ratio, int32_t cap, int32_t* n_plan) {
+    if (cap > 0 && !out_ratio) return PF_EINVAL;
+    return eval_holdout_friends(ctx, ds, sample_size, shard, nshards, batch, out_ratio, nullptr, cap, n_plan);
+}
+
+int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
+                                 int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, int32_t cap,
+                                 int32_t* n_plan) {
+    if (cap > 0 && (!out_hits || !out_club)) return PF_EINVAL;
+    return eval_recommendation_tests(ctx, ds, sample_size, topk, shard, nshards, batch, out_hits, out_club, nullptr,
+                                     cap, n_plan);
+}
+
+int pf_eval_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard,
+                                   int32_t nshards, int32_t batch, uint64_t* out_digest, int32_t cap, int32_t* n_plan) {
+    if (cap > 0 && !out_digest) return PF_EINVAL;
+    return eval_holdout_friends(ctx, ds, sample_size, shard, nshards, batch, nullptr, out_digest, cap, n_plan);
+}
+
+int pf_eval_recommendation_tests_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                        int32_t shard, int32_t nshards, int32_t batch, uint64_t* out_digest,
+                                        int32_t cap, int32_t* n_plan) {
+    if (cap > 0 && !out_digest) return PF_EINVAL;
+    return eval_recommendation_tests(ctx, ds, sample_size, topk, shard, nshards, batch, nullptr, nullptr, out_digest,
+                                     cap, n_plan);
 }
 
 }  // extern "C"

@@ -4,15 +4,19 @@
 //                          df = #profiles whose column map holds the tid (tf 0 included).
 //                          Every token's key (column << 32 | tid) is written by a row kernel,
 //                          radix-sorted (hipCUB onesweep) and run-length encoded: the runs are
-//                          the distinct (column, tid) pairs, their lengths the df.  Any tid
-//                          value works (no dense table is assumed).
+//                          the distinct (column, tid) pairs, their lengths the df.  Any int tid
+//                          works, negative ones included (the reference keys unordered_map<int,int>).
+//   tid ranks              the rest of the engine sees each tid as its rank among the column's
+//                          distinct tids (order kept; only equality and the idf lookup depend
+//                          on the id), so every device layout has dense ids.
 //   idf                    logf(1 + N / (1 + df)) in float32 on the host, over the distinct pairs
-//                          only (~10^5 logf calls): glibc's logf, so the bits are the reference's.
+//                          only (~10^5 logf calls): glibc's logf, so the bits are the reference's;
+//                          or the caller's map (set_tfidf_index), 1.0 for an absent tid.
 //   candidate norms        sqrt(sum (tf * idf)^2) per (user, column) row, in the row's tid order
-//                          (recommender.cpp:74-90), one thread per row; idf found by bisection
-//                          in the column's segment of the sorted (key, idf) table, 1.0 for a tid
-//                          without idf or a column without an idf map (A7).  FP64 with no FMA
-//                          contraction (-ffp-contract=off), so each step rounds as on the host.
+//                          (recommender.cpp:74-90), one thread per row, in the pass that finds
+//                          each token's rank by bisection in its column's segment of the sorted
+//                          key table; idf 1.0 for a column without an idf map (A7).  FP64 with
+//                          no FMA contraction (-ffp-contract=off): each step rounds as on the host.
 // The normaliser statistic (utils.cpp:155-240) stays on the host: its mt19937 pair sampler walks
 // the profiles map in hash order.
 #include <hip/hip_runtime.h>
@@ -35,8 +39,10 @@ constexpr int kIdfThreads = 256;
 constexpr int kKeyBits = 32 + 6;  // tid (any 32-bit value) + column (< kMaxCols = 48 < 64)
 static_assert(kMaxCols <= 64, "column fits 6 key bits");
 
-__device__ __forceinline__ uint64_t col_key(int col, int32_t tid) {
-    return ((uint64_t)(uint32_t)col << 32) | (uint32_t)tid;
+// (column, tid) key; the tid biased by 2^31 so the keys' unsigned order is the tids' signed order
+// (ranks then follow each row's ascending-tid order)
+__host__ __device__ __forceinline__ uint64_t col_key(int col, int32_t tid) {
+    return ((uint64_t)(uint32_t)col << 32) | ((uint32_t)tid ^ 0x80000000u);
 }
 
 // keys[k] = (column, tid) of token k; rows r = user * T + column
@@ -49,11 +55,12 @@ __global__ __launch_bounds__(kIdfThreads) void idf_keys_kernel(const int64_t* __
     }
 }
 
-// sqrt_nb[r] = sqrt(sum over the row's tokens, in order, of ((double)tf * idf)^2)
-// tab_key / tab_idf: sorted (column, tid) keys with their float idf; seg[c] .. seg[c + 1] is
-// column c's segment; has_idf[c] = 0: idf 1.0 for the whole column (raw counts, A7)
+// Per row r (= user * T + column), in the row's token order: the token's index x in the sorted
+// distinct (column, tid) table (bisection in the column's segment seg[c] .. seg[c + 1]); its
+// column rank x - seg[c] replaces the tid; and sqrt_nb[r] = sqrt(sum ((double)tf * idf)^2)
+// with idf = tab_idf[x] (has_idf[c] = 0: 1.0 for the whole column, raw counts, A7).
 __global__ __launch_bounds__(kIdfThreads) void idf_norms_kernel(const int64_t* __restrict__ tok_off,
-                                                                const int32_t* __restrict__ tid,
+                                                                int32_t* __restrict__ tid,
                                                                 const int32_t* __restrict__ tf, int64_t rows, int T,
                                                                 const uint64_t* __restrict__ tab_key,
                                                                 const float* __restrict__ tab_idf,
@@ -66,17 +73,15 @@ __global__ __launch_bounds__(kIdfThreads) void idf_norms_kernel(const int64_t* _
         const int64_t s0 = seg[col], s1 = seg[col + 1];
         double nb = 0.0;
         for (int64_t k = tok_off[r]; k < tok_off[r + 1]; ++k) {
-            double idf = 1.0;
-            if (hi) {
-                const uint64_t key = col_key(col, tid[k]);
-                int64_t lo = s0, up = s1;  // first entry >= key
-                while (lo < up) {
-                    const int64_t mid = (lo + up) >> 1;
-                    if (tab_key[mid] < key) lo = mid + 1;
-                    else up = mid;
-                }
-                if (lo < s1 && tab_key[lo] == key) idf = (double)tab_idf[lo];
+            const uint64_t key = col_key(col, tid[k]);
+            int64_t lo = s0, up = s1;  // first entry >= key (the key is always present)
+            while (lo < up) {
+                const int64_t mid = (lo + up) >> 1;
+                if (tab_key[mid] < key) lo = mid + 1;
+                else up = mid;
             }
+            tid[k] = (int32_t)(lo - s0);
+            const double idf = hi ? (double)tab_idf[lo] : 1.0;
             const double w = (double)tf[k] * idf;
             nb += w * w;
         }
@@ -103,7 +108,7 @@ int grid_for(int64_t rows) {
     do {                                                                      \
         hipError_t e_ = (x);                                                  \
         if (e_ != hipSuccess) {                                               \
-            err = std::string("F3 (df / norms on the device): ") + #x + ": " + \
+            err = std::string("F3 (df / ranks / norms on the device): ") + #x + ": " + \
                   hipGetErrorString(e_);                                      \
             (void)hipStreamDestroy(s);                                        \
             return e_ == hipErrorOutOfMemory ? PF_ENOMEM : PF_ENODEV;         \
@@ -129,10 +134,10 @@ int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err) {
         F3CHK(hipMemcpyAsync(d_tid.p, hc.tid.data(), (size_t)nt * 4, hipMemcpyHostToDevice, s));
         F3CHK(hipMemcpyAsync(d_tf.p, hc.tf.data(), (size_t)nt * 4, hipMemcpyHostToDevice, s));
     }
-    // ---- the (key, idf) table: df on the device (from profiles) or the caller's map (explicit)
+    // ---- the corpus's distinct (column, tid) keys (sorted) and their df, on the device
     std::vector<uint64_t> tab_key;
-    std::vector<float> tab_idf;
-    if (from_profiles && nt > 0) {
+    std::vector<int32_t> cnt;
+    if (nt > 0) {
         Dev<uint64_t> d_keys, d_sorted, d_uniq;
         Dev<int32_t> d_cnt, d_nruns;
         F3CHK(d_keys.alloc((size_t)nt));
@@ -155,31 +160,13 @@ int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err) {
         int32_t nruns = 0;
         F3CHK(hipMemcpyAsync(&nruns, d_nruns.p, 4, hipMemcpyDeviceToHost, s));
         F3CHK(hipStreamSynchronize(s));
-        std::vector<int32_t> cnt((size_t)nruns);
+        cnt.resize((size_t)nruns);
         tab_key.resize((size_t)nruns);
         F3CHK(hipMemcpyAsync(tab_key.data(), d_uniq.p, (size_t)nruns * 8, hipMemcpyDeviceToHost, s));
         F3CHK(hipMemcpyAsync(cnt.data(), d_cnt.p, (size_t)nruns * 4, hipMemcpyDeviceToHost, s));
         F3CHK(hipStreamSynchronize(s));
-        // recommender.cpp:56-64: idf = logf(1 + N / (1 + df)), float32, N = profiles loaded
-        const float N = (float)hc.n;
-        tab_idf.resize((size_t)nruns);
-        for (int32_t i = 0; i < nruns; ++i) {
-            tab_idf[i] = logf(1.0f + N / (1.0f + (float)cnt[i]));
-            hc.idf[(int)(tab_key[i] >> 32)][(int32_t)(uint32_t)tab_key[i]] = tab_idf[i];
-        }
-    } else {
-        for (int t = 0; t < T; ++t) {
-            if (!hc.has_idf[t]) continue;
-            std::vector<std::pair<uint32_t, float>> v;
-            for (const auto& e : hc.idf[t]) v.emplace_back((uint32_t)e.first, e.second);
-            std::sort(v.begin(), v.end());
-            for (const auto& e : v) {
-                tab_key.push_back(((uint64_t)(uint32_t)t << 32) | e.first);
-                tab_idf.push_back(e.second);
-            }
-        }
     }
-    // column segments of the sorted table
+    // column segments of the sorted table; rank = index - segment start
     std::vector<int64_t> seg((size_t)T + 1, 0);
     {
         size_t i = 0;
@@ -188,6 +175,32 @@ int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err) {
             while (i < tab_key.size() && (int)(tab_key[i] >> 32) == t) ++i;
         }
         seg[T] = (int64_t)tab_key.size();
+    }
+    // ---- idf per distinct key: recommender.cpp:56-64 logf(1 + N / (1 + df)) in float32 over
+    // the profiles (N = profiles loaded), or the caller's map (set_tfidf_index; absent -> 1.0,
+    // recommender.cpp:78); by rank on the host
+    std::vector<float> tab_idf(tab_key.size(), 1.0f);
+    const float N = (float)hc.n;
+    hc.tid_of_rank.assign(T, {});
+    for (int t = 0; t < T; ++t) {
+        const int64_t b = seg[t], e = seg[t + 1];
+        auto& ids = hc.tid_of_rank[t];
+        ids.resize((size_t)(e - b));
+        for (int64_t i = b; i < e; ++i) ids[i - b] = (int32_t)((uint32_t)tab_key[i] ^ 0x80000000u);
+        if (!hc.has_idf[t]) continue;
+        auto& ex = hc.idf_explicit[t];
+        for (int64_t i = b; i < e; ++i) {
+            if (from_profiles) {
+                tab_idf[i] = logf(1.0f + N / (1.0f + (float)cnt[i]));
+            } else {
+                auto it = ex.find(ids[i - b]);
+                if (it != ex.end()) {
+                    tab_idf[i] = it->second;
+                    ex.erase(it);  // what remains names ids the corpus does not hold
+                }
+            }
+        }
+        hc.idf[t].assign(tab_idf.begin() + b, tab_idf.begin() + e);
     }
     // ---- norms
     Dev<uint64_t> d_tk;
@@ -210,6 +223,7 @@ int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err) {
                        T, d_tk.p, d_ti.p, d_seg.p, d_has.p, d_nb.p);
     F3CHK(hipGetLastError());
     F3CHK(hipMemcpyAsync(hc.sqrt_nb.data(), d_nb.p, (size_t)rows * 8, hipMemcpyDeviceToHost, s));
+    if (nt > 0) F3CHK(hipMemcpyAsync(hc.tid.data(), d_tid.p, (size_t)nt * 4, hipMemcpyDeviceToHost, s));
     F3CHK(hipStreamSynchronize(s));
     (void)hipStreamDestroy(s);
     return PF_OK;

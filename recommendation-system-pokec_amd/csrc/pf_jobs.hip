@@ -333,15 +333,12 @@ __device__ __forceinline__ int find_val(const int32_t* vals, int n, int32_t v) {
     return (lo < n && vals[lo] == v) ? lo : -1;
 }
 
-// float idf of (column t, tid) as the reference reads it (recommender.cpp:78: absent -> 1.0):
-// one load from the column's dense table when it has one, else a bisection of its sorted tids
+// float idf of (column t, tid rank) as the reference reads it (recommender.cpp:78; a column
+// without an idf map: 1.0, the raw-count cosine A7)
 __device__ __forceinline__ double idf_of(const DevJobsStore& g, int t, int32_t tid) {
-    if (!g.has_idf[t]) return 1.0;
     const int64_t d = g.idf_dense_off[t];
-    if (d >= 0) return (tid >= 0 && tid < g.idf_dense_len[t]) ? (double)g.idf_dense[d + tid] : 1.0;
-    const int64_t b = g.idf_off[t];
-    const int i = find_val(g.idf_tid + b, (int)(g.idf_off[t + 1] - b), tid);
-    return i < 0 ? 1.0 : (double)g.idf_val[b + i];
+    if (d < 0) return 1.0;
+    return (tid >= 0 && tid < g.idf_dense_len[t]) ? (double)g.idf_dense[d + tid] : 1.0;
 }
 
 // One workgroup per image: QConst | table (ntab << lg, then 2^lge exclusions) | vals.

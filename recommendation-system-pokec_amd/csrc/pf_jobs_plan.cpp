@@ -112,29 +112,16 @@ int jobs_open(pf_ctx* c) {
     std::vector<double> comp_rows, age_rows;
     ratio_rows(hc.comp, PF_F_COMPLETION, comp_vals, comp_rows);
     ratio_rows(hc.age, PF_F_AGE, age_vals, age_rows);
-    // idf per column, sorted by tid (recommender.cpp:78: absent -> 1.0)
-    std::vector<int64_t> idf_off(T + 1, 0);
-    std::vector<int32_t> idf_tid;
-    std::vector<float> idf_val;
-    for (int t = 0; t < T; ++t) {
-        std::vector<std::pair<int32_t, float>> v(hc.idf[t].begin(), hc.idf[t].end());
-        std::sort(v.begin(), v.end());
-        for (auto& e : v) { idf_tid.push_back(e.first); idf_val.push_back(e.second); }
-        idf_off[t + 1] = (int64_t)idf_tid.size();
-    }
-    // dense idf tables where the column's tids are small and the total stays under 512 MB
+    // idf per column by tid rank (pf_store.h: the engine's token ids are column ranks), one dense
+    // table for every column with an idf map
     std::vector<int64_t> dense_off(T, -1);
     std::vector<int32_t> dense_len(T, 0);
     std::vector<float> dense;
     for (int t = 0; t < T; ++t) {
-        const int64_t b0 = idf_off[t], b1 = idf_off[t + 1];
-        if (!hc.has_idf[t] || b1 == b0 || idf_tid[b0] < 0 || idf_tid[b1 - 1] >= (1 << 24)) continue;
-        const int64_t len = (int64_t)idf_tid[b1 - 1] + 1;
-        if ((int64_t)dense.size() + len > (128ll << 20)) continue;
+        if (!hc.has_idf[t]) continue;
         dense_off[t] = (int64_t)dense.size();
-        dense_len[t] = (int32_t)len;
-        dense.resize(dense.size() + (size_t)len, 1.0f);
-        for (int64_t k = b0; k < b1; ++k) dense[dense_off[t] + idf_tid[k]] = idf_val[k];
+        dense_len[t] = (int32_t)hc.idf[t].size();
+        dense.insert(dense.end(), hc.idf[t].begin(), hc.idf[t].end());
     }
     if (dense.empty()) dense.push_back(1.0f);
     // graph: nodes 0..n-1 = profiles (idx), then adj_list uids without a profile
@@ -219,7 +206,6 @@ int jobs_open(pf_ctx* c) {
         J.img_nset[i] = (int32_t)((hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]));
     }, 4096);
     std::vector<int32_t> slot_of(hs.slot_of_idx.begin(), hs.slot_of_idx.end());
-    std::vector<uint8_t> has_idf(hc.has_idf.begin(), hc.has_idf.end());
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = up(c, J.d_tmpl, tv);
     if (e == hipSuccess) e = up(c, J.d_sigreg, sreg);
@@ -227,13 +213,9 @@ int jobs_open(pf_ctx* c) {
     if (e == hipSuccess) e = up(c, J.d_comp_rows, comp_rows);
     if (e == hipSuccess) e = up(c, J.d_age_vals, age_vals);
     if (e == hipSuccess) e = up(c, J.d_age_rows, age_rows);
-    if (e == hipSuccess) e = up(c, J.d_idf_off, idf_off);
-    if (e == hipSuccess) e = up(c, J.d_idf_tid, idf_tid);
-    if (e == hipSuccess) e = up(c, J.d_idf_val, idf_val);
     if (e == hipSuccess) e = up(c, J.d_idf_doff, dense_off);
     if (e == hipSuccess) e = up(c, J.d_idf_dlen, dense_len);
     if (e == hipSuccess) e = up(c, J.d_idf_dense, dense);
-    if (e == hipSuccess) e = up(c, J.d_has_idf, has_idf);
     if (e == hipSuccess) e = up(c, J.d_slot_of, slot_of);
     if (e == hipSuccess) e = up(c, J.d_goff, g_off);
     if (e == hipSuccess) e = up(c, J.d_glen, J.g_len);
@@ -253,13 +235,9 @@ int jobs_open(pf_ctx* c) {
     g.age_rows = J.d_age_rows.as<double>();
     g.n_comp = (int32_t)comp_vals.size();
     g.n_age = (int32_t)age_vals.size();
-    g.idf_off = J.d_idf_off.as<int64_t>();
-    g.idf_tid = J.d_idf_tid.as<int32_t>();
-    g.idf_val = J.d_idf_val.as<float>();
     g.idf_dense_off = J.d_idf_doff.as<int64_t>();
     g.idf_dense_len = J.d_idf_dlen.as<int32_t>();
     g.idf_dense = J.d_idf_dense.as<float>();
-    g.has_idf = J.d_has_idf.as<uint8_t>();
     g.slot_of = J.d_slot_of.as<int32_t>();
     g.g_off = J.d_goff.as<int64_t>();
     g.g_len = J.d_glen.as<int32_t>();
@@ -281,15 +259,45 @@ int jobs_open(pf_ctx* c) {
     return PF_OK;
 }
 
-void jobs_note_edit(pf_ctx* c, int32_t uid) {
+// A batched driver call starts or ends: its versioned edit set (a map on the driver's stack) is
+// new, so the next call uploads the overrides again even when a later map lands at the same
+// address with the same size.
+void jobs_view_scope(pf_ctx* c) {
+    ++c->jb.call_gen;
+    c->jb.view_over = nullptr;
+    c->jb.view_over_n = 0;
+}
+
+// pf_set_adj (test.cpp:73, recommendation_tests.cpp:111-114 mutate adj_list between queries):
+// the host row changes now, the device graph sees it through the override table at the next job
+// batch.  An edit that restores the open-time row drops the override, so a caller that edits and
+// restores rows (the drivers, the C++ facade) keeps the table small.
+int jobs_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
+    auto& adj = c->hc.adj;
     auto& J = c->jb;
-    if (!J.ok) return;
+    auto it = adj.find(uid);
+    if (J.ok && !J.orig.count(uid))
+        J.orig.emplace(uid, it == adj.end() ? std::make_pair(false, std::vector<int32_t>())
+                                            : std::make_pair(true, it->second));
+    if (n < 0) {
+        if (it != adj.end()) adj.erase(it);
+    } else {
+        adj[uid].assign(nbrs, nbrs + n);
+    }
+    if (!J.ok) return PF_OK;
     ensure_node(c, uid);
-    auto it = c->hc.adj.find(uid);
-    if (it != c->hc.adj.end())
-        for (int32_t x : it->second) ensure_node(c, x);
-    J.edited.insert(uid);
+    for (int32_t k = 0; k < n; ++k) ensure_node(c, nbrs[k]);
+    const auto& o = J.orig.at(uid);
+    const bool base = n < 0 ? !o.first : (o.first && (int64_t)o.second.size() == n &&
+                                          std::equal(o.second.begin(), o.second.end(), nbrs));
+    if (base) {
+        J.edited.erase(uid);
+        J.orig.erase(uid);
+    } else {
+        J.edited.insert(uid);
+    }
     ++J.edit_gen;
+    return PF_OK;
 }
 
 namespace {
@@ -324,7 +332,9 @@ int sync_nodes(pf_ctx* c) {
 int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>>* over) {
     auto& J = c->jb;
     const size_t on = over ? over->size() : 0;
-    if (J.view_gen == J.edit_gen && J.view_over == (const void*)over && J.view_over_n == on) return PF_OK;
+    if (J.view_gen == J.edit_gen && J.view_over == (const void*)over && J.view_over_n == on &&
+        J.view_call == J.call_gen)
+        return PF_OK;
     struct E { int32_t node, ver; int32_t len; const std::vector<int32_t>* row; };
     std::vector<E> es;
     for (int32_t u : J.edited) {
@@ -368,6 +378,7 @@ int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, st
     J.view_gen = J.edit_gen;
     J.view_over = over;
     J.view_over_n = on;
+    J.view_call = J.call_gen;
     return PF_OK;
 }
 
@@ -384,6 +395,8 @@ struct JP {
     int64_t cap = 0, seqlen = 0;
     int ht_lg = 0;
     int64_t elems = 0, ht_words = 0;
+    bool unmapped = false;       // a row names a uid without a graph node (never expected: open and
+                                 // pf_set_adj give every adjacency uid one); the call fails loudly
 };
 
 // Plan job i of `jobs` under its view: 1-hop work only.
@@ -406,6 +419,9 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
         p.F.reserve(ru->size());
         for (int32_t x : *ru) p.F.push_back(node_of(c, x));
     }
+    // K3's hash table keys nodes as node + 1 (0 = empty): a node of -1 would alias an empty slot
+    for (int32_t x : p.F) p.unmapped |= x < 0;
+    for (int32_t x : p.own) p.unmapped |= x < 0;
     const int64_t L = std::max<int32_t>(Jb.limit, 1);
     // |row(node)| under the view: the base CSR's length unless an edit or the view covers it
     const bool plain = c->jb.edited.empty() && !Jb.view.over && !Jb.view.own_row;
@@ -914,6 +930,8 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         par_jobs(lim - b, [&](size_t i) { if (P[b + i].u < 0 && P[b + i].kind < 0) plan_job(c, jobs[b + i], P[b + i], raw); },
                  256);
         hl.lap(kHpPrep);
+        for (size_t i = b; i < lim; ++i)
+            if (P[i].unmapped) return drain(c->fail(PF_EINTERNAL, "adjacency row names an unmapped uid"));
         size_t e = b;
         int64_t el = 0, ht = 0;
         while (e < lim) {

@@ -50,10 +50,18 @@ int32_t HostCorpus::idx_of(int32_t u) const {
     return (int32_t)(it - uid.begin());
 }
 
-float HostCorpus::idf_of(int t, int32_t k) const {
+float HostCorpus::idf_of(int t, int32_t rank) const {
     if (!has_idf[t]) return NAN;
-    auto it = idf[t].find(k);
-    return it == idf[t].end() ? 1.0f : it->second;
+    return (rank >= 0 && (size_t)rank < idf[t].size()) ? idf[t][rank] : 1.0f;
+}
+
+float HostCorpus::idf_of_tid(int t, int32_t k) const {
+    if (!has_idf[t]) return NAN;
+    const auto& v = tid_of_rank[t];
+    auto it = std::lower_bound(v.begin(), v.end(), k);
+    if (it != v.end() && *it == k) return idf_of(t, (int32_t)(it - v.begin()));
+    auto e = idf_explicit[t].find(k);  // recommender.cpp:78: absent -> 1.0
+    return e == idf_explicit[t].end() ? 1.0f : e->second;
 }
 
 int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err) {
@@ -114,16 +122,17 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
 
     // ---- IDF ------------------------------------------------------------
     hc.idf.assign(T, {});
+    hc.idf_explicit.assign(T, {});
     hc.has_idf.assign(T, 1);
     if (d->idf_mode == PF_IDF_EXPLICIT) {
         for (int t = 0; t < T; ++t) {
             hc.has_idf[t] = d->col_has_idf ? d->col_has_idf[t] : 1;
             if (!hc.has_idf[t] || !d->idf_off) continue;
-            for (int64_t k = d->idf_off[t]; k < d->idf_off[t + 1]; ++k) hc.idf[t][d->idf_tid[k]] = d->idf_val[k];
+            for (int64_t k = d->idf_off[t]; k < d->idf_off[t + 1]; ++k) hc.idf_explicit[t][d->idf_tid[k]] = d->idf_val[k];
         }
     }
-    // ---- df / idf (profiles mode) and the candidate norms sqrt(sum (tf*idf)^2) per (user,
-    // col) row: on the device (F3, pf_idf.hip)
+    // ---- token ids -> column ranks, df / idf (profiles mode) and the candidate norms
+    // sqrt(sum (tf*idf)^2) per (user, col) row: on the device (F3, pf_idf.hip)
     const int rc = device_idf_norms(hc, d->idf_mode != PF_IDF_EXPLICIT, err);
     if (rc != PF_OK) return rc;
     // ---- normalisers -----------------------------------------------------
@@ -158,18 +167,19 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
 int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     const int32_t n = hc.n, T = hc.T;
     // packed (fast) layout: one word per token and one tagged hash table, which needs
-    // tid < 2^18 - 1 (the all-ones token key is the padding word's), 0 <= tf < 256 and
-    // club / friend ids below 2^30 (bits 30-31 are the kind tags)
+    // column ranks < 2^18 - 1 (the all-ones token key is the padding word's), 0 <= tf < 256
+    // and club / friend ids below 2^30 (bits 30-31 are the kind tags)
     bool packed = true;
-    for (size_t k = 0; k < hc.tid.size() && packed; ++k)
-        if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] >= kTidMask || hc.tf[k] < 0 || hc.tf[k] > 255) packed = false;
+    for (int t = 0; t < T && packed; ++t) packed = (uint32_t)hc.n_ranks(t) < kTidMask;
+    for (size_t k = 0; k < hc.tf.size() && packed; ++k) packed = hc.tf[k] >= 0 && hc.tf[k] <= 255;
     for (size_t k = 0; k < hc.clubs.size() && packed; ++k) packed = hc.clubs[k] < kIdLimit;
     for (size_t k = 0; k < hc.friends.size() && packed; ++k) packed = hc.friends[k] < kIdLimit;
-    if (!packed)
-        for (size_t k = 0; k < hc.tf.size(); ++k) {
+    if (!packed) {
+        for (int t = 0; t < T; ++t)
+            if ((uint32_t)hc.n_ranks(t) > kWideTidMask + 1u) { err = "more than 2^26 distinct token ids in a column"; return PF_EUNSUPP; }
+        for (size_t k = 0; k < hc.tf.size(); ++k)
             if (hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23)) { err = "token count outside [-2^23, 2^23)"; return PF_EUNSUPP; }
-            if (hc.tid[k] < 0 || (uint32_t)hc.tid[k] > kWideTidMask) { err = "token id outside [0, 2^26)"; return PF_EUNSUPP; }
-        }
+    }
     hs.packed = packed;
     // record length in words: clubs, friends, tokens
     std::vector<uint32_t> len(n), ncols(n);
@@ -418,7 +428,7 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
         const size_t r = (size_t)i * T + t;
         if (hc.tok_off[r + 1] == hc.tok_off[r]) continue;
         for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
-            const double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;  // recommender.cpp:78
+            const double idf = hc.has_idf[t] ? (double)hc.idf_of(t, hc.tid[k]) : 1.0;  // recommender.cpp:78 (A7)
             QVal v;
             v.wq = (double)hc.tf[k] * idf;
             v.idf = idf;
@@ -527,10 +537,11 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
         if (hc.club_off[i + 1] - hc.club_off[i] > 0xFFFF || hc.friend_off[i + 1] - hc.friend_off[i] > 0xFFFF)
             return bail("more than 65535 clubs or friends");
     }
-    for (size_t k = 0; k < hc.tid.size(); ++k)
-        if (hc.tid[k] < 0 || hc.tid[k] >= (1 << 22) || hc.tf[k] < 0 || hc.tf[k] > 255)
-            return bail("token id / count outside the packed encoding");
-    // ---- token lists: (column, tid) ascending; entries idx << 8 | tf, tf > 0 only (a tf = 0
+    for (int t = 0; t < T; ++t)
+        if (hc.n_ranks(t) >= (1 << 22)) return bail("more than 2^22 distinct token ids in a column");
+    for (size_t k = 0; k < hc.tf.size(); ++k)
+        if (hc.tf[k] < 0 || hc.tf[k] > 255) return bail("token count outside the packed encoding");
+    // ---- token lists: (column, tid rank) ascending; entries idx << 8 | tf, tf > 0 only (a tf = 0
     // token adds +0 to a dot and never decides a hit: recommender.cpp:74-85)
     hp.tok_list.assign(T, {});
     std::vector<std::vector<uint32_t>> cnt(T);
@@ -538,11 +549,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
         std::vector<std::thread> ts;
         for (int t = 0; t < T; ++t)
             ts.emplace_back([&, t]() {
-                int32_t mx = -1;
-                for (int32_t i = 0; i < n; ++i)
-                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
-                        mx = std::max(mx, hc.tid[k]);
-                cnt[t].assign((size_t)mx + 1, 0u);
+                cnt[t].assign((size_t)hc.n_ranks(t), 0u);
                 for (int32_t i = 0; i < n; ++i)
                     for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
                         if (hc.tf[k] > 0) ++cnt[t][hc.tid[k]];

@@ -13,15 +13,24 @@ namespace pf {
 
 // Host copy of the corpus in candidate-index order (idx = rank of uid,
 // ascending, so idx order is the reference's tie-break order).
+//
+// Token ids: the caller's ids (any int, as the reference's unordered_map<int,int> keys) are
+// replaced at open by their rank among the column's distinct ids (F3 on the device,
+// pf_idf.hip).  Ranks keep the ids' order, and the path only compares ids for equality and
+// looks up their idf, so every score is unchanged; the device layouts then see dense ids.
 struct HostCorpus {
     int32_t n = 0, T = 0;
     std::vector<int32_t> uid, pub, comp, gen, age, reg;  // reg: 3 per user
     std::vector<int64_t> club_off, friend_off, tok_off;  // tok_off: n*T+1, rows sorted by tid
     std::vector<uint32_t> clubs, friends;
-    std::vector<int32_t> tid, tf;
+    std::vector<int32_t> tid, tf;                        // tid: the column rank of the token id
     std::vector<double> sqrt_nb;                         // per (user, col) row
     std::vector<uint8_t> has_idf;                        // per column
-    std::vector<std::unordered_map<int32_t, float>> idf; // per column
+    std::vector<std::vector<int32_t>> tid_of_rank;       // per column: the caller's id of each rank
+    std::vector<std::vector<float>> idf;                 // per column, by rank (empty: no idf map)
+    // PF_IDF_EXPLICIT: the caller's map per column; after open only its entries for ids the
+    // corpus does not hold remain (pf_idf reports them, no score reads them)
+    std::vector<std::unordered_map<int32_t, float>> idf_explicit;
     std::vector<uint8_t> npres;                          // 7 + T
     std::vector<float> nmean, nsd;
     std::unordered_map<int32_t, uint32_t> pub_code, gen_code;
@@ -29,7 +38,9 @@ struct HostCorpus {
     std::unordered_map<int32_t, std::vector<int32_t>> adj;
 
     int32_t idx_of(int32_t u) const;   // -1 when uid has no profile
-    float idf_of(int t, int32_t tid) const;  // 1.0 for absent token; NaN if no idf map
+    float idf_of(int t, int32_t rank) const;     // idf of a rank; NaN if the column has no idf map
+    float idf_of_tid(int t, int32_t tid) const;  // by the caller's id: 1.0 for an absent token
+    int32_t n_ranks(int t) const { return (int32_t)tid_of_rank[t].size(); }
 };
 
 struct HostStore {
@@ -72,9 +83,11 @@ struct HostPost {
 };
 
 int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err);
-// F3 on the device (pf_idf.hip): with from_profiles, df per (column, tid) and hc.idf (host
-// logf over the distinct pairs); then hc.sqrt_nb for every (user, column) row.  Needs the
-// current HIP device; hc.has_idf (and, explicit mode, hc.idf) set by the caller.
+// F3 on the device (pf_idf.hip): the distinct (column, tid) pairs of the corpus (radix sort +
+// run-length encoding); hc.tid rewritten as column ranks, hc.tid_of_rank; hc.idf by rank (with
+// from_profiles: logf over df on the host; else from hc.idf_explicit, 1.0 for absent ids); then
+// hc.sqrt_nb for every (user, column) row.  Needs the current HIP device; hc.has_idf (and,
+// explicit mode, hc.idf_explicit) set by the caller.
 int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err);
 // fills hp (hp.ok = false with hp.why when the corpus is outside the encoding)
 void build_postings(const HostCorpus& hc, HostPost& hp);

@@ -253,13 +253,9 @@ struct DevJobsStore {
     const int32_t* age_vals;
     const double* age_rows;
     int32_t n_comp, n_age;
-    const int64_t* idf_off;     // [T + 1] per column: sorted tids and their float idf
-    const int32_t* idf_tid;
-    const float* idf_val;
-    const int64_t* idf_dense_off;  // [T] a column's dense idf table (1.0 for absent tids), -1 = none
+    const int64_t* idf_dense_off;  // [T] a column's float idf by tid rank, -1 = no idf map (1.0)
     const int32_t* idf_dense_len;  // [T]
     const float* idf_dense;
-    const uint8_t* has_idf;     // [T]
     const int32_t* slot_of;     // [n] idx -> tile-store slot
     // graph
     const int64_t* g_off;       // [M] row start in g_nbr

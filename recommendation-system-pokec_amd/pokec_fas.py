@@ -32,7 +32,9 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
               "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests",
-              "pf_eval_holdout_friends", "pf_eval_recommendation_tests"]
+              "pf_eval_holdout_friends", "pf_eval_recommendation_tests", "pf_holdout_friends_digest",
+              "pf_recommendation_tests_digest", "pf_eval_holdout_friends_digest",
+              "pf_eval_recommendation_tests_digest"]
 PF_LOAD_REFERENCE_CAP = 100000
 
 
@@ -127,6 +129,10 @@ def lib():
         L.pf_recommendation_tests.argtypes = [V, V, I32, I32, V]
         L.pf_eval_holdout_friends.argtypes = [V, V, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_eval_recommendation_tests.argtypes = [V, V, I32, I32, I32, I32, I32, V, V, I32, ctypes.POINTER(I32)]
+        L.pf_holdout_friends_digest.argtypes = [V, V, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_recommendation_tests_digest.argtypes = [V, V, I32, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_eval_holdout_friends_digest.argtypes = [V, V, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_eval_recommendation_tests_digest.argtypes = [V, V, I32, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
         _lib = L
     return _lib
 
@@ -410,6 +416,43 @@ class Dataset:
                                                   hits.ctypes.data, club.ctypes.data, cap, ctypes.byref(n))
         eng._check(rc, "pf_eval_recommendation_tests")
         return hits[:n.value], club[:n.value]
+
+
+    # -- per-user result digests (pokec_io.h pf_result_digest): parity probes of the drivers
+    def holdout_friends_digest(self, eng, sample_size):
+        cap = max(int(sample_size), 1)
+        out = np.zeros(cap, np.uint64)
+        n = ctypes.c_int32()
+        rc = self._L.pf_holdout_friends_digest(eng.h, self.h, sample_size, out.ctypes.data, cap, ctypes.byref(n))
+        eng._check(rc, "pf_holdout_friends_digest")
+        return out[:n.value]
+
+    def recommendation_tests_digest(self, eng, sample_size, topk):
+        cap = max(int(sample_size), 1)
+        out = np.zeros((cap, 4), np.uint64)
+        n = ctypes.c_int32()
+        rc = self._L.pf_recommendation_tests_digest(eng.h, self.h, sample_size, topk, out.ctypes.data, cap,
+                                                    ctypes.byref(n))
+        eng._check(rc, "pf_recommendation_tests_digest")
+        return out[:n.value]
+
+    def eval_holdout_friends_digest(self, eng, sample_size, shard=0, nshards=1, batch=256):
+        cap = max(int(sample_size), 1)
+        out = np.zeros(cap, np.uint64)
+        n = ctypes.c_int32()
+        rc = self._L.pf_eval_holdout_friends_digest(eng.h, self.h, sample_size, shard, nshards, batch,
+                                                    out.ctypes.data, cap, ctypes.byref(n))
+        eng._check(rc, "pf_eval_holdout_friends_digest")
+        return out[:n.value]
+
+    def eval_recommendation_tests_digest(self, eng, sample_size, topk, shard=0, nshards=1, batch=128):
+        cap = max(int(sample_size), 1)
+        out = np.zeros((cap, 4), np.uint64)
+        n = ctypes.c_int32()
+        rc = self._L.pf_eval_recommendation_tests_digest(eng.h, self.h, sample_size, topk, shard, nshards, batch,
+                                                         out.ctypes.data, cap, ctypes.byref(n))
+        eng._check(rc, "pf_eval_recommendation_tests_digest")
+        return out[:n.value]
 
 
 def merge_shards(parts):

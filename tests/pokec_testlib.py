@@ -427,6 +427,15 @@ def golden_pairs_file(name, fn):
     return np.array(a, np.int32), np.array(b, np.int32), np.array(s, np.uint32)
 
 
+def golden_digests(name, fn):
+    """<fn>_digest.txt: per tested user `uid digest...` (hex), the reference's result digests
+    (oracle/ref_fixture.cpp replaying the drivers over the real Recommender)."""
+    rows = [ln.split() for ln in fixture_lines(name, fn)]
+    uids = np.array([int(r[0]) for r in rows], np.int32)
+    dig = np.array([[int(x, 16) for x in r[1:]] for r in rows], np.uint64)
+    return uids, (dig[:, 0] if dig.shape[1] == 1 else dig)
+
+
 def golden_idf(name):
     lines = fixture_lines(name, "idf.txt")
     N = int(lines[0].split()[1])
@@ -461,6 +470,8 @@ def oracle_lib():
     L.ro_profile_order.argtypes = [V, V, I32]
     L.ro_holdout_friends.argtypes = [V, I32, V, I32, ctypes.POINTER(I32)]
     L.ro_recommendation_tests.argtypes = [V, I32, I32, V]
+    L.ro_holdout_friends_digest.argtypes = [V, I32, V, I32, ctypes.POINTER(I32)]
+    L.ro_recommendation_tests_digest.argtypes = [V, I32, I32, V, I32, ctypes.POINTER(I32)]
     return L
 
 
@@ -550,6 +561,18 @@ class Oracle:
         m = np.zeros(5, np.float64)
         self.L.ro_recommendation_tests(self.h, sample, topk, m.ctypes.data)
         return m
+
+    def holdout_friends_digest(self, sample):
+        out = np.zeros(max(sample, 1), np.uint64)
+        n = ctypes.c_int32()
+        self.L.ro_holdout_friends_digest(self.h, sample, out.ctypes.data, len(out), ctypes.byref(n))
+        return out[:n.value]
+
+    def recommendation_tests_digest(self, sample, topk):
+        out = np.zeros((max(sample, 1), 4), np.uint64)
+        n = ctypes.c_int32()
+        self.L.ro_recommendation_tests_digest(self.h, sample, topk, out.ctypes.data, len(out), ctypes.byref(n))
+        return out[:n.value]
 
 
 # ------------------------------------------------------------------ product

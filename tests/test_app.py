@@ -86,6 +86,26 @@ def test_app_routes_against_protocol_stand_in(fake_cli, tmp_path):
     assert a.state.cli.p.poll() is not None  # shutdown ended the backend
 
 
+def test_app_slow_backend_does_not_block_other_routes(fake_cli, tmp_path):
+    """a request waiting on the backend runs in the threadpool, so /health answers
+    while it waits (an `async def` route calling the blocking send froze the event loop)."""
+    import threading
+    import time
+    from fastapi.testclient import TestClient
+    import app as appmod
+    a = appmod.create_app(str(tmp_path), cli_cmd=fake_cli, request_timeout=10.0)
+    with TestClient(a) as c:
+        done = {}
+        t = threading.Thread(target=lambda: done.setdefault("r", c.get("/api/user/77")))
+        t.start()
+        time.sleep(0.5)  # the backend now sleeps 3 s on USER 77
+        t0 = time.perf_counter()
+        assert c.get("/health").status_code == 200
+        assert time.perf_counter() - t0 < 1.5
+        t.join()
+        assert done["r"].status_code == 200 and done["r"].json() == {}
+
+
 def test_app_backend_without_ready_fails(fake_cli, tmp_path):
     import app as appmod
     with pytest.raises(RuntimeError, match="READY"):

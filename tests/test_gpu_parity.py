@@ -271,8 +271,9 @@ def test_hub_recommenders_vs_oracle(hubs):
     qc = q[:4]  # collaborative: 4242 (friends = the 60 hubs, 2-hop list > 10,000) and the edge users
     for lim, k in ((10000, 10), (5000, 20), (1000, 100)):
         ops = [(eng.recommend_clubs_collab, orc.clubs, q)]
-        if lim < 10000:  # the oracle's collaborative at 10,000 takes ~45 s on one core
-            ops.append((eng.recommend_collaborative, orc.collab, qc))
+        # the oracle's collaborative for the hub itself at 10,000 takes ~45 s on one core: the
+        # other users of qc run at 10,000 (the default limit, cfg 3), the hub below it
+        ops.append((eng.recommend_collaborative, orc.collab, qc if lim < 10000 else qc[1:]))
         for fn_e, fn_o, qq in ops:
             for u, g, r in zip(qq, fn_e(qq, k, lim), fn_o(qq, k, lim)):
                 assert list(g[0]) == list(r[0]), (fn_e.__name__, u, lim, k)
@@ -457,6 +458,41 @@ def test_cpp_facade_matches_reference():
     assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))
 
 
+def test_cpp_facade_replays_reference_drivers():
+    """B1 under the reference's own call sequences: tests/cpp/facade_check replays test.cpp:13-89
+    (a Recommender over one adj_mod, rows edited between calls) and recommendation_tests.cpp:
+    68-169 (a fresh adj_mod and Recommender per user) literally, with no sync call: the ratios
+    and averages equal the reference's holdout_friends.txt / rectests.txt, and every per-user
+    list (hashed) equals the reference's.  An adj_list edit alone (no sync) reaches the next call."""
+    import os
+    import subprocess
+    import tempfile
+    exe = os.path.join(tl.ROOT, "tests", "cpp", "facade_check")
+    m = tl.manifest()["corpora"]["A"]
+    q = [f"holdout {m['holdout']}", f"rectests {m['rectest']} 10", f"holdout {m['digest_holdout']}",
+         f"rectests {m['digest_rectest']} 10", "edit 1 2 3 4", "collab 1 10 5000"]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        r = subprocess.run([exe, d], input="\n".join(q) + "\n", capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.splitlines()
+    assert len(out) == 10, out
+    assert out[0].split()[2:] == tl.fixture_lines("A", "holdout_friends.txt")
+    assert [float(x) for x in out[2].split()[1:]] == [float(x) for x in tl.fixture_lines("A", "rectests.txt")[0].split()]
+    _, hold = tl.golden_digests("A", "holdout_digest.txt")
+    _, rect = tl.golden_digests("A", "rectests_digest.txt")
+    assert [int(x, 16) for x in out[5].split()[1:]] == [int(x) for x in hold]
+    assert [int(x, 16) for x in out[7].split()[1:]] == [int(x) for x in rect.reshape(-1)]
+    assert out[8] == "edit 1"
+    corpus = tl.golden_corpus("A")
+    eng = tl.engine(corpus)
+    eng.set_adj(1, [2, 3, 4])
+    (ids, sc), = eng.recommend_collaborative([1], 10, 5000)
+    p = out[9].split()
+    assert [int(x.split(":")[0]) for x in p[5:]] == list(ids)
+    assert [int(x.split(":")[1], 16) for x in p[5:]] == list(sc.view(np.uint32))
+
+
 def test_cpp_facade_explicit_idf_matches_reference():
     """The drop-in facade's set_tfidf_index (recommender.h:31) with the golden explicit map:
     FAS pairs, all-candidates and recommenders equal the reference's (A7 columns included)."""
@@ -540,15 +576,37 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
     eng2.set_shard(0, 1)
 
 
-def test_full_size_kernels_agree():
+@pytest.fixture(scope="module")
+def full():
+    """The BASELINE cfg 2 / cfg 3 corpus: 1,632,803 synthetic Pokec-shaped users (seed 1, the
+    bench's), its engine, and the oracle on the same arrays (built on first use, ~6 GB)."""
+    import time
+    t0 = time.time()
+    c = tl.synth.Corpus(n_users=1632803, seed=1, edge_cases=0, threads=16)
+    eng = tl.engine(c.desc_ptr())
+    print(f"[full] corpus + engine {time.time() - t0:.1f}s", flush=True)
+    box = {}
+
+    def oracle():
+        if "o" not in box:
+            t1 = time.time()
+            box["o"] = tl.Oracle(None, desc_ptr=c.desc_ptr())
+            print(f"[full] oracle maps {time.time() - t1:.1f}s", flush=True)
+        return box["o"]
+    yield c, eng, oracle
+    if "o" in box:
+        box["o"].close()
+    eng.close()
+
+
+def test_full_size_kernels_agree(full):
     """BASELINE cfg 2 size (1,632,803 users): the postings scan (K5), the record-stream scan
     (K1) and the pair kernel (K1') are three independent GPU paths; on the full corpus
     their top-k ids and FAS bits agree, equal the oracle's for two queries, the top-k is
     sorted by the reference comparator, and the 2-shard merge equals the single-shard result."""
     import torch
     pf = tl.product()
-    c = tl.synth.Corpus(n_users=1632803, seed=1, edge_cases=0, threads=16)
-    eng = tl.engine(c.desc_ptr())
+    c, eng, oracle = full
     rng = np.random.default_rng(21)
     q = [int(x) for x in rng.integers(1, 1632804, 6)]
     k = 10
@@ -568,11 +626,9 @@ def test_full_size_kernels_agree():
         assert np.array_equal(again.view(np.uint32), p[1].view(np.uint32)), u
     # the oracle on the full corpus (the reference algorithm, one core: ~5 s per query) for two
     # of the queries: the only oracle anchor at the BASELINE cfg-2 size
-    orc = tl.Oracle(None, desc_ptr=c.desc_ptr())
-    for u, p, r in zip(q[:2], post[:2], orc.interest(q[:2], k, tl.PF_MODE_ALL, 0)):
+    for u, p, r in zip(q[:2], post[:2], oracle().interest(q[:2], k, tl.PF_MODE_ALL, 0)):
         assert list(p[0]) == list(r[0]), u
         assert np.array_equal(p[1].view(np.uint32), r[1].view(np.uint32)), u
-    orc.close()
     s = torch.cuda.Stream()
     parts = torch.empty((2, len(q), k), dtype=torch.int64, device="cuda")
     for r in range(2):
@@ -587,13 +643,74 @@ def test_full_size_kernels_agree():
         uids, scores = pf.decode_keys(keys[i])
         assert list(uids) == list(post[i][0])
         assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32))
-    eng.close()
 
 
-def test_batched_sharded_holdout_drivers_equal_sequential():
-    """F1 / cfg 5: the batched drivers (adjacency views instead of edits, users batched and
-    sharded) reproduce the sequential drivers bit for bit on corpus A, for 1 and 3 shards and
-    batch sizes 1 and 64 (test.cpp's cumulative edits included)."""
+def _adjacency(ptr):
+    """(adj_uid, adj_off, adj_nbr) views of a pf_corpus_desc (no copy)."""
+    import ctypes
+    d = tl.PfCorpusDesc.from_address(ptr)
+    n = d.n_adj
+    arr = lambda p, t, k: np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(k,))
+    off = arr(d.adj_off, ctypes.c_int64, n + 1)
+    return arr(d.adj_uid, ctypes.c_int32, n), off, arr(d.adj_nbr, ctypes.c_int32, int(off[-1]))
+
+
+def _cfg3_users(ptr, n_random=5, seed=31, lo=2e4, hi=2.5e5):
+    """Users for BASELINE cfg 3 at its own configuration (recommend_collaborative(u, 10, 10000) on
+    the full corpus): n_random seeded users whose collaborative work |F| * min(sum of the friends'
+    row lengths, 10000) lies in [lo, hi) pair-FAS (a one-core oracle second or two each), and the
+    15 highest-degree uids (a row naming them has a 2-hop list far beyond 10,000)."""
+    uid, off, nbr = _adjacency(ptr)
+    deg = np.diff(off)
+    deg_of = np.zeros(int(max(uid.max(), nbr.max())) + 2, np.int64)
+    deg_of[uid] = deg
+    nbr_deg = deg_of[np.clip(nbr, 0, len(deg_of) - 1)] * (nbr >= 0)
+    seq = np.add.reduceat(nbr_deg, off[:-1].clip(max=len(nbr_deg) - 1)) * (deg > 0)
+    work = deg * np.minimum(seq, 10000)
+    rng = np.random.default_rng(seed)
+    ok = np.nonzero((work >= lo) & (work < hi) & (uid >= 1))[0]
+    pick = [int(uid[i]) for i in rng.choice(ok, n_random, replace=False)]
+    hubs = [int(x) for x in uid[np.argsort(-deg)[:15]]]
+    return pick, hubs
+
+
+def test_full_size_collaborative_at_limit_10000(full):
+    """BASELINE cfg 3 at its own configuration: recommend_collaborative(u, 10, 10000) on the
+    1,632,803-user corpus (the bench's seed), one batched call through the device job pipeline,
+    against the oracle: ids and score bits equal (recommender_graph.cpp:105-222).  One more user's
+    row is set (pf_set_adj, on the oracle too) to the 15 highest-degree users, so its 2-hop
+    candidate list is truncated at 10,000 (:114-125); its K3 list equals the oracle's too."""
+    c, eng, oracle = full
+    q, hubs = _cfg3_users(c.desc_ptr())
+    orc = oracle()
+    u_h = 777777
+    uid, off, nbr = _adjacency(c.desc_ptr())
+    i = int(np.nonzero(uid == u_h)[0][0])
+    row0 = nbr[off[i]:off[i + 1]].copy()
+    eng.set_adj(u_h, hubs)
+    orc.set_adj(u_h, hubs)
+    try:
+        assert len(orc.fof(u_h, 10000, tl.PF_FOF_COLLAB)) == 10000
+        assert list(eng.fof_candidates(u_h, 10000, tl.PF_FOF_COLLAB)) == list(orc.fof(u_h, 10000, tl.PF_FOF_COLLAB))
+        q = q + [u_h]
+        got = eng.recommend_collaborative(q, 10, 10000)
+        ref = orc.collab(q, 10, 10000)
+        for u, g, r in zip(q, got, ref):
+            assert len(g[0]) == len(r[0]) and len(g[0]) > 0, u
+            assert list(g[0]) == list(r[0]), u
+            assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
+    finally:
+        eng.set_adj(u_h, row0)
+        orc.set_adj(u_h, row0)
+
+
+def test_driver_digests_match_reference():
+    """Every per-user list of the two hold-out drivers equals the reference's (ids + score bits,
+    hashed per user; tests/golden/A/*_digest.txt from the real Recommender): the sequential
+    drivers (pf_set_adj edits) and the batched, sharded ones (adjacency views: test.cpp's
+    cumulative edit versions, recommendation_tests.cpp's own-row replacement), clubs included,
+    which the drivers' averages cannot see (recommend_clubs_collab never returns the user's own
+    clubs, so the club precision is always 0)."""
     import tempfile
     pf = tl.product()
     m = tl.manifest()["corpora"]["A"]
@@ -601,48 +718,45 @@ def test_batched_sharded_holdout_drivers_equal_sequential():
         tl.regen_reference_dir("A", d)
         ds = pf.Dataset(d)
     eng = pf.FasEngine(ds.desc_ptr(), 0)
-    seq = ds.holdout_friends(eng, m["holdout"])
-    seq5 = ds.recommendation_tests(eng, m["rectest"], 10)
-    # the reference's own outputs on this corpus (test.cpp:95 prints fixed << setprecision(6);
-    # recommendation_tests.cpp:150-168 the averaged ratios): the batched results are compared
-    # with them directly, not only through the sequential drivers
-    ref = tl.fixture_lines("A", "holdout_friends.txt")
-    ref5 = [float(x) for x in tl.fixture_lines("A", "rectests.txt")[0].split()]
-    for nshards, batch in ((1, 64), (3, 1), (3, 64)):
-        parts = [ds.eval_holdout_friends(eng, m["holdout"], s, nshards, batch) for s in range(nshards)]
-        got = pf.merge_shards(parts)
-        assert np.array_equal(got.view(np.uint64), seq.view(np.uint64)), (nshards, batch)
-        assert [f"{v:.6f}" for v in got] == ref, (nshards, batch)
-        hp = [ds.eval_recommendation_tests(eng, m["rectest"], 10, s, nshards, batch) for s in range(nshards)]
-        hits = pf.merge_shards([h for h, _ in hp])
-        club = pf.merge_shards([c for _, c in hp])
-        assert (hits >= 0).all()
-        assert list(pf.rec_tests_summary(hits, club)) == list(seq5), (nshards, batch)
-        assert list(pf.rec_tests_summary(hits, club)) == ref5, (nshards, batch)
-    # the engine's own adjacency is untouched: the sequential driver still matches
-    assert np.array_equal(ds.holdout_friends(eng, m["holdout"]).view(np.uint64), seq.view(np.uint64))
+    _, hold = tl.golden_digests("A", "holdout_digest.txt")
+    _, rect = tl.golden_digests("A", "rectests_digest.txt")
+    assert np.array_equal(ds.holdout_friends_digest(eng, m["digest_holdout"]), hold)
+    assert np.array_equal(ds.recommendation_tests_digest(eng, m["digest_rectest"], 10), rect)
+    for nshards, batch in ((1, 128), (3, 1), (3, 64), (2, 7)):
+        parts = [ds.eval_holdout_friends_digest(eng, m["digest_holdout"], s, nshards, batch) for s in range(nshards)]
+        assert np.array_equal(pf.merge_shards(parts), hold), (nshards, batch)
+        parts = [ds.eval_recommendation_tests_digest(eng, m["digest_rectest"], 10, s, nshards, batch)
+                 for s in range(nshards)]
+        assert np.array_equal(pf.merge_shards(parts), rect), (nshards, batch)
+    # the engine's adjacency is back to the loaded one: a second sequential run agrees
+    assert np.array_equal(ds.recommendation_tests_digest(eng, m["digest_rectest"], 10), rect)
+    eng.close()
 
 
-def test_device_df_idf_norms_and_wide_token_ids():
-    """F3 on the device (pf_idf.hip): df by radix sort + run-length encoding and the candidate
-    norms by per-row bisection, on a corpus whose token ids pass the packed limit (2^18 - 1),
-    so the record-stream scan and the pair kernel use the wide format, where a token's key is
-    tid | col << 26 (a tid in several of the query's columns is one entry per column).  idf
-    bits equal the oracle's float32 logf (recommender.cpp:43-66) for every (column, tid), and
-    the scores that depend on the norms and the wide tables are bit-exact.  Token ids outside
-    [0, 2^26) are refused at open (the reference's encoder writes vocabulary indices)."""
+def test_device_df_idf_norms_and_any_token_ids(wide_fmt):
+    """F3 on the device (pf_idf.hip) with token ids anywhere in int32 (the reference
+    keys unordered_map<int,int>, so negative ids and ids past 2^30 are legal): df by radix sort +
+    run-length encoding, every id replaced by its column rank, the candidate norms by per-row
+    bisection.  idf bits equal the oracle's float32 logf (recommender.cpp:43-66) for every
+    (column, tid), pairs, all-candidates (both scan kernels) and collaborative lists are
+    bit-exact.  wide: some counts above 255 as well, so the tile store takes its wide format
+    (two words per token) and the all-candidates scan its record-stream kernel."""
     base = tl.synth.Corpus(n_users=6000, seed=11, edge_cases=1)
     c = tl.corpus_from_desc(base.desc_ptr())
     t = c.tok_tid.astype(np.int64)
-    c.tok_tid[:] = ((t * 1048573) % 2**26).astype(np.int32)  # a bijection of [0, 2^26)
+    # an odd multiplier mod 2^32 is a bijection, so every row keeps distinct ids
+    c.tok_tid[:] = (((t * 2654435761 + 977) % 2**32) - 2**31).astype(np.int32)
+    assert (c.tok_tid < 0).any() and (c.tok_tid >= 2**30).any()
+    if wide_fmt:
+        c.tok_tf[::97] = 300
     eng = tl.engine(c.desc_ptr())
-    assert not eng.layout().packed_tokens
+    assert bool(eng.layout().packed_tokens) == (not wide_fmt)
+    assert eng.layout().scan_kernel == (1 if wide_fmt else 2)
     orc = tl.Oracle(c)
     T = c.n_cols
     rows = np.repeat(np.arange(len(c.tok_off) - 1) % T, np.diff(c.tok_off))
     pairs = np.unique(np.stack([rows, c.tok_tid.astype(np.int64)]), axis=1)
-    assert (pairs[1] > 2**25).any()
-    for col, tid in pairs.T[:: max(1, pairs.shape[1] // 3000)]:
+    for col, tid in list(pairs.T[:: max(1, pairs.shape[1] // 3000)]) + [(0, 2**31 - 1), (3, -(2**31))]:
         g, r = np.float32(eng.idf(int(col), int(tid))), np.float32(orc.idf(int(col), int(tid)))
         assert g.view(np.uint32) == r.view(np.uint32), (col, tid)
     rng = np.random.default_rng(3)
@@ -650,17 +764,18 @@ def test_device_df_idf_norms_and_wide_token_ids():
     b = rng.integers(1, 6001, 20000).astype(np.int32)
     assert np.array_equal(eng.fas_pairs(a, b).view(np.uint32), orc.fas_pairs(a, b).view(np.uint32))
     q = [1, 8, 77, 1500, 5999]
-    for u, gq, rq in zip(q, eng.recommend_interest_all(q, 10), orc.interest(q, 10, tl.PF_MODE_ALL, 0)):
-        assert list(gq[0]) == list(rq[0]), u
-        assert np.array_equal(gq[1].view(np.uint32), rq[1].view(np.uint32)), u
+    ref = orc.interest(q, 10, tl.PF_MODE_ALL, 0)
+    for kern in ((1,) if wide_fmt else (1, 2)):
+        eng.set_scan_kernel(kern)
+        for u, gq, rq in zip(q, eng.recommend_interest_all(q, 10), ref):
+            assert list(gq[0]) == list(rq[0]), (kern, u)
+            assert np.array_equal(gq[1].view(np.uint32), rq[1].view(np.uint32)), (kern, u)
+    eng.set_scan_kernel(0)
     for u, gq, rq in zip(q, eng.recommend_collaborative(q, 10, 1000), orc.collab(q, 10, 1000)):
         assert list(gq[0]) == list(rq[0]), u
         assert np.array_equal(gq[1].view(np.uint32), rq[1].view(np.uint32)), u
     eng.close()
     orc.close()
-    c.tok_tid[int(np.nonzero(c.tok_tid != 0)[0][0])] = -5
-    with pytest.raises(tl.product().FasError, match="outside"):
-        tl.engine(c.desc_ptr())
 
 
 def test_pipelined_job_chunks_equal_small_calls(big):

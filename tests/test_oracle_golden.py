@@ -95,6 +95,22 @@ def test_oracle_holdout_drivers():
     assert list(got) == ref
 
 
+def test_oracle_driver_digests():
+    """Every list the two drivers produce (test.cpp:49-89 collaborative under the cumulative
+    edits; recommendation_tests.cpp:93-156 graph / collaborative / interest / clubs under each
+    user's own edited row), hashed per user, equals the reference's (ref_fixture.cpp replays the
+    drivers over the real Recommender)."""
+    corpus = tl.golden_corpus("A")
+    m = tl.manifest()["corpora"]["A"]
+    orc = tl.Oracle(corpus)
+    uids, ref = tl.golden_digests("A", "holdout_digest.txt")
+    assert len(uids) == m["digest_holdout"]
+    assert np.array_equal(orc.holdout_friends_digest(m["digest_holdout"]), ref)
+    uids, ref = tl.golden_digests("A", "rectests_digest.txt")
+    assert len(uids) == m["digest_rectest"]
+    assert np.array_equal(orc.recommendation_tests_digest(m["digest_rectest"], 10), ref)
+
+
 @pytest.mark.parametrize("name", ["A", "B"])
 def test_oracle_explicit_idf(name):
     """A7 and set_tfidf_index: with an explicit idf map that omits columns (raw-count cosine,

@@ -17,6 +17,7 @@
 
 #include "pf_batch.h"
 #include "pf_ctx.h"
+#include "pf_debug.h"
 #include "pf_kernels.h"
 #include "pf_store.h"
 #include "pokec_fas.h"
@@ -53,13 +54,10 @@ struct Images {
 
 constexpr uint32_t kStageLimit = 48 * 1024;   // keys+vals above this are probed in global memory
 
-// PF_STAGE_LIMIT (bytes) lowers the LDS staging limit; tests use it to force the
+// PF_DEBUG stage_limit (bytes) lowers the LDS staging limit; tests use it to force the
 // global-memory table variant on small corpora.
 uint32_t stage_limit() {
-    static const uint32_t lim = [] {
-        const char* e = getenv("PF_STAGE_LIMIT");
-        return e ? (uint32_t)strtoul(e, nullptr, 10) : kStageLimit;
-    }();
+    static const uint32_t lim = (uint32_t)pf::debug_long("stage_limit", kStageLimit);
     return lim;
 }
 constexpr uint32_t kBlockThreads = 256;
@@ -247,38 +245,21 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
     oc[i] = n;
 }
 
-// Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
-// launch the caller passes timed = false, or that sampling skips, records nothing and clears
-// last_ev0/last_ev1, so pf_last_scan_ms never reports another launch's time.
+// K5 mode word: bit 0 dynamic block hand-out (each workgroup's first block, then the next
+// unclaimed one), for one-query launches only.  r2fb A/B: 205.3 / 205.6 us vs 206.9 / 206.9 us
+// static per cfg-2 launch; batches (one block per workgroup in L2-sharing order) stay static
+// (cfg 4 9.83e9 dynamic vs 9.88e9 static).
+uint32_t post_mode(int nq) { return nq == 1 ? 1u : 0u; }
+
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
-// candidates/s.  PF_K5_BATCH_SPAN overrides it (profiling only).
-// K5 block hand-out of a one-query launch (profiling knob PF_K5_DYN): 1 dynamic (each
-// workgroup's first block, then the next unclaimed one; the default), 0 static (workgroup w
-// takes blocks w, w + grid, ...).  r2fb A/B: 205.3 / 205.6 us vs 206.9 / 206.9 us per cfg-2
-// launch; batches (one block per workgroup in L2-sharing order) stay static (cfg 4 9.83e9
-// dynamic vs 9.88e9 static).
-int post_dynamic() {
-    static const int v = [] {
-        const char* e = getenv("PF_K5_DYN");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
+// candidates/s.
+constexpr int kBatchBlocksPerWg = 4;
 
-// K5 mode word: bit 0 dynamic hand-out (one-query launches only)
-uint32_t post_mode(int nq) { return nq == 1 && post_dynamic() ? 1u : 0u; }
-
-int batch_blocks_per_wg() {
-    static const int v = [] {
-        const char* e = getenv("PF_K5_BATCH_SPAN");
-        const int x = e ? atoi(e) : 0;
-        return x > 0 ? x : 4;
-    }();
-    return v;
-}
-
+// Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
+// launch the caller passes timed = false, or that sampling skips, records nothing and clears
+// last_ev0/last_ev1, so pf_last_scan_ms never reports another launch's time.
 int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
     e0 = c->ev0;
     e1 = c->ev1;
@@ -337,7 +318,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // query looping over the range instead, 256 queries run at once and L2 hits collapse
     // (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
     const int blocks = nq == 1 ? std::max(1, std::min(nwb, c->num_cus * per_cu))
-                               : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
+                               : std::max(1, (nwb + kBatchBlocksPerWg - 1) / kBatchBlocksPerWg);
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
@@ -356,21 +337,14 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     hipEvent_t e0, e1;
     int rc = scan_events(c, timed, e0, e1);
     if (rc != PF_OK) return rc;
-    // timed: the events ride in the kernel's dispatch (its own start / end), or, with the
-    // A/B knob PF_EV_MARKERS=1, are two marker packets recorded around it
-    static const bool markers = [] {
-        const char* v = getenv("PF_EV_MARKERS");
-        return v && atoi(v);
-    }();
-    if (timed && markers) HIPCHK(c, hipEventRecord(e0, s));
-    const bool in_dispatch = timed && !markers;
+    // timed: the events ride in the kernel's dispatch (its own start / end; r2ff: 1.8 us less
+    // per launch than two marker packets around it)
     HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
                               nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
                               reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
                               reinterpret_cast<const int32_t*>(base + offs_b), post_mode(nq),
-                              in_dispatch ? e0 : nullptr, in_dispatch ? e1 : nullptr, s));
+                              timed ? e0 : nullptr, timed ? e1 : nullptr, s));
     if (timed) {
-        if (markers) HIPCHK(c, hipEventRecord(e1, s));
         c->last_ev0 = e0;
         c->last_ev1 = e1;
     }
@@ -510,8 +484,7 @@ namespace pf {
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c) { return c->hc.adj; }
 
 HostProf::HostProf() {
-    const char* e = getenv("PF_HOST_PROF");
-    on = e && *e && *e != '0';
+    on = debug_long("host_prof", 0) != 0;
     for (auto& x : ns) x = 0;
 }
 HostProf::~HostProf() {
@@ -573,9 +546,9 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     stage("tile store");
     pf::build_postings(c->hc, c->hp);  // hp.ok = false: the stream scan serves every query
     stage("postings store");
-    // PF_SCAN=stream|postings sets the context's initial scan kernel (tests force variants
+    // PF_DEBUG scan=stream|postings sets the context's initial scan kernel (tests force variants
     // per process with it); pf_set_scan_kernel changes it later
-    if (const char* sk = getenv("PF_SCAN")) {
+    if (const char* sk = pf::debug_str("scan")) {
         if (!strcmp(sk, "stream")) c->scan_kind = PF_SCAN_STREAM;
         else if (!strcmp(sk, "postings") && c->hp.ok) c->scan_kind = PF_SCAN_POSTINGS;
     }
@@ -652,10 +625,9 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         c->ps.n = c->hc.n;
         // block size: the LDS capacity.  Sizing blocks to fill whole waves of resident
         // workgroups (798 at 1.6M) measured slower (258 vs 244 us): per-block costs dominate
-        // the half-empty last wave.  PF_K5_BLOCK overrides it (tests, experiments).
+        // the half-empty last wave.  PF_DEBUG k5_block overrides it (tests).
         {
-            int64_t b = pf::kBlockCands;
-            if (const char* e = getenv("PF_K5_BLOCK")) b = strtol(e, nullptr, 10);
+            const int64_t b = pf::debug_long("k5_block", pf::kBlockCands);
             c->ps.bsize = (int32_t)std::max<int64_t>(64, std::min<int64_t>(pf::kBlockCands, b));
         }
         c->ps.n_blocks = (c->hc.n + c->ps.bsize - 1) / c->ps.bsize;
@@ -921,7 +893,7 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     // workgroups that stage a query's image, as scan_post launches the fitting queries
     const int nwb = c->wb_end - c->wb_begin;
     const int wgs = nfit == 1 ? c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists))
-                              : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
+                              : (nwb + kBatchBlocksPerWg - 1) / kBatchBlocksPerWg;
     par_jobs((size_t)nq, [&](size_t i) {
         out[i] = kind[i] == 0 ? 0 : (kind[i] == 2 ? k1 : post_query_bytes(c, imgs[i], wgs));
     }, 1);

@@ -115,7 +115,7 @@ struct JobsState {
         size_t o_cnt = 0, o_keys = 0, o_fail = 0;
         int ktop = 1;
     } ws[2];
-    DBuf d_acc, d_touched;
+    DBuf d_acc;
     int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
     bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)
@@ -236,15 +236,8 @@ inline void par_jobs(size_t n, F f, size_t grain = 4) {
 // A timing event of the profiling pools (pf_profile_*, the job statistics).  Created without
 // the system-scope fence (hipEventDisableSystemFence): every read of these events follows a
 // stream or device synchronisation, and the fence's L2 write-back and invalidation would
-// otherwise run between the timed kernels and perturb them.  PF_EV_FENCE=1 restores the
-// default flags (A/B knob).
-inline hipError_t timing_event(hipEvent_t* e) {
-    static const unsigned flags = [] {
-        const char* v = getenv("PF_EV_FENCE");
-        return (v && atoi(v)) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
-    }();
-    return hipEventCreateWithFlags(e, flags);
-}
+// otherwise run between the timed kernels and perturb them (r2fe: 1.6 us of kernel time).
+inline hipError_t timing_event(hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableSystemFence); }
 
 template <class T>
 inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {

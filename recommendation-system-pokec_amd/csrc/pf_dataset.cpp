@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "pf_batch.h"
+#include "pf_debug.h"
 #include "pokec_io.h"
 
 namespace pf {
@@ -177,10 +178,8 @@ void split_lines(const std::string& buf, size_t from, int64_t max_lines, std::ve
 }
 
 int ingest_threads() {
-    if (const char* e = getenv("PF_LOAD_THREADS")) {
-        const int v = atoi(e);
-        if (v > 0) return std::min(v, 256);
-    }
+    const long v = pf::debug_long("load_threads", 0);  // PF_DEBUG load_threads (tests, tools)
+    if (v > 0) return (int)std::min<long>(v, 256);
     const unsigned hc = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
 }
@@ -670,9 +669,9 @@ int pf_dataset_load_cached(const char* root, int64_t max_lines, const char* cach
     auto bail = [&](const std::string& m) { delete d; return fail(m); };
     if (!load_columns(r + "/config/text_columns.txt", d->cols)) return bail("cannot read config/text_columns.txt");
     if (d->cols.size() > PF_MAX_COLS) return bail("more than PF_MAX_COLS text columns");
-    const bool prof = getenv("PF_HOST_PROF") && atoi(getenv("PF_HOST_PROF")) > 0;
+    const bool prof = pf::debug_long("host_prof", 0) > 0;
     auto t0 = std::chrono::steady_clock::now();
-    auto stage = [&](const char* what) {  // PF_HOST_PROF=1: loader stage clocks on stderr
+    auto stage = [&](const char* what) {  // PF_DEBUG host_prof=1: loader stage clocks on stderr
         const auto t1 = std::chrono::steady_clock::now();
         if (prof) fprintf(stderr, "[pf_dataset_load] %s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
         t0 = t1;

@@ -1,0 +1,48 @@
+// pf_debug.h — the engine's only environment switch, PF_DEBUG: comma-separated name=value
+// settings that force code paths the tests cover, or turn on profiling output.  Unset, the
+// engine runs its fixed configuration (the measured winners); nothing on the
+// product path reads any other variable.
+//
+//   scan=stream|postings  initial all-candidates scan kernel of every context (default: postings
+//                         when the corpus fits its encoding; tests: test_kernel_variants)
+//   stage_limit=BYTES     query tables above this are probed in global memory (default 49152)
+//   tile_steps=N          tile-store chunk limit in 16-B steps, splits records over lanes (48)
+//   k5_block=N            postings-scan block size in candidates (1024)
+//   load_threads=N        loader threads (default: min(16, hardware threads))
+//   host_prof=1           host stage clocks on stderr (pf_open, the loaders, the job pipeline)
+//
+// e.g. PF_DEBUG=scan=stream,stage_limit=0
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace pf {
+
+// The value of PF_DEBUG's `name` setting, or nullptr when absent (read at each call: the
+// engine calls it at open / load time only).
+inline const char* debug_str(const char* name) {
+    const char* e = std::getenv("PF_DEBUG");
+    const std::string all(e ? e : "");
+    static thread_local std::string val;
+    const size_t n = std::strlen(name);
+    size_t p = 0;
+    while (p < all.size()) {
+        size_t q = all.find(',', p);
+        if (q == std::string::npos) q = all.size();
+        if (q - p > n && all.compare(p, n, name) == 0 && all[p + n] == '=') {
+            val.assign(all, p + n + 1, q - p - n - 1);
+            return val.c_str();
+        }
+        p = q + 1;
+    }
+    return nullptr;
+}
+
+// PF_DEBUG's `name` as an integer, dflt when absent.
+inline long debug_long(const char* name, long dflt) {
+    const char* v = debug_str(name);
+    return v ? std::strtol(v, nullptr, 0) : dflt;
+}
+
+}  // namespace pf

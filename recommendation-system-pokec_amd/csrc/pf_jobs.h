@@ -26,7 +26,7 @@ uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed);
 hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
                          const float* pout, const int32_t* cand_slot, float* score, hipStream_t s);
 hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
-                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, int32_t* touched,
+                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc,
                         float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);
 hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
                              unsigned long long* acc, hipStream_t s);

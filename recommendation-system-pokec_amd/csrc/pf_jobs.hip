@@ -555,9 +555,6 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
 // contributions all go to one lane and keep their sequence order, so each club's double sum
 // is the reference's.  acc[d] == 0.0 marks an untouched club (every contribution is > 0).
 constexpr int kClubBuf = 512;  // contributions per round (LDS: 2 x 12 B each)
-#ifndef PF_CLUBS_SERIAL
-#define PF_CLUBS_SERIAL 0  // 1: the former one-contribution-at-a-time walk (A/B)
-#endif
 
 __device__ __forceinline__ int wave_excl_prefix(int x, int lane, int& total) {
     int v = x;
@@ -573,14 +570,12 @@ __device__ __forceinline__ int wave_excl_prefix(int x, int lane, int& total) {
 __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
                                                    const int32_t* __restrict__ jix, const int32_t* __restrict__ pool,
                                                    const int64_t* __restrict__ pool64, const float* __restrict__ pout,
-                                                   double* __restrict__ acc_all, int32_t* __restrict__ touched_all,
-                                                   float* __restrict__ score, int32_t* __restrict__ ids,
+                                                   double* __restrict__ acc_all, float* __restrict__ score, int32_t* __restrict__ ids,
                                                    int32_t* __restrict__ ncand, int64_t acc_stride) {
     const int slot = blockIdx.x;
     const DevJob J = jobs[jix[slot]];
     const int lane = threadIdx.x;
     double* acc = acc_all + (size_t)slot * acc_stride;     // dense club scores (zero between jobs)
-    int32_t* touched = touched_all + (size_t)slot * acc_stride;  // 0 / 1 per dense club
     __shared__ int s_n;
     if (lane == 0) s_n = 0;
     __syncthreads();
@@ -596,59 +591,6 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         return false;
     };
     int32_t* list = ids + J.out_off;  // dense indices of the touched clubs
-#if PF_CLUBS_SERIAL
-    auto add = [&](int32_t d, double v) {
-        if ((d & 63) != lane) return;
-        if (!touched[d]) {
-            touched[d] = 1;
-            list[atomicAdd(&s_n, 1)] = d;
-        }
-        acc[d] += v;
-    };
-    for (int j = 0; j < J.nf; ++j) {
-        const int r = fpos[j];
-        if (r < 0) continue;
-        const double w = (double)sim[r];
-        if (w <= 0.0) continue;
-        const int32_t f = frow[j];
-        for (int64_t k = g.club_off[f]; k < g.club_off[f + 1]; ++k) {
-            const int32_t d = g.club_dense[k];
-            if (!own_club(d)) add(d, w);
-        }
-    }
-    for (int j = 0; j < J.nf; ++j) {
-        const int r = fpos[j];
-        if (r < 0) continue;
-        const int32_t f = frow[j];
-        int32_t len;
-        const int32_t* row = row_of(g, vw, J, pool, f, len);
-        if (len < 0) continue;
-        const double w = (double)sim[r];
-        if (w <= 0.0) continue;
-        const float* S = pout + sreg[r];
-        for (int k = 0; k < len; ++k) {
-            const int32_t x = row[k];
-            if (x == u || x < 0 || x >= g.n) continue;
-            const double s = (double)S[k];
-            if (s <= 0.0) continue;
-            const double contrib = w * s;
-            for (int64_t c = g.club_off[x]; c < g.club_off[x + 1]; ++c) {
-                const int32_t d = g.club_dense[c];
-                if (!own_club(d)) add(d, contrib);
-            }
-        }
-    }
-    __syncthreads();
-    const int n = s_n;
-    for (int i = lane; i < n; i += 64) {
-        const int32_t d = list[i];
-        score[J.out_off + i] = (float)acc[d];
-        acc[d] = 0.0;
-        touched[d] = 0;
-        list[i] = g.club_id[d];
-    }
-#else
-    (void)touched;
     __shared__ int32_t bd[kClubBuf];  // a round's contributions in sequence order (-1: own club)
     __shared__ double bv[kClubBuf];
     __shared__ int32_t sd[kClubBuf];  // the same bucketed by owner lane, stable
@@ -806,7 +748,6 @@ __global__ __launch_bounds__(64) void clubs_kernel(DevJobsStore g, DevView vw, c
         acc[d] = 0.0;
         list[i] = g.club_id[d];
     }
-#endif
     if (lane == 0) ncand[jix[slot]] = n;
 }
 
@@ -934,11 +875,11 @@ hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int 
 }
 
 hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
-                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, int32_t* touched,
-                        float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s) {
+                        const int32_t* pool, const int64_t* pool64, const float* pout, double* acc, float* score,
+                        int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(clubs_kernel, dim3(njobs), dim3(64), 0, s, g, v, jobs, jix, pool, pool64, pout, acc, touched,
-                       score, ids, ncand, acc_stride);
+    hipLaunchKernelGGL(clubs_kernel, dim3(njobs), dim3(64), 0, s, g, v, jobs, jix, pool, pool64, pout, acc, score, ids,
+                       ncand, acc_stride);
     return hipGetLastError();
 }
 

@@ -62,16 +62,8 @@ int a16(int64_t x) { return (int)((x + 15) & ~15ll); }
 
 // candidates per collaborative pair block (a multiple of 256): one staged image per block.
 // 256 measured best (r2r, cfg 3 pair kernel: 256 -> 360 us, 512 -> 367, 1024 -> 391, 2048 ->
-// 433: wider blocks stage fewer images but balance worse).  PF_PAIR_SPAN overrides it
-// (profiling only).
-int64_t pair_span() {
-    static const int64_t v = [] {
-        const char* e = getenv("PF_PAIR_SPAN");
-        const long x = e ? strtol(e, nullptr, 0) : 0;
-        return x >= 256 ? (int64_t)(x / 256 * 256) : (int64_t)256;
-    }();
-    return v;
-}
+// 433: wider blocks stage fewer images but balance worse).
+constexpr int64_t kPairSpan = 256;
 size_t a16z(size_t x) { return (x + 15) & ~(size_t)15; }
 
 int pow2_lg(int64_t n) {
@@ -599,7 +591,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                 // candidate-chunk major: the friends' blocks of one candidate chunk are
                 // consecutive, so they run together and share the chunk's records in cache;
                 // a block scores span() candidates against one staged friend image
-                const int64_t span = pair_span();
+                const int64_t span = kPairSpan;
                 std::vector<int32_t> fimg(d.nfd);
                 for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
                 for (int64_t x = 0; x < p.cap; x += span)
@@ -736,9 +728,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         if (want > J.acc_jobs) {
             const size_t words = (size_t)want * (size_t)std::max(J.js.n_club_ids, 1);
             HIPCHK(c, J.d_acc.ensure(words * 8));
-            HIPCHK(c, J.d_touched.ensure(words * 4));
             HIPCHK(c, hipMemsetAsync(J.d_acc.p, 0, J.d_acc.cap, c->stream));
-            HIPCHK(c, hipMemsetAsync(J.d_touched.p, 0, J.d_touched.cap, c->stream));
             J.acc_jobs = want;
         }
     }
@@ -781,7 +771,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
                             W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
-                           J.d_acc.as<double>(), J.d_touched.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
+                           J.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                            W.d_ncand.as<int32_t>(), (int64_t)J.js.n_club_ids, c->stream));
     HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                               W.d_slots.as<int32_t>(), W.d_ncand.as<int32_t>(), W.d_keys.as<uint64_t>(), ktop,

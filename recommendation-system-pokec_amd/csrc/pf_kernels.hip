@@ -693,10 +693,7 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
 // the block's token prefix gpre: a thread finds the list of a flat entry in 3 bisection
 // steps.  One group of 512 flat entries: a thread's two (list - js or -1, entry, norm),
 // loaded together.
-#ifndef PF_K5_GROUP_U
-#define PF_K5_GROUP_U 2
-#endif
-constexpr int kGroupU = PF_K5_GROUP_U;  // flat entries per thread in a group (3: 218 us vs 213)
+constexpr int kGroupU = 2;  // flat entries per thread in a group (r2i: 3 -> 210 us, 4 -> 217.6 vs 206)
 struct Group {
     int jj[kGroupU];
     uint32_t ent[kGroupU];
@@ -755,15 +752,11 @@ __device__ unsigned long long g_k5t[16];
 #define K5T(slot) do { } while (0)
 #endif
 
-// DBG: the PF_K5_DBG phase switches are compiled in (profiling builds of the launch only)
-template <bool DBG>
 __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-                                                              const int32_t* __restrict__ out_rows, uint32_t dbg_arg,
-                                                              uint32_t mode) {
-    const uint32_t dbg = DBG ? dbg_arg : 0u;
+                                                              const int32_t* __restrict__ out_rows, uint32_t mode) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint8_t* img = pool + img_off[blockIdx.y];
     const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
@@ -825,8 +818,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
             const bool a = c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B;
-            ha[kk] = (a && !(dbg & 128)) ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
-            hb[kk] = (a && !(dbg & 128)) ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
+            ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
+            hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
             cnt[kk * kPostThreads + tid] = 0u;
         }
         if (tid < kBlockCands / 32) exb[tid] = 0u;
@@ -836,7 +829,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
         {
-            uint32_t lo = 0, hi = (dbg & 16) ? 0u : (uint32_t)H.n_excl;
+            uint32_t lo = 0, hi = (uint32_t)H.n_excl;
             if (hi > kPostThreads) {
                 while (lo < hi) {  // first entry >= c0
                     const uint32_t mid = (lo + hi) >> 1;
@@ -853,7 +846,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             }
         }
         // 2. clubs / friends
-        if (!(dbg & 4)) walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
+        walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
             const uint32_t p = (e >> 8) - c0;
             if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
@@ -874,7 +867,6 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             pend[kk] = cm & q.colmask;
             double s = 0.0;
             int u = 0;
-            if (dbg & 32) { sum[kk] = 0.0; used |= 1u << (8 * kk); continue; }
             const uint32_t pb = (ha[kk].y >> 16) & 0xFFu, gb = ha[kk].y >> 24;
             if (q.pubcode != kCodeMissing && pb != kCodeMissing) { s += q.sig_pub[pb == q.pubcode]; ++u; }
             if (q.gencode != kCodeMissing && gb != kCodeMissing) { s += q.sig_gen[gb == q.gencode]; ++u; }
@@ -901,7 +893,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         // 4. text columns, ascending.  A pass is one column's tokens js .. js + nj - 1
         // (nj <= kChunkToks); the first group of the next pass's entries is loaded while
         // this pass is scored (software pipeline: the loads are the walk's latency).
-        const int n_act = (dbg & 8) ? 0 : H.n_act;
+        const int n_act = H.n_act;
         Group ahead;
         {
             int c = 0;  // the first column with tokens (columns without any have no passes)
@@ -922,7 +914,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             for (int js = col.j0; js < col.j1; js += kChunkToks) {
                 const int nj = min(kChunkToks, col.j1 - js);
                 const bool last = js + kChunkToks >= col.j1;
-                if (!(dbg & 1)) walk_pass(ps, rng, gpre, js, nj, ahead, [&](int j, uint32_t e, double nv) {
+                walk_pass(ps, rng, gpre, js, nj, ahead, [&](int j, uint32_t e, double nv) {
                     const uint32_t p = (e >> 8) - c0;
                     if (p < B) {
                         tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
@@ -956,7 +948,6 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 for (int kk = 0; kk < kCandsPerThread; ++kk) {
                     const int p = kk * kPostThreads + tid;
                     if (tfv[p] != 0ull) colhit |= 1u << kk;
-                    if (dbg & 2048) { tfv[p] = 0ull; continue; }
                     const bool h = (colhit >> kk) & 1u;
                     const uint64_t m = __ballot(h);
                     if (h) wl[nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
@@ -968,7 +959,6 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     const int p = wl[i];
                     uint64_t v = tfv[p];
                     tfv[p] = 0ull;
-                    if (dbg & 1024) { term[p] = (double)v; continue; }
                     double dot = multi ? term[p] : 0.0;
                     while (v) {  // the hit tokens in ascending order
                         const int j = (__ffsll((unsigned long long)v) - 1) >> 3;
@@ -980,7 +970,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                         else x = pw[2] * ((double)tf * pw[3]);
                         dot += x;
                     }
-                    term[p] = (!last || (dbg & 2)) ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
+                    term[p] = !last ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
                 wave_sync();
                 K5T(7);
@@ -1021,10 +1011,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             keys[b] = x < y ? y : x;
         };
         cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
-        if (!(dbg & 64)) {
 #pragma unroll
-            for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
-        }
+        for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         K5T(10);
         if (mode & 1u) {
             // misc[0] was last read before this block's first barrier
@@ -1159,19 +1147,6 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
     return last_nb;
 }
 
-// PF_K5_DBG: bit mask that switches K5 phases off (profiling only; results are wrong then):
-// 1 text scatter, 2 dense terms, 4 set lists, 8 all columns, 16 exclusions, 32 fixed terms,
-// 64 top-k pushes, 128 header loads, 1024 dense dots and terms, 2048 hit compaction
-static uint32_t post_dbg() {
-    static const uint32_t v = [] {
-        const char* e = getenv("PF_K5_DBG");
-        const uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
-        if (x) fprintf(stderr, "pokec_fas: PF_K5_DBG=%#x switches postings-scan phases off; scores are wrong\n", x);
-        return x;
-    }();
-    return v;
-}
-
 // K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | ranges[n_lists] | prefix[n_tok + 1]
 uint32_t post_var_lds(int n_tok, int n_lists) {
     return (uint32_t)(sizeof(PTok) * n_tok + 8 * n_lists + 4 * (n_tok + 1) + 15) & ~15u;
@@ -1182,15 +1157,10 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
                        const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
-    const uint32_t dbg = post_dbg();
     // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
     // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
-    if (dbg)
-        hipExtLaunchKernelGGL(fas_post_kernel<true>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0, e1,
-                              0u, ps, pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, dbg, mode);
-    else
-        hipExtLaunchKernelGGL(fas_post_kernel<false>, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0,
-                              e1, 0u, ps, pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, 0u, mode);
+    hipExtLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
+                          pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;
@@ -1216,7 +1186,7 @@ int post_blocks_per_cu(uint32_t var_lds) {
     static thread_local int last_nb = 1;
     if (var_lds == last_key) return last_nb;
     int nb = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel<false>, kPostThreads, post_lds(var_lds));
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel, kPostThreads, post_lds(var_lds));
     last_key = var_lds;
     last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
     return last_nb;

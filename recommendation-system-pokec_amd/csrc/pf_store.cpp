@@ -4,6 +4,8 @@
 // host-precomputed sigmoid tables (recommender_similarity.cpp:18-36).
 #include "pf_store.h"
 
+#include "pf_debug.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -209,9 +211,8 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     // longest chunk (its first record's) within kMaxTileSteps
     hs.tile_off.clear(); hs.tile_steps.clear(); hs.norm_off.clear(); hs.tile_slot0.clear(); hs.tile_lgk.clear();
     hs.slot_tile.assign(n, 0);
-    // PF_TILE_STEPS lowers the limit (tests use it to split ordinary records)
-    const char* ts = getenv("PF_TILE_STEPS");
-    const uint32_t max_steps = ts ? std::max<uint32_t>(1, (uint32_t)strtoul(ts, nullptr, 10)) : kMaxTileSteps;
+    // PF_DEBUG tile_steps lowers the limit (tests use it to split ordinary records)
+    const uint32_t max_steps = (uint32_t)std::max<long>(1, debug_long("tile_steps", kMaxTileSteps));
     uint64_t off = 0, noff = 0;
     for (int s0 = 0; s0 < n;) {
         const uint32_t mx = len[hs.idx_of_slot[s0]];
@@ -499,22 +500,14 @@ void radix_sort_u64(std::vector<uint64_t>& a, int bits) {
     }
 }
 
-// cell width 2^shift: the smallest >= one wave block holding ~<= cell_entries() of the list's
+// cell width 2^shift: the smallest >= one wave block holding ~<= kCellEntries of the list's
 // entries.  A block reads whole cells, so a short list costs up to a cell of entries per block
 // for the few that fall in it: 8 per cell reads 0.175 GB per cfg-2 query instead of 0.194 at
 // 32, and K5 takes 202.8 us instead of 206.0 (r2p A/B; 4 per cell: no further gain).
-// PF_CELL_ENTRIES overrides it (profiling only).
-uint64_t cell_entries() {
-    static const uint64_t v = [] {
-        const char* e = getenv("PF_CELL_ENTRIES");
-        const long x = e ? strtol(e, nullptr, 0) : 0;
-        return x > 0 ? (uint64_t)x : (uint64_t)8;
-    }();
-    return v;
-}
+constexpr uint64_t kCellEntries = 8;
 uint32_t list_shift(uint64_t len, int32_t n) {
     uint32_t s = kPostMinShift;
-    while (s < 30 && (len << (s + 1)) <= cell_entries() * (uint64_t)n) ++s;
+    while (s < 30 && (len << (s + 1)) <= kCellEntries * (uint64_t)n) ++s;
     return s;
 }
 

@@ -1,5 +1,5 @@
-"""Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_STAGE_LIMIT
-and PF_TILE_STEPS once per process/context, so each forced kernel variant (global-memory
+"""Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_DEBUG's
+stage_limit and tile_steps once per process/context, so each forced kernel variant (global-memory
 query tables, records split over lanes) runs in its own process.  Exits non-zero on any
 mismatch."""
 import sys

@@ -343,13 +343,13 @@ def test_big_top64_vs_oracle(big, kernel):
         assert np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), u
 
 
-@pytest.mark.parametrize("env", [{"PF_SCAN": "stream", "PF_STAGE_LIMIT": "0"},
-                                 {"PF_SCAN": "stream", "PF_STAGE_LIMIT": "1024"},
-                                 {"PF_SCAN": "stream", "PF_TILE_STEPS": "3"},
-                                 {"PF_SCAN": "stream", "PF_TILE_STEPS": "1", "PF_STAGE_LIMIT": "0"},
-                                 {"PF_SCAN": "postings"},
-                                 {"PF_SCAN": "postings", "PF_K5_BLOCK": "64"},
-                                 {"PF_SCAN": "postings", "PF_K5_BLOCK": "333"}],
+@pytest.mark.parametrize("env", [{"PF_DEBUG": "scan=stream,stage_limit=0"},
+                                 {"PF_DEBUG": "scan=stream,stage_limit=1024"},
+                                 {"PF_DEBUG": "scan=stream,tile_steps=3"},
+                                 {"PF_DEBUG": "scan=stream,tile_steps=1,stage_limit=0"},
+                                 {"PF_DEBUG": "scan=postings"},
+                                 {"PF_DEBUG": "scan=postings,k5_block=64"},
+                                 {"PF_DEBUG": "scan=postings,k5_block=333"}],
                          ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings",
                               "postings-block64", "postings-block333"])
 def test_kernel_variants(env):

@@ -187,18 +187,18 @@ def test_parallel_ingest_equals_one_thread():
         c.write_reference_files(d)
         c.close()
         out = {}
-        old = os.environ.get("PF_LOAD_THREADS")
+        old = os.environ.get("PF_DEBUG")
         try:
             for th in ("1", "7"):
-                os.environ["PF_LOAD_THREADS"] = th
+                os.environ["PF_DEBUG"] = f"load_threads={th}"
                 ds = pf.Dataset(d, -1)
                 out[th] = (desc_arrays(ds.desc_ptr()), list(ds.profile_order()), list(ds.adj_order()))
                 ds.close()
         finally:
             if old is None:
-                os.environ.pop("PF_LOAD_THREADS", None)
+                os.environ.pop("PF_DEBUG", None)
             else:
-                os.environ["PF_LOAD_THREADS"] = old
+                os.environ["PF_DEBUG"] = old
     a1, p1, j1 = out["1"]
     a7, p7, j7 = out["7"]
     assert a1["n"] == a7["n"] > 20000

@@ -4,7 +4,7 @@ reference's formats (tools/synth.py; no Pokec data offline).  Host only, no GPU.
 
     python tools/ingest_timing.py [--users N] [--dir DIR] [--single]
 
-Prints one JSON line; PF_HOST_PROF=1 adds the loader's stage clocks on stderr.
+Prints one JSON line; PF_DEBUG=host_prof=1 adds the loader's stage clocks on stderr.
 """
 import argparse
 import json
@@ -20,11 +20,11 @@ sys.path.insert(0, HERE)
 
 
 def timed_load(pf, root, threads):
-    old = os.environ.get("PF_LOAD_THREADS")
+    old = os.environ.get("PF_DEBUG")
     if threads:
-        os.environ["PF_LOAD_THREADS"] = str(threads)
+        os.environ["PF_DEBUG"] = f"load_threads={threads}"
     else:
-        os.environ.pop("PF_LOAD_THREADS", None)
+        os.environ.pop("PF_DEBUG", None)
     try:
         t = time.perf_counter()
         ds = pf.Dataset(root, -1)
@@ -33,9 +33,9 @@ def timed_load(pf, root, threads):
         ds.close()
     finally:
         if old is None:
-            os.environ.pop("PF_LOAD_THREADS", None)
+            os.environ.pop("PF_DEBUG", None)
         else:
-            os.environ["PF_LOAD_THREADS"] = old
+            os.environ["PF_DEBUG"] = old
     return dt, n
 
 

@@ -244,6 +244,8 @@ def pmc_pass(args, select):
            "--cfg3-steps", str(args.cfg3_steps)]
     if args.no_cfg3:
         cmd.append("--no-cfg3")
+    if args.sync_calls:
+        cmd.append("--sync-calls")
     try:
         r = subprocess.run(["timeout", "-s", "KILL", "240"] + cmd, capture_output=True, text=True,
                            env={**os.environ, "TMPDIR": os.environ.get("TMPDIR", "/tmp")})
@@ -334,14 +336,16 @@ def cfg3_queries(users, warm, steps, rank=0, world=1):
     return [qs[rank::world] for qs in qstream]
 
 
-def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None):
+def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True):
     """cfg 3 (BASELINE configs[2]): collaborative FoF propagation top-10 on the full corpus.  A
     step = recommend_collaborative(u, 10, 10000) for a batch of 64 seeded users (this rank's share
     at N > 1), through the device job pipeline (K3 gather, K6 images, K1' pairs, K4' sums, K8
     top-k) and back to the host.  Returns the timing and counters: pair-FAS scored (SURVEY D3's
     cfg-3 unit, |F| + |F|.|C| per user) and the pair kernel's HIP-event time per launch (its
-    roofline).  With C = len(engs) > 1 contexts, step i runs on context i % C from its own host
-    thread (ctypes releases the GIL), so one context's host planning overlaps another's device work."""
+    roofline).  One context: the steps go through the asynchronous calls (pf_recommend_collab_async,
+    two in flight), so step i + 1 is planned on the host while step i runs on the device
+    (use_async=False: the synchronous calls).  With C = len(engs) > 1 contexts, step i runs on
+    context i % C from its own host thread (ctypes releases the GIL)."""
     eng = engs[0]
     C = len(engs)
     for i in range(warm):
@@ -356,8 +360,18 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None):
 
     def run_steps(t):  # context t: steps warm + t, warm + t + C, ...
         n = 0
+        e = engs[t]
+        if use_async:
+            pend = []
+            for i in range(warm + t, warm + steps, C):
+                pend.append(e.recommend_collaborative_async(mine[i], TOPK, CFG3_LIMIT))
+                if len(pend) == 2:
+                    n += sum(len(o[0]) for o in e.wait(pend.pop(0)))
+            for p in pend:
+                n += sum(len(o[0]) for o in e.wait(p))
+            return n
         for i in range(warm + t, warm + steps, C):
-            out = engs[t].recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
+            out = e.recommend_collaborative(mine[i], TOPK, CFG3_LIMIT)
             n += sum(len(o[0]) for o in out)
         return n
 
@@ -385,7 +399,7 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None):
     st = eng.jobs_stats()
     eng.jobs_stats_reset(time_pairs=False, count=False)
     st["pair_ms"], st["pair_launches"] = timing["pair_ms"], timing["pair_launches"]
-    st["elapsed"], st["results"] = elapsed, nres
+    st["elapsed"], st["results"], st["async"] = elapsed, nres, use_async
     if dist:
         t = torch.tensor([st["pairs"], st["candidates"]], dtype=torch.float64, device="cuda")
         tm = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -434,7 +448,7 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, open_s):
     strong scaling); value = FAS pairs scored / s."""
     steps, warm = args.steps, args.warmup
     mine = cfg3_queries(args.users, warm, steps, rank, world)
-    st = measure_cfg3(engs, mine, warm, steps, dist, torch)
+    st = measure_cfg3(engs, mine, warm, steps, dist, torch, use_async=not args.sync_calls)
     C = len(engs)
     f = cfg3_fields(st, steps, pmc)
     rec = {
@@ -446,7 +460,8 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, open_s):
                                f"query users per step (limit {CFG3_LIMIT})" + (f", split over {world} GPUs" if world > 1 else ""),
                    "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{CFG3_QUERIES}_limit{CFG3_LIMIT}_world{world}",
                    "n_users": args.users, "queries_per_step": CFG3_QUERIES, "topk": TOPK, "limit": CFG3_LIMIT,
-                   "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")},
+                   "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")
+                                  + (", asynchronous calls (2 in flight)" if st["async"] else "")},
         **f, "open_s": open_s,
     }
     if rank == 0 and world == 1 and base is not None:
@@ -718,9 +733,11 @@ def main():
                          "users per step, users split over the ranks")
     ap.add_argument("--contexts", type=int, default=None,
                     help="cfg3 / cfg5: engine contexts per GPU, each a full replica driven by its own host "
-                         "thread; default 3 for cfg3 (r2s: 1 -> 1.1e9, 2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 "
-                         "pair-FAS/s) and 3 for cfg5 (with the bucketed clubs kernel, r2fk: 1 -> 39.7k, 2 -> 51.5k, "
-                         "3 -> 61.7k users/s; r2t, before it: 1 -> 28.3k, 2 -> 39.8k, 3 -> 35.4k)")
+                         "thread; default 1 for cfg3 (asynchronous calls overlap the host planning; round 2 needed "
+                         "three contexts for that: r2s 1 -> 1.1e9, 2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 pair-FAS/s) and "
+                         "3 for cfg5 (r2fk: 1 -> 39.7k, 2 -> 51.5k, 3 -> 61.7k users/s)")
+    ap.add_argument("--sync-calls", action="store_true",
+                    help="cfg3: the synchronous recommender calls instead of the asynchronous ones")
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")
@@ -748,7 +765,7 @@ def main():
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
     if args.contexts is None:
-        args.contexts = {"cfg3": 3, "cfg5": 3}.get(args.workload, 1)
+        args.contexts = {"cfg5": 3}.get(args.workload, 1)
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local)
     import synth

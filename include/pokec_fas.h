@@ -165,6 +165,29 @@ int pf_recommend_clubs(pf_ctx* ctx, const int32_t* query_uid, int32_t nq,
                        int32_t topk, int32_t candidate_limit,
                        int32_t* out_uid, float* out_score, int32_t* out_count);
 
+/*
+ * Asynchronous forms of the three job recommenders (interest in PF_MODE_FOF): the call plans the
+ * batch on the host and queues its device stages on the context's stream, then returns; the
+ * outputs (same layout as above) are written when pf_wait(ctx, ticket) returns, so the caller
+ * keeps its buffers alive until then.  While call i runs on the device the host can plan call
+ * i + 1: one context then keeps the GPU busy where the synchronous calls leave it idle during
+ * planning (what several contexts per GPU were used for).  At most two calls are in flight: a
+ * third waits for the oldest itself.  Any other call on the context (synchronous recommenders,
+ * pf_set_adj, pf_jobs_stats_*) first completes the pending ones; pf_close drops them unwritten.
+ * pf_wait(ticket) completes every call up to that ticket, in launch order; it returns the first
+ * failure among them (PF_OK for a ticket already completed).
+ */
+int pf_recommend_interest_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int32_t topk,
+                                int32_t candidate_limit, int32_t* out_uid, float* out_score,
+                                int32_t* out_count, uint64_t* ticket);
+int pf_recommend_collab_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int32_t topk,
+                              int32_t candidate_limit, int32_t* out_uid, float* out_score,
+                              int32_t* out_count, uint64_t* ticket);
+int pf_recommend_clubs_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int32_t topk,
+                             int32_t candidate_limit, int32_t* out_uid, float* out_score,
+                             int32_t* out_count, uint64_t* ticket);
+int pf_wait(pf_ctx* ctx, uint64_t ticket);
+
 /* Ordered, de-duplicated, limit-truncated 2-hop candidate list of uid
  * (flavour PF_FOF_GRAPH or PF_FOF_COLLAB).  Writes at most `cap` ids; *n gets
  * the full list length. */

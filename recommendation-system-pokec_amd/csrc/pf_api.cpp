@@ -644,6 +644,7 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
 void pf_close(pf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    c->jb.pending.clear();  // calls never waited for: their outputs are not written
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     for (auto& st : c->stage) {
@@ -763,6 +764,40 @@ int pf_recommend_clubs(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, in
         jobs[i].view = plain_view(c);
     }
     return emit_jobs(c, jobs, topk, ou, os, oc);
+}
+
+// Asynchronous forms: plan + launch now, outputs written by pf_wait (pokec_fas.h)
+static int job_async(pf_ctx* c, int kind, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
+                     float* os, int32_t* oc, uint64_t* ticket) {
+    if (!c || !ticket || nq < 0 || topk < 0 || (nq && (!q || !oc || (topk && (!ou || !os))))) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    std::vector<pf::Job> jobs(nq);
+    for (int i = 0; i < nq; ++i) {
+        jobs[i].kind = kind;
+        jobs[i].uid = q[i];
+        jobs[i].topk = topk;
+        jobs[i].limit = limit;
+        jobs[i].view = plain_view(c);
+    }
+    return pf::run_jobs_async(c, std::move(jobs), topk, ou, os, oc, ticket);
+}
+
+int pf_recommend_interest_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
+                                float* os, int32_t* oc, uint64_t* ticket) {
+    return job_async(c, pf::kJobInterest, q, nq, topk, limit, ou, os, oc, ticket);
+}
+int pf_recommend_collab_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
+                              float* os, int32_t* oc, uint64_t* ticket) {
+    return job_async(c, pf::kJobCollab, q, nq, topk, limit, ou, os, oc, ticket);
+}
+int pf_recommend_clubs_async(pf_ctx* c, const int32_t* q, int32_t nq, int32_t topk, int32_t limit, int32_t* ou,
+                             float* os, int32_t* oc, uint64_t* ticket) {
+    return job_async(c, pf::kJobClubs, q, nq, topk, limit, ou, os, oc, ticket);
+}
+int pf_wait(pf_ctx* c, uint64_t ticket) {
+    if (!c) return PF_EINVAL;
+    (void)hipSetDevice(c->device);
+    return pf::jobs_wait(c, ticket);
 }
 
 int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
+#include <deque>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -13,6 +14,7 @@
 #include <utility>
 #include <vector>
 
+#include "pf_batch.h"
 #include "pf_jobs.h"
 #include "pf_store.h"
 #include "pokec_fas.h"
@@ -115,6 +117,19 @@ struct JobsState {
         size_t o_cnt = 0, o_keys = 0, o_fail = 0;
         int ktop = 1;
     } ws[2];
+    // asynchronous calls (pf_recommend_*_async): each holds one workspace slot from its launch
+    // until pf_wait unpacks it, so at most two are in flight; their jobs live here meanwhile
+    struct Pending {
+        uint64_t ticket = 0;
+        int slot = 0;
+        std::vector<Job> jobs;
+        int32_t topk = 0;
+        int32_t* ou = nullptr;
+        float* os = nullptr;
+        int32_t* oc = nullptr;
+    };
+    std::deque<Pending> pending;                 // launch order
+    uint64_t next_ticket = 1;
     DBuf d_acc;
     int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
@@ -251,6 +266,10 @@ inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 // the device job pipeline (pf_jobs.cpp)
 int jobs_open(pf_ctx* c);                            // after the tile store is on the device
 int jobs_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n);  // pf_set_adj
+int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou, float* os, int32_t* oc,
+                   uint64_t* ticket);                // pf_recommend_*_async
+int jobs_wait(pf_ctx* c, uint64_t ticket);           // pf_wait
+int jobs_drain(pf_ctx* c);                           // every pending asynchronous call unpacked
 int fof_device(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, std::vector<int32_t>& out);
 int jobs_stats_reset(pf_ctx* c, int enable);
 int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o);

@@ -265,6 +265,8 @@ void jobs_view_scope(pf_ctx* c) {
 // batch.  An edit that restores the open-time row drops the override, so a caller that edits and
 // restores rows (the drivers, the C++ facade) keeps the table small.
 int jobs_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
+    const int rc = jobs_drain(c);  // calls in flight read the adjacency they were launched with
+    if (rc != PF_OK) return rc;
     auto& adj = c->hc.adj;
     auto& J = c->jb;
     auto it = adj.find(uid);
@@ -881,10 +883,46 @@ int finish_chunk(pf_ctx* c, std::vector<Job>& jobs, JobsState::Ws& W, std::vecto
     return PF_OK;
 }
 
+// Unpack the oldest pending asynchronous call into its caller's buffers (pf_wait).
+int finish_pending(pf_ctx* c) {
+    auto& J = c->jb;
+    JobsState::Pending& p = J.pending.front();
+    int rc = finish_chunk(c, p.jobs, J.ws[p.slot], nullptr);
+    if (rc == PF_OK)
+        for (size_t i = 0; i < p.jobs.size(); ++i) {
+            const auto& r = p.jobs[i].out;
+            const int n = std::min<int>((int)r.size(), p.topk);
+            for (int k = 0; k < n; ++k) {
+                p.ou[(int64_t)i * p.topk + k] = r[k].first;
+                p.os[(int64_t)i * p.topk + k] = r[k].second;
+            }
+            p.oc[i] = n;
+        }
+    J.pending.pop_front();
+    if (rc != PF_OK) (void)hipStreamSynchronize(c->stream);
+    return rc;
+}
+
+}  // namespace
+
+// Every pending asynchronous call unpacked (before any other use of the job pipeline's state).
+int jobs_drain(pf_ctx* c) {
+    int rc = PF_OK;
+    while (!c->jb.pending.empty()) {
+        const int r = finish_pending(c);
+        if (rc == PF_OK) rc = r;
+    }
+    return rc;
+}
+
+namespace {
+
 int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector<int32_t>>* raw_out) {
     auto& J = c->jb;
     if (!J.ok) return c->fail(PF_EUNSUPP, "device job pipeline unavailable: " + J.why);
     (void)hipSetDevice(c->device);
+    int rc0 = jobs_drain(c);  // asynchronous calls in flight finish first (they hold the workspaces)
+    if (rc0 != PF_OK) return rc0;
     for (Job& jb : jobs) jb.out.clear();
     if (jobs.empty()) return PF_OK;
     int rc = sync_nodes(c);
@@ -955,9 +993,84 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
 
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs) { return run_all(c, jobs, false, nullptr); }
 
+// An asynchronous call: planned and launched now into a free workspace slot (the oldest pending
+// call is unpacked first when both are taken), unpacked into the caller's buffers by pf_wait.
+// Its device stages queue behind the previous call's on the context's stream, so the host plans
+// call i + 1 while the device runs call i.  A call that needs more than one chunk runs as
+// run_jobs does (its outputs are written before this returns).
+int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou, float* os, int32_t* oc,
+                   uint64_t* ticket) {
+    auto& J = c->jb;
+    *ticket = J.next_ticket++;
+    if (!J.ok) return c->fail(PF_EUNSUPP, "device job pipeline unavailable: " + J.why);
+    (void)hipSetDevice(c->device);
+    for (size_t i = 0; i < jobs.size(); ++i) oc[i] = 0;
+    if (jobs.empty() || topk == 0) return PF_OK;
+    if (J.pending.size() >= 2) {
+        const int r = finish_pending(c);
+        if (r != PF_OK) return r;
+    }
+    int rc = sync_nodes(c);
+    if (rc == PF_OK) rc = sync_view(c, nullptr);
+    if (rc != PF_OK) return rc;
+    const size_t n = jobs.size();
+    std::vector<JP> P(n);
+    par_jobs(n, [&](size_t i) { plan_job(c, jobs[i], P[i], false); }, 256);
+    int64_t el = 0, ht = 0;
+    for (const JP& p : P) {
+        if (p.unmapped) return c->fail(PF_EINTERNAL, "adjacency row names an unmapped uid");
+        el += p.elems;
+        ht += p.ht_words;
+    }
+    if (n >= kPipeJobs || (n > 1 && (el > kChunkElems || ht > kChunkHt))) {  // several chunks: synchronous
+        rc = jobs_drain(c);
+        if (rc == PF_OK) rc = run_all(c, jobs, false, nullptr);
+        if (rc != PF_OK) return rc;
+        for (size_t i = 0; i < n; ++i) {
+            const int m = std::min<int>((int)jobs[i].out.size(), topk);
+            for (int k = 0; k < m; ++k) {
+                ou[(int64_t)i * topk + k] = jobs[i].out[k].first;
+                os[(int64_t)i * topk + k] = jobs[i].out[k].second;
+            }
+            oc[i] = m;
+        }
+        return PF_OK;
+    }
+    const int slot = (!J.pending.empty() && J.pending.back().slot == 0) ? 1 : 0;
+    JobsState::Pending pd;
+    pd.ticket = *ticket;
+    pd.slot = slot;
+    pd.jobs = std::move(jobs);
+    pd.topk = topk;
+    pd.ou = ou;
+    pd.os = os;
+    pd.oc = oc;
+    rc = launch_chunk(c, pd.jobs, P, 0, n, J.ws[slot]);
+    if (rc != PF_OK) {
+        (void)hipStreamSynchronize(c->stream);
+        J.ws[slot].active = false;
+        return rc;
+    }
+    if (!J.ws[slot].active) return PF_OK;  // nothing reached the device (every user unknown)
+    J.pending.push_back(std::move(pd));
+    return PF_OK;
+}
+
+int jobs_wait(pf_ctx* c, uint64_t ticket) {
+    auto& J = c->jb;
+    int rc = PF_OK;
+    while (!J.pending.empty() && J.pending.front().ticket <= ticket) {
+        const int r = finish_pending(c);
+        if (rc == PF_OK) rc = r;
+    }
+    return rc;
+}
+
 int jobs_stats_reset(pf_ctx* c, int enable) {
     auto& J = c->jb;
     (void)hipSetDevice(c->device);
+    const int rc = jobs_drain(c);
+    if (rc != PF_OK) return rc;
     HIPCHK(c, J.d_stats.ensure(64));
     HIPCHK(c, hipMemsetAsync(J.d_stats.p, 0, 64, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -971,6 +1084,8 @@ int jobs_stats_reset(pf_ctx* c, int enable) {
 int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) {
     auto& J = c->jb;
     (void)hipSetDevice(c->device);
+    const int rc = jobs_drain(c);
+    if (rc != PF_OK) return rc;
     std::memset(o, 0, sizeof *o);
     unsigned long long v[3] = {0, 0, 0};
     if (J.d_stats.p) {

@@ -27,7 +27,8 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
            "pf_recommend_interest", "pf_recommend_collab", "pf_recommend_clubs", "pf_fof_candidates", "pf_set_adj",
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
            "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel",
-           "pf_scan_bytes", "pf_jobs_stats_reset", "pf_jobs_stats_read"]
+           "pf_scan_bytes", "pf_jobs_stats_reset", "pf_jobs_stats_read", "pf_recommend_interest_async",
+           "pf_recommend_collab_async", "pf_recommend_clubs_async", "pf_wait"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -94,6 +95,9 @@ def lib():
         L.pf_recommend_collab.argtypes = [V, V, I32, I32, I32, V, V, V]
         L.pf_recommend_clubs.argtypes = [V, V, I32, I32, I32, V, V, V]
         L.pf_fof_candidates.argtypes = [V, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+        for fn in ("pf_recommend_interest_async", "pf_recommend_collab_async", "pf_recommend_clubs_async"):
+            getattr(L, fn).argtypes = [V, V, I32, I32, I32, V, V, V, ctypes.POINTER(ctypes.c_uint64)]
+        L.pf_wait.argtypes = [V, ctypes.c_uint64]
         L.pf_set_adj.argtypes = [V, I32, V, I32]
         L.pf_set_shard.argtypes = [V, I32, I32]
         L.pf_set_scan_kernel.argtypes = [V, I32]
@@ -196,6 +200,37 @@ class FasEngine:
         self._check(getattr(self._L, fn)(self.h, q.ctypes.data, len(q), k, *extra, ou.ctypes.data,
                                          os_.ctypes.data, oc.ctypes.data), fn)
         return [(ou[i * k:i * k + oc[i]].copy(), os_[i * k:i * k + oc[i]].copy()) for i in range(len(q))]
+
+    # -- asynchronous calls (pokec_fas.h): the handle keeps the output arrays alive until wait()
+    class Pending:
+        def __init__(self, q, k, ou, os_, oc, ticket):
+            self.q, self.k, self.ou, self.os, self.oc, self.ticket = q, k, ou, os_, oc, ticket
+
+    def _topk_async(self, fn, users, topk, limit):
+        q = _i32(users)
+        k = max(int(topk), 0)
+        ou = np.zeros(max(len(q) * k, 1), np.int32)
+        os_ = np.zeros(max(len(q) * k, 1), np.float32)
+        oc = np.zeros(max(len(q), 1), np.int32)
+        t = ctypes.c_uint64()
+        self._check(getattr(self._L, fn)(self.h, q.ctypes.data, len(q), k, limit, ou.ctypes.data, os_.ctypes.data,
+                                         oc.ctypes.data, ctypes.byref(t)), fn)
+        return FasEngine.Pending(q, k, ou, os_, oc, t.value)
+
+    def recommend_interest_async(self, users, topk, candidate_limit=10000):
+        return self._topk_async("pf_recommend_interest_async", users, topk, candidate_limit)
+
+    def recommend_collaborative_async(self, users, topk, candidate_limit=10000):
+        return self._topk_async("pf_recommend_collab_async", users, topk, candidate_limit)
+
+    def recommend_clubs_collab_async(self, users, topk, candidate_limit=10000):
+        return self._topk_async("pf_recommend_clubs_async", users, topk, candidate_limit)
+
+    def wait(self, p):
+        """Results of an asynchronous call (and of every earlier one), as the synchronous form's."""
+        self._check(self._L.pf_wait(self.h, p.ticket), "pf_wait")
+        k = p.k
+        return [(p.ou[i * k:i * k + p.oc[i]].copy(), p.os[i * k:i * k + p.oc[i]].copy()) for i in range(len(p.q))]
 
     # -- Recommender surface (include/recommender.h:24-35); batched over users
     def recommend_interest(self, users, topk, mode=PF_MODE_FOF, candidate_limit=10000):

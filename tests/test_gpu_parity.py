@@ -733,6 +733,7 @@ def test_driver_digests_match_reference():
     eng.close()
 
 
+@pytest.mark.parametrize("wide_fmt", [False, True], ids=["packed", "wide"])
 def test_device_df_idf_norms_and_any_token_ids(wide_fmt):
     """F3 on the device (pf_idf.hip) with token ids anywhere in int32 (the reference
     keys unordered_map<int,int>, so negative ids and ids past 2^30 are legal): df by radix sort +
@@ -796,6 +797,56 @@ def test_pipelined_job_chunks_equal_small_calls(big):
         for u, a, r in zip(q[:24], whole[:24], ofn(q[:24], 10, 1000)):
             assert list(a[0]) == list(r[0]), u
             assert np.array_equal(a[1].view(np.uint32), r[1].view(np.uint32)), u
+
+
+def test_async_calls_equal_sync(big):
+    """pf_recommend_*_async + pf_wait: up to two calls in flight on one context (a third waits for
+    the oldest), results equal to the synchronous calls bit for bit; waiting on a later ticket
+    completes the earlier ones; pf_set_adj and synchronous calls complete the pending ones first
+    (a row edit between launches affects only later calls); a batch too large for one chunk runs
+    synchronously inside the async call."""
+    c, eng, orc = big
+    rng = np.random.default_rng(31)
+    qs = [[int(x) for x in rng.integers(1, 20001, 48)] for _ in range(5)]
+    want_c = [eng.recommend_collaborative(q, 10, 2000) for q in qs]
+    want_k = [eng.recommend_clubs_collab(q, 10, 5000) for q in qs]
+    want_i = [eng.recommend_interest(q, 10, tl.PF_MODE_FOF, 5000) for q in qs]
+
+    def same(a, b):
+        for x, y in zip(a, b):
+            assert list(x[0]) == list(y[0])
+            assert np.array_equal(x[1].view(np.uint32), y[1].view(np.uint32))
+
+    hs = [eng.recommend_collaborative_async(q, 10, 2000) for q in qs]  # 3rd..5th wait for the oldest
+    for h, w in zip(hs, want_c):
+        same(eng.wait(h), w)
+    h1 = eng.recommend_clubs_collab_async(qs[0], 10, 5000)
+    h2 = eng.recommend_interest_async(qs[1], 10, 5000)
+    same(eng.wait(h2), want_i[1])  # completes h1 too
+    same(eng.wait(h1), want_k[0])
+    # an edit between two launches: the first call sees the old row, the second the new one
+    u = qs[2][0]
+    row = [int(x) for x in rng.integers(1, 20001, 7)]
+    h1 = eng.recommend_collaborative_async([u], 10, 2000)
+    eng.set_adj(u, row)
+    h2 = eng.recommend_collaborative_async([u], 10, 2000)
+    orc.set_adj(u, row)
+    (r_new,) = orc.collab([u], 10, 2000)
+    same(eng.wait(h1), [want_c[2][0]])
+    same(eng.wait(h2), [r_new])
+    # a batch of >= 1024 jobs: run synchronously inside the async call
+    q = [int(x) for x in rng.integers(1, 20001, 1100)]
+    want = eng.recommend_collaborative(q, 10, 1000)
+    same(eng.wait(eng.recommend_collaborative_async(q, 10, 1000)), want)
+    base = tl.corpus_from_desc(c.desc_ptr())
+    i = int(np.nonzero(base.adj_uid == u)[0][0]) if (base.adj_uid == u).any() else -1
+    if i >= 0:  # restore the module fixture's row
+        r0 = base.adj_nbr[base.adj_off[i]:base.adj_off[i + 1]]
+        eng.set_adj(u, r0)
+        orc.set_adj(u, r0)
+    else:
+        eng.set_adj(u, None)
+        orc.set_adj(u, None)
 
 
 def test_two_contexts_from_two_threads(big):

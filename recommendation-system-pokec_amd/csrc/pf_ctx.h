@@ -94,6 +94,9 @@ struct JobsState {
     bool nodes_dirty = false;
     std::vector<uint8_t> img_lg;                 // per idx: query-table log2 (0 = outside the device limits)
     std::vector<int32_t> img_nset;               // per idx: clubs + friends words of the record
+    std::vector<uint32_t> img_stamp;             // per idx: the layout pass that last gave it an image ...
+    std::vector<int32_t> img_pos;                // ... and that image's index (no hash map per call)
+    uint32_t img_gen = 0;
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
     std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;
@@ -106,7 +109,7 @@ struct JobsState {
     // per-chunk workspaces, double-buffered: chunk i + 1 is planned and launched while chunk i
     // runs (run_all in pf_jobs_plan.cpp); the clubs accumulators are shared (stream order)
     struct Ws {
-        DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr, d_ncand, d_keys, d_fail;
+        DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr;  // d_plan: the plan, then the results
         PinBuf h_plan, h_out;
         hipEvent_t done = nullptr;  // recorded after the chunk's result copies
         // what the chunk's unpack needs (host)

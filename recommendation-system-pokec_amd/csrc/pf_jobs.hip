@@ -32,9 +32,14 @@ namespace pf {
 
 constexpr int kJobThreads = 256;
 constexpr int kJobWaves = kJobThreads / 64;
+// K3 walks a job's 2-hop sequence in chunks of one workgroup's width: 1024 threads per job
+// (a hub's sequence of 40,000 elements is 40 chunks with 4 barriers each instead of 160)
+constexpr int kGatherThreads = 1024;
+constexpr int kGatherWaves = kGatherThreads / 64;
 
 // ---------------------------------------------------------------- block helpers
 // exclusive rank of `flag` among the block's threads and the block total (ballots + LDS)
+template <int NW = kJobWaves>
 __device__ __forceinline__ int block_rank(bool flag, int* wsum, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t m = __ballot(flag);
@@ -44,7 +49,7 @@ __device__ __forceinline__ int block_rank(bool flag, int* wsum, int& total) {
     int before = 0;
     total = 0;
 #pragma unroll
-    for (int w = 0; w < kJobWaves; ++w) {
+    for (int w = 0; w < NW; ++w) {
         const int x = wsum[w];
         if (w < wave) before += x;
         total += x;
@@ -54,6 +59,7 @@ __device__ __forceinline__ int block_rank(bool flag, int* wsum, int& total) {
 }
 
 // inclusive prefix of v over the block; total in `total`
+template <int NW = kJobWaves>
 __device__ __forceinline__ int block_scan_incl(int v, int* wsum, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int x = v;
@@ -67,7 +73,7 @@ __device__ __forceinline__ int block_scan_incl(int v, int* wsum, int& total) {
     int before = 0;
     total = 0;
 #pragma unroll
-    for (int w = 0; w < kJobWaves; ++w) {
+    for (int w = 0; w < NW; ++w) {
         const int t = wsum[w];
         if (w < wave) before += t;
         total += t;
@@ -120,12 +126,12 @@ __device__ __forceinline__ uint32_t ht_claim(int32_t* keys, uint32_t mask, int32
 
 // one workgroup per job
 // slot_shift: slot >> slot_shift < 256 (the length buckets of the candidate grouping)
-__global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
+__global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
                                                              const int32_t* __restrict__ pool, int32_t* __restrict__ ht,
                                                              int32_t* __restrict__ seq, int32_t* __restrict__ cand_slot,
                                                              int32_t* __restrict__ cand_id, int32_t* __restrict__ ncand,
                                                              const int64_t* __restrict__ pool64, int slot_shift) {
-    __shared__ int wsum[kJobWaves];
+    __shared__ int wsum[kGatherWaves];
     __shared__ int s_count, s_keep, s_done;
     const DevJob J = jobs[blockIdx.x];
     const int tid = threadIdx.x;
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
 
     if (J.kind == kDjCollab || J.kind == kDjClubs) {  // the pairs (u, f) of sim_u_f
         const int32_t* fd = pool + J.fd_off;
-        for (int r = tid; r < J.nfd; r += kJobThreads) cand_slot[J.sim_off + r] = g.slot_of[fd[r]];
+        for (int r = tid; r < J.nfd; r += kGatherThreads) cand_slot[J.sim_off + r] = g.slot_of[fd[r]];
     }
     if (J.kind == kDjClubs) {
         // recommender_clubs.cpp:47-58: each distinct friend's row, fof != u with a profile
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
         for (int r = 0; r < J.nfd; ++r) {
             int32_t len;
             const int32_t* row = row_of(g, vw, J, pool, fd[r], len);
-            for (int k = tid; k < len; k += kJobThreads) {
+            for (int k = tid; k < len; k += kGatherThreads) {
                 const int32_t x = row[k];
                 cand_slot[sreg[r] + k] = (x != u && x >= 0 && x < g.n) ? g.slot_of[x] : -1;
             }
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
     int32_t* keys = ht + J.ht_off;
     int32_t* pos = keys + cap;
     int32_t* flag = pos + cap;
-    for (uint32_t i = tid; i < cap; i += kJobThreads) {
+    for (uint32_t i = tid; i < cap; i += kGatherThreads) {
         keys[i] = 0;
         pos[i] = INT_MAX;
         flag[i] = 0;
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
     __syncthreads();
     const bool interest = J.kind == kDjInterest || J.kind == kDjAll;
     if (interest) {  // recommender_graph.cpp:46-52: existing = adj[u] + {u}
-        for (int j = tid; j <= J.nf; j += kJobThreads) {
+        for (int j = tid; j <= J.nf; j += kGatherThreads) {
             const int32_t x = j < J.nf ? frow[j] : u;
             __hip_atomic_store(&flag[ht_claim(keys, mask, x)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
     __syncthreads();
 
     if (J.kind == kDjAll) {  // every profile but the excluded ones, in idx order
-        for (int32_t i = tid; i < J.cap; i += kJobThreads) {
+        for (int32_t i = tid; i < J.cap; i += kGatherThreads) {
             bool ex = false;
             uint32_t h = (node_hash(i) >> 7) & mask;
             for (;;) {
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
     if (tid == 0) s_count = 0;
     {
         int carry = 0;
-        for (int b = 0; b < J.nf; b += kJobThreads) {
+        for (int b = 0; b < J.nf; b += kGatherThreads) {
             const int j = b + tid;
             int len = 0;
             if (j < J.nf) {
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
                 else len = rl > 0 ? rl : 0;
             }
             int tot;
-            const int incl = block_scan_incl(len, wsum, tot);
+            const int incl = block_scan_incl<kGatherWaves>(len, wsum, tot);
             if (j < J.nf) seg[j] = carry + incl - len;
             carry += tot;
         }
@@ -225,7 +231,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
         s_done = 0;
     }
     __syncthreads();
-    for (int base = 0; base < total; base += kJobThreads) {
+    for (int base = 0; base < total; base += kGatherThreads) {
         const int p = base + tid;
         int32_t x = -1;
         if (p < total) {
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
         // the table lives at L2 (device-scope atomics): read it past the CU's L1
         const bool first = x >= 0 && __hip_atomic_load(&pos[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p;
         int nfirst;
-        const int rf = block_rank(first, wsum, nfirst);
+        const int rf = block_rank<kGatherWaves>(first, wsum, nfirst);
         const int cnt = s_count;
         const bool in = first && cnt + rf < J.L;
         bool keep = in;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
             else keep = keep && x < g.n;                           // :167-170
         }
         int nkeep;
-        const int rk = block_rank(keep, wsum, nkeep);
+        const int rk = block_rank<kGatherWaves>(keep, wsum, nkeep);
         const int kb = s_keep;
         if (keep) {
             slots[kb + rk] = raw ? 0 : g.slot_of[x];
@@ -287,9 +293,9 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
     if (!raw && nk > 64) {
         __shared__ int hist[256];
         int2* tmp = reinterpret_cast<int2*>(keys);  // 3 << ht_lg words >= 2 * nk
-        hist[tid] = 0;
+        if (tid < 256) hist[tid] = 0;
         __syncthreads();
-        for (int i = tid; i < nk; i += kJobThreads) atomicAdd(&hist[slots[i] >> slot_shift], 1);
+        for (int i = tid; i < nk; i += kGatherThreads) atomicAdd(&hist[slots[i] >> slot_shift], 1);
         __syncthreads();
         if (tid < 64) {  // exclusive scan of 256 counts by one wave
             int v[4], t = 0;
@@ -305,18 +311,18 @@ __global__ __launch_bounds__(kJobThreads) void gather_kernel(DevJobsStore g, Dev
             for (int k = 0; k < 4; ++k) { hist[tid * 4 + k] = run; run += v[k]; }
         }
         __syncthreads();
-        for (int i = tid; i < nk; i += kJobThreads) {
+        for (int i = tid; i < nk; i += kGatherThreads) {
             const int32_t sl = slots[i];
             tmp[atomicAdd(&hist[sl >> slot_shift], 1)] = make_int2(sl, ids[i]);
         }
         __syncthreads();
-        for (int i = tid; i < nk; i += kJobThreads) {
+        for (int i = tid; i < nk; i += kGatherThreads) {
             const int2 e = tmp[i];
             slots[i] = e.x;
             ids[i] = e.y;
         }
     }
-    for (int i = nk + tid; i < J.cap; i += kJobThreads) {
+    for (int i = nk + tid; i < J.cap; i += kGatherThreads) {
         slots[i] = -1;
         ids[i] = -1;
     }
@@ -836,7 +842,7 @@ hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* 
     if (njobs <= 0) return hipSuccess;
     int shift = 0;
     while ((g.n >> shift) >= 256) ++shift;
-    hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kJobThreads), 0, s, g, v, jobs, pool, ht, seq, cand_slot,
+    hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kGatherThreads), 0, s, g, v, jobs, pool, ht, seq, cand_slot,
                        cand_id, ncand, pool64, shift);
     return hipGetLastError();
 }

@@ -27,6 +27,8 @@ constexpr int64_t kChunkElems = 192ll << 20; // element workspace per chunk (x 1
 constexpr int64_t kChunkHt = 128ll << 20;    // gather hash tables per chunk (int32 words)
 constexpr size_t kPipeJobs = 1024;           // calls of this many jobs or more run as pipelined chunks
 constexpr uint32_t kStageLimitJobs = 48 * 1024;  // as pf_api.cpp kStageLimit (LDS-staged tables)
+constexpr int64_t kGatherChunk = 1024;          // K3's chunk (pf_jobs.hip kGatherThreads): the last chunk
+                                                // claims up to this many table slots past the limit
 
 int32_t node_of(const pf_ctx* c, int32_t uid) {
     const auto& dn = c->jb.dense_node;  // uids of a dense range: one load (built at open)
@@ -438,7 +440,7 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
                 else p.seqlen += std::max<int64_t>(rl, 0);
             }
             p.cap = std::min<int64_t>(L, p.seqlen);
-            p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + 256));
+            p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + kGatherChunk));
         }
         p.elems = p.cap;
         p.ht_words = 3ll << p.ht_lg;
@@ -476,7 +478,7 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
         p.kind = kDjCollab;
         for (int32_t f : p.F) p.seqlen += std::max<int64_t>(rowlen(f), 0);
         p.cap = std::min<int64_t>(L, p.seqlen);
-        p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + 256));
+        p.ht_lg = pow2_lg(2 * ((int64_t)p.F.size() + 1 + p.cap + kGatherChunk));
         p.elems = p.cap + (int64_t)p.fd.size() * (1 + p.cap);
         p.ht_words = 3ll << p.ht_lg;
     } else {
@@ -506,13 +508,18 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     std::vector<int64_t> pool64;
     std::vector<int32_t> jmap;  // dj index -> job index
     int64_t E = 0, HT = 0, SEQ = 0;
-    std::unordered_map<int32_t, int32_t> img_of;
     std::vector<int32_t> img_idx;
+    if (J.img_stamp.size() != (size_t)hc.n || ++J.img_gen == 0) {  // a stamp per profile idx
+        J.img_stamp.assign((size_t)hc.n, 0u);
+        J.img_pos.assign((size_t)hc.n, 0);
+        J.img_gen = 1;
+    }
+    const uint32_t gen = J.img_gen;
     auto img = [&](int32_t idx) {
-        auto it = img_of.find(idx);
-        if (it != img_of.end()) return it->second;
+        if (J.img_stamp[idx] == gen) return J.img_pos[idx];
         const int32_t k = (int32_t)img_idx.size();
-        img_of.emplace(idx, k);
+        J.img_stamp[idx] = gen;
+        J.img_pos[idx] = k;
         img_idx.push_back(idx);
         return k;
     };
@@ -673,7 +680,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         max_lds = std::max(max_lds, need);
     }
     hl.lap(kHpImages);
-    // ---- staging: [DevJob | pool32 | pool64 | ImgJob | QImageRef | PairBlock | jix x3]
+    // ---- staging: [DevJob | pool32 | pool64 | ImgJob | QImageRef | PairBlock | jix x3], then the
+    // chunk's result region [fail word (16 B, uploaded as zero) | ncand | top-k keys], so one
+    // upload and one download carry everything (no memset, one result copy)
     if (pool32.empty()) pool32.push_back(0);
     if (pool64.empty()) pool64.push_back(0);
     const size_t o_dj = 0;
@@ -685,7 +694,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_jc = a16z(o_blk + blocks.size() * sizeof(PairBlock));
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
-    const size_t total = a16z(o_jt + jix_topk.size() * 4) + 16;
+    const size_t o_res = a16z(o_jt + jix_topk.size() * 4);
+    const size_t o_rcnt = o_res + 16, o_rkeys = o_rcnt + a16z(dj.size() * 4);
+    const size_t res_b = o_rkeys - o_res + dj.size() * (size_t)ktop * 8;
+    const size_t total = o_res + 16;  // uploaded: the plan and the zero fail word
     HIPCHK(c, W.h_plan.ensure(total));
     uint8_t* h = W.h_plan.as<uint8_t>();
     auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(h + o, src, bytes); };
@@ -698,7 +710,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
-    HIPCHK(c, W.d_plan.reserve(total));
+    std::memset(h + o_res, 0, 16);
+    HIPCHK(c, W.d_plan.reserve(o_res + res_b));
     HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
     uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
@@ -710,6 +723,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
+    int32_t* d_fail = reinterpret_cast<int32_t*>(d + o_res);
+    int32_t* d_ncand = reinterpret_cast<int32_t*>(d + o_rcnt);
+    uint64_t* d_keys = reinterpret_cast<uint64_t*>(d + o_rkeys);
     hl.lap(kHpPack);
     // ---- workspaces
     const size_t nE = (size_t)std::max<int64_t>(E, 1);
@@ -720,10 +736,6 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
     HIPCHK(c, W.d_img.reserve(std::max<size_t>(ipool, 16)));
     HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
-    HIPCHK(c, W.d_ncand.reserve(dj.size() * 4));
-    HIPCHK(c, W.d_keys.reserve(dj.size() * (size_t)ktop * 8));
-    HIPCHK(c, W.d_fail.ensure(16));
-    HIPCHK(c, hipMemsetAsync(W.d_fail.p, 0, 16, c->stream));
     hl.lap(kHpPlan);  // workspaces
     if (!jix_clubs.empty()) {
         const int64_t want = (int64_t)jix_clubs.size();
@@ -736,10 +748,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     // ---- the stages, in stream order
     HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
-                             W.d_scr.as<uint32_t>(), W.d_fail.as<int32_t>(), c->stream));
+                             W.d_scr.as<uint32_t>(), d_fail, c->stream));
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
-                            W.d_ncand.as<int32_t>(), c->stream));
+                            d_ncand, c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {
@@ -774,15 +786,15 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                             W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
                            J.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                           W.d_ncand.as<int32_t>(), (int64_t)J.js.n_club_ids, c->stream));
+                           d_ncand, (int64_t)J.js.n_club_ids, c->stream));
     HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                              W.d_slots.as<int32_t>(), W.d_ncand.as<int32_t>(), W.d_keys.as<uint64_t>(), ktop,
+                              W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop,
                               c->stream));
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
     for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;
     std::vector<size_t> full;  // dj indices copied whole
-    size_t ob = a16z(dj.size() * 4) + a16z(dj.size() * (size_t)ktop * 8) + 16;
+    size_t ob = res_b;  // [fail | ncand | keys] as on the device, then the full lists
     std::vector<size_t> full_off;
     for (size_t x = 0; x < dj.size(); ++x) {
         if (tpos[x] >= 0) continue;
@@ -792,10 +804,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     HIPCHK(c, W.h_out.ensure(ob));
     uint8_t* ho = W.h_out.as<uint8_t>();
-    const size_t o_cnt = 0, o_keys = a16z(dj.size() * 4), o_fail = o_keys + a16z(dj.size() * (size_t)ktop * 8);
-    HIPCHK(c, hipMemcpyAsync(ho + o_cnt, W.d_ncand.p, dj.size() * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ho + o_keys, W.d_keys.p, dj.size() * (size_t)ktop * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(ho + o_fail, W.d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
+    const size_t o_fail = 0, o_cnt = o_rcnt - o_res, o_keys = o_rkeys - o_res;
+    HIPCHK(c, hipMemcpyAsync(ho, d + o_res, res_b, hipMemcpyDeviceToHost, c->stream));
     for (size_t q = 0; q < full.size(); ++q) {
         const DevJob& x = dj[full[q]];
         const size_t cnt = (size_t)std::max(x.cap, x.kind == kDjClubs ? J.js.n_club_ids : 0);

@@ -122,33 +122,51 @@ __device__ __forceinline__ void walk_step_w(Walk& W, const uint4& cw, uint32_t j
     }
 }
 
+// A candidate's record and column norms as the epilogue reads them: word j of the record, and
+// sqrt(sum w_B^2) of column t (cmask = its non-empty columns).
+//   TileRec: the tile store (K1, the record-stream scan): words interleaved per tile, norms in
+//            the tile's [candidate][rank] block (two dependent loads);
+//   RowRec:  the row store (K1', pairs): the record contiguous, its norms right after it.
+struct TileRec {
+    const DevStore* st;
+    Loc l;
+    uint32_t qw;
+    __device__ uint32_t word(uint32_t j) const { return word_at(*st, l, qw, j); }
+    __device__ double norm(uint64_t cmask, int t) const { return col_norm(*st, l, cmask, t); }
+};
+struct RowRec {
+    const uint32_t* w;
+    const double* n;
+    __device__ uint32_t word(uint32_t j) const { return w[j]; }
+    __device__ double norm(uint64_t cmask, int t) const { return n[__popcll(cmask & ((1ull << t) - 1ull))]; }
+};
+
 // Text terms of a candidate whose hit list overflowed: re-walk its token words from
 // global memory, accumulating each column's dot in stream order (rare path).
-template <bool PACKED>
-__device__ __forceinline__ double text_terms_slow(const DevStore& st, const QView& v, const Loc& l, uint32_t nset,
-                                                  uint32_t len, uint64_t cmask, double sum) {
+template <bool PACKED, class Rec>
+__device__ __forceinline__ double text_terms_slow(const QView& v, const Rec& rec, uint32_t nset, uint32_t len,
+                                                  uint64_t cmask, double sum) {
     const QConst& q = *v.q;
-    const uint32_t qw = chunk_words(len, l.lgk, PACKED);
     const uint32_t cap = 1u << v.lg;
     int cur = -1;
     double dot = 0.0;
     auto close = [&]() {
         if (cur >= 0 && ((q.colmask >> cur) & 1ull))
-            sum += dot == 0.0 ? q.sig0_col[cur] : text_term(q, cur, dot, col_norm(st, l, cmask, cur));
+            sum += dot == 0.0 ? q.sig0_col[cur] : text_term(q, cur, dot, rec.norm(cmask, cur));
     };
     for (uint32_t j = nset; j < len; j += PACKED ? 1 : 2) {
         uint32_t key, col, val;
         int32_t tf;
         if (PACKED) {
-            const uint32_t w = word_at(st, l, qw, j);
+            const uint32_t w = rec.word(j);
             key = kTagTok | (w & 0xFFFFFFu);
             col = (w >> kTidBits) & 63u;
             tf = (int32_t)(w >> 24);
             val = probe_p(v, 0u, v.lg, key);
             if (val == 0u) val = kEmptyVal;
         } else {
-            const uint32_t w = word_at(st, l, qw, j + 1);
-            key = word_at(st, l, qw, j);
+            const uint32_t w = rec.word(j + 1);
+            key = rec.word(j);
             col = w & 0xFFu;
             tf = (int32_t)w >> 8;
             val = probe(v, 2u * cap, v.lg, key);
@@ -204,10 +222,9 @@ __device__ __forceinline__ void walk_chunk(Walk& W, const uint4* base, uint32_t 
 // FAS(A = staged query, B = slot p) from the walk's results: the reference's terms in the
 // reference's order.  The candidate's token hits are the hit lists of threads
 // first .. first + nl - 1 (its chunks, in record order); nh_of(g) = hits of thread first + g.
-template <bool PACKED, class NH>
-__device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v, const Loc& l, const uint4& h0,
-                                              const uint4& h1, const uint4& h2, uint32_t cnt, uint32_t first,
-                                              uint32_t nl, NH nh_of) {
+template <bool PACKED, class Rec, class NH>
+__device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, const uint4& h0, const uint4& h1,
+                                              const uint4& h2, uint32_t cnt, uint32_t first, uint32_t nl, NH nh_of) {
     using H = HitT<PACKED>;
     const QConst& q = *v.q;
     const uint32_t hstride = blockDim.x;
@@ -232,7 +249,7 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
     };
     bool have = next();
     // the first hit column's norm (global) is requested now and lands under the fixed terms
-    double nrm = have ? col_norm(st, l, cmask, (int)H::col(e)) : 0.0;
+    double nrm = have ? rec.norm(cmask, (int)H::col(e)) : 0.0;
 
     double sum = 0.0;
     int used = 0;
@@ -273,7 +290,7 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
                 dot += hit_product(v, H::vi(e), H::tf(e));
                 have = next();
             }
-            if (have) nrm = col_norm(st, l, cmask, (int)H::col(e));
+            if (have) nrm = rec.norm(cmask, (int)H::col(e));
             uint64_t below = common & ((1ull << t) - 1ull);
             common &= ~below & ~(1ull << t);
             while (below) {
@@ -289,7 +306,7 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
             sum += q.sig0_col[c];
         }
     } else {
-        sum = text_terms_slow<PACKED>(st, v, l, nc + nf, record_words(h2, PACKED), cmask, sum);
+        sum = text_terms_slow<PACKED>(v, rec, nc + nf, record_words(h2, PACKED), cmask, sum);
     }
     if (used == 0) return 0.0f;
     // recommender_similarity.cpp:114-123
@@ -301,17 +318,16 @@ __device__ __forceinline__ float fas_epilogue(const DevStore& st, const QView& v
 
 // FAS of slot p by one lane alone (pairs kernel): the lane walks the slot's record in the row
 // store (contiguous 16-B steps, so the lane's loads consume whole cache lines), its own hit list
-// then holds the whole record's hits in order.
+// then holds the whole record's hits in order; the column norms follow the record in the row
+// store, so no tile lookup sits in front of them.
 template <bool PACKED>
 __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-    Loc l{0, 0, 0};
     uint64_t ro = 0;
     if (active) {
         h0 = st.hdr0[p];
         h1 = st.hdr1[p];
         h2 = st.hdr2[p];
-        l = loc_of(st, p);
         ro = st.row_off[p];
     }
     const uint32_t nc = h2.y, nset = h2.y + h2.z;
@@ -321,7 +337,9 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     walk_chunk<PACKED, true, 1>(W, st.rows + ro, 0u, len, nc, nset, v, blockDim.x);
     if (!active) return 0.0f;
     const uint32_t nh = W.nh;
-    return fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+    const RowRec rec{reinterpret_cast<const uint32_t*>(st.rows + ro),
+                     reinterpret_cast<const double*>(st.rows + ro + ((len + 3) >> 2))};
+    return fas_epilogue<PACKED>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
 }
 
 // ---------------------------------------------------------------- LDS staging
@@ -566,7 +584,8 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         if (lgk == 0) {
             if (active) {
                 const uint32_t nh = W.nh;
-                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+                const TileRec rec{&st, l, q};
+                f = fas_epilogue<PACKED>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
             }
         } else {
             // a split record: sum the chunk counters over its lanes, publish the hit counts,
@@ -577,7 +596,8 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
             __builtin_amdgcn_wave_barrier();
             if (active && ci == 0) {
                 const uint32_t* nhp = v.nh + threadIdx.x;
-                f = fas_epilogue<PACKED>(st, v, l, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
+                const TileRec rec{&st, l, q};
+                f = fas_epilogue<PACKED>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
                                          [&](uint32_t g) { return nhp[g]; });
             }
         }

@@ -241,9 +241,14 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     hs.norm_off.push_back(noff);  // sentinel: a tile's rank count = (norm_off[t+1] - norm_off[t]) / 64
     hs.stream.assign(off + 4 * kTileSlots, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     // row store (the pair kernel K1'): each slot's record contiguous, padded to 16 B, so a lane
-    // walking one candidate reads whole cache lines (the tile stream strides a record by 1 KiB)
+    // walking one candidate reads whole cache lines (the tile stream strides a record by 1 KiB),
+    // then the slot's column norms (one double per non-empty column, 16-B padded): the epilogue
+    // reads them from the lines after the record, with no tile lookup in front
     hs.row_off.assign((size_t)n + 1, 0);
-    for (int p = 0; p < n; ++p) hs.row_off[p + 1] = hs.row_off[p] + (len[hs.idx_of_slot[p]] + 3) / 4;
+    for (int p = 0; p < n; ++p) {
+        const int i = hs.idx_of_slot[p];
+        hs.row_off[p + 1] = hs.row_off[p] + (len[i] + 3) / 4 + (ncols[i] + 1) / 2;
+    }
     hs.rows.assign(hs.row_off[n] + 1, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     hs.norms.assign(noff, 0.0);
     hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
@@ -276,6 +281,14 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                 }
             }
             std::memcpy(reinterpret_cast<uint32_t*>(hs.rows.data() + hs.row_off[p]), w.data(), w.size() * 4);
+            {  // the record's norms after its 16-B padded words
+                double* rn = reinterpret_cast<double*>(hs.rows.data() + hs.row_off[p] + (w.size() + 3) / 4);
+                uint32_t rk = 0;
+                for (int t = 0; t < T; ++t) {
+                    const size_t r = (size_t)i * T + t;
+                    if (hc.tok_off[r + 1] != hc.tok_off[r]) rn[rk++] = hc.sqrt_nb[r];
+                }
+            }
             // chunk c of the record goes to lane cand * k + c
             const uint32_t q = chunk_words((uint32_t)w.size(), lgk, packed);
             uint32_t* base = reinterpret_cast<uint32_t*>(hs.stream.data() + hs.tile_off[tile]);

@@ -16,7 +16,7 @@ constexpr int kNormSlots = kNumFixed + kMaxCols;
 constexpr int kValTab = 128;        // completion/age sigmoid tables cover values 1..128
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
-constexpr uint32_t kHitCap = 24;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
+constexpr uint32_t kHitCap = 16;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
 constexpr int kMaxHashLog2 = 16;    // cuckoo tables <= 65536 slots (h1/h2 from one 32-bit product)
 constexpr uint32_t kMaxTileSteps = 48;  // a record longer than 48 steps (192 words) is split over lanes
 
@@ -165,7 +165,8 @@ struct DevStore {
     const uint4* hdr0;         // [n_slots]
     const uint4* hdr1;
     const uint4* hdr2;
-    const uint4* rows;         // row store: slot p's record contiguous from rows[row_off[p]] (pair kernel)
+    const uint4* rows;         // row store: slot p's record contiguous from rows[row_off[p]], padded to 16 B,
+                               // then its column norms (double per non-empty column, ascending) (pair kernel)
     const uint64_t* row_off;   // [n_slots + 1]
     int32_t n_slots;
     int32_t n_tiles;

@@ -85,6 +85,7 @@ void add_image(Images& im, const pf::QImageHost& q) {
     im.max_lds = std::max(im.max_lds, need);
     im.refs.push_back(r);
 }
+constexpr uint32_t kPairThreads = (uint32_t)pf::kPairThreads;
 
 // Many images at once: refs and offsets first (returns the pool bytes), then fill_images
 // copies them on threads into `dst` (pinned; a few thousand images per chunk).
@@ -100,8 +101,8 @@ size_t plan_images(Images& im, const std::vector<pf::QImageHost>& qs) {
         const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
         r.lds_bytes = kv <= stage_limit() ? (uint32_t)kv : 0u;
         im.gtab = im.gtab || r.lds_bytes == 0;
-        const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kBlockThreads +
-                              4u * kBlockThreads + 2048u;
+        const uint32_t need = (uint32_t)sizeof(pf::QConst) + r.lds_bytes + q.c.n_hits_max * kPairThreads +
+                              4u * kPairThreads + 2048u;
         im.max_lds = std::max(im.max_lds, need);
         im.refs.push_back(r);
     }
@@ -185,7 +186,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
         // per group: first block and first pair (serial, O(groups)); then the copies on threads
         std::vector<size_t> gb(g1 - g0 + 1), gf(g1 - g0 + 1);
         for (size_t g = g0; g < g1; ++g) {
-            gb[g - g0 + 1] = gb[g - g0] + (slots[g].size() + 255) / 256;
+            gb[g - g0 + 1] = gb[g - g0] + (slots[g].size() + kPairThreads - 1) / kPairThreads;
             gf[g - g0 + 1] = gf[g - g0] + slots[g].size();
         }
         const size_t npairs = gf.back();
@@ -200,8 +201,8 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
             if (slots[g].empty()) return;
             const int32_t img = img_of.at(qidx[g]);
             std::memcpy(flat + gf[i], slots[g].data(), slots[g].size() * sizeof(int32_t));
-            for (size_t b = 0, x = gb[i]; b < slots[g].size(); b += 256, ++x)
-                blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(256, slots[g].size() - b),
+            for (size_t b = 0, x = gb[i]; b < slots[g].size(); b += kPairThreads, ++x)
+                blocks[x] = pf::PairBlock{img, (int32_t)(gf[i] + b), (int32_t)std::min<size_t>(kPairThreads, slots[g].size() - b),
                                            (int32_t)(gf[i] + b)};
         }, 256);
         hl.lap(pf::kHpPack);
@@ -220,7 +221,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
             dsc = c->d_scores.as<float>();
         }
         HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
-                                   c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), c->d_slots.as<int32_t>(), dsc,
+                                   c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), nullptr, c->d_slots.as<int32_t>(), dsc,
                                    c->stream));
         const float* res = c->h_scores.as<float>();
         HIPCHK(c, hipMemcpyAsync(c->h_scores.p, dsc, npairs * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -585,6 +586,7 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         c->hip_fail(e, "corpus upload");
         return bail(e == hipErrorOutOfMemory ? PF_ENOMEM : PF_ENODEV);
     }
+    c->ds.row_pad = c->d_rowstore.as<uint4>() + hs.row_off[c->hc.n];  // build_store's trailing padding line
     c->stream_bytes = (int64_t)hs.stream.size() * 16;
     c->norm_bytes = (int64_t)hs.norms.size() * 8;
     std::vector<uint4>().swap(hs.stream);

@@ -13,6 +13,8 @@
 //
 // e.g. PF_DEBUG=scan=stream,stage_limit=0
 #pragma once
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -44,5 +46,18 @@ inline long debug_long(const char* name, long dflt) {
     const char* v = debug_str(name);
     return v ? std::strtol(v, nullptr, 0) : dflt;
 }
+
+// Sub-stage clock of pf_open's builders: lap(what) prints the time since the last lap on stderr
+// when PF_DEBUG host_prof is set.
+struct StageClock {
+    bool on = debug_long("host_prof", 0) != 0;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[pf_open]     %s %.3f s\n", what, std::chrono::duration<double>(n - t).count());
+        t = n;
+    }
+};
 
 }  // namespace pf

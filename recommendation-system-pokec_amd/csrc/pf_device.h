@@ -76,17 +76,20 @@ __device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, 
     return r1 & r2;
 }
 
-// Packed tables: the same probe with miss = 0 (empty slots are {~0, 0})
-__device__ __forceinline__ uint32_t probe_p(const QView& v, uint32_t off, int lg, uint32_t key) {
-    const uint32_t x = cuckoo_x(key, v.hmul);
+// Packed tables: the same probe with miss = 0 (empty slots are {~0, 0}); x = the key's hash
+__device__ __forceinline__ uint32_t probe_px(const QView& v, uint32_t off, int lg, uint32_t key, uint32_t x) {
     const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
     const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
     return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
 }
+// the record table T
+__device__ __forceinline__ uint32_t probe_p(const QView& v, uint32_t key) {
+    return probe_px(v, 0u, v.lg, key, cuckoo_x(key, v.hmul));
+}
 
 template <bool PACKED>
 __device__ __forceinline__ bool excluded(const QView& v, uint32_t uid) {
-    if (PACKED) return probe_p(v, v.excl_off, v.lge, uid) != 0u;
+    if (PACKED) return probe_px(v, v.excl_off, v.lge, uid, cuckoo_x(uid, v.hmul)) != 0u;
     return probe(v, v.excl_off, v.lge, uid) != kEmptyVal;
 }
 

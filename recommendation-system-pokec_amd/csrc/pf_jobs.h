@@ -28,6 +28,9 @@ hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int 
 hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
                         const int32_t* pool, const int64_t* pool64, const float* pout, double* acc,
                         float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);
+// the pair blocks' dispatch order, longest first record first (pf_jobs.hip order_pairs_kernel)
+hipError_t launch_order_pairs(const PairBlock* blocks, int nblocks, const int32_t* slots, int32_t n_slots,
+                              int32_t* order, hipStream_t s);
 hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
                              unsigned long long* acc, hipStream_t s);
 hipError_t launch_job_topk(const DevJob* jobs, const int32_t* jix, int njobs, const float* score, const int32_t* ids,

@@ -124,13 +124,22 @@ __device__ __forceinline__ uint32_t ht_claim(int32_t* keys, uint32_t mask, int32
     }
 }
 
+// Length class of a slot (< 232 for any int32 slot, monotone): slots are assigned longest
+// record first, so small slots are the long records, whose lengths spread the most (the synthetic
+// D1 corpus: slot 0 holds 2,155 words, slot 1,600 ~430, the median 125).  Classes 0..7 are slots
+// 0..7, then eight classes per power of two of the slot (its top four bits).
+__device__ __forceinline__ int slot_class(int32_t sl) {
+    if (sl < 8) return sl;
+    const int lg = 31 - __clz(sl);  // >= 3
+    return 8 + ((lg - 3) << 3) + ((sl >> (lg - 3)) & 7);
+}
+
 // one workgroup per job
-// slot_shift: slot >> slot_shift < 256 (the length buckets of the candidate grouping)
 __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, DevView vw, const DevJob* __restrict__ jobs,
                                                              const int32_t* __restrict__ pool, int32_t* __restrict__ ht,
                                                              int32_t* __restrict__ seq, int32_t* __restrict__ cand_slot,
                                                              int32_t* __restrict__ cand_id, int32_t* __restrict__ ncand,
-                                                             const int64_t* __restrict__ pool64, int slot_shift) {
+                                                             const int64_t* __restrict__ pool64) {
     __shared__ int wsum[kGatherWaves];
     __shared__ int s_count, s_keep, s_done;
     const DevJob J = jobs[blockIdx.x];
@@ -284,10 +293,9 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
         if (s_count >= J.L) break;
     }
     const int nk = s_keep;
-    // The scored candidates grouped by slot range, i.e. by record length (slots are assigned
-    // longest record first, pf_store.cpp build_store), so the pair kernel's 64-lane waves walk
-    // records of similar length instead of waiting on the longest of 64 random ones: a counting
-    // sort into 256 slot buckets through the (finished) hash table's memory.  The order is free:
+    // The scored candidates grouped by length class (slot_class), longest first, so the pair
+    // kernel's 64-lane waves walk records of similar length instead of waiting on the longest of
+    // 64 random ones: a counting sort into 256 buckets through the (finished) hash table's memory.  The order is free:
     // every later stage keeps slot, id and score together, and the top-k's total order does not
     // depend on it.  (Raw lists keep the reference's order.)
     if (!raw && nk > 64) {
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
         int2* tmp = reinterpret_cast<int2*>(keys);  // 3 << ht_lg words >= 2 * nk
         if (tid < 256) hist[tid] = 0;
         __syncthreads();
-        for (int i = tid; i < nk; i += kGatherThreads) atomicAdd(&hist[slots[i] >> slot_shift], 1);
+        for (int i = tid; i < nk; i += kGatherThreads) atomicAdd(&hist[slot_class(slots[i])], 1);
         __syncthreads();
         if (tid < 64) {  // exclusive scan of 256 counts by one wave
             int v[4], t = 0;
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
         __syncthreads();
         for (int i = tid; i < nk; i += kGatherThreads) {
             const int32_t sl = slots[i];
-            tmp[atomicAdd(&hist[sl >> slot_shift], 1)] = make_int2(sl, ids[i]);
+            tmp[atomicAdd(&hist[slot_class(sl)], 1)] = make_int2(sl, ids[i]);
         }
         __syncthreads();
         for (int i = tid; i < nk; i += kGatherThreads) {
@@ -327,6 +335,35 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
         ids[i] = -1;
     }
     if (tid == 0) ncand[blockIdx.x] = nk;
+}
+
+// ---------------------------------------------------------------- pair-block dispatch order
+// The pair kernel's blocks longest work first: a block's key is the record length class of its
+// first candidate (K3 lists a job's candidates longest first, in slot buckets; slots are
+// assigned longest record first, pf_store.cpp build_store), so the blocks holding the few
+// hub-length records (up to ~17x the mean) start in the first resident round instead of
+// trailing the launch.  One workgroup, a counting sort over 256 slot buckets (+ one for blocks
+// without a candidate, last); the order within a bucket is free (each block writes its own
+// outputs).
+constexpr int kOrderThreads = 1024;
+
+__global__ __launch_bounds__(kOrderThreads) void order_pairs_kernel(const PairBlock* __restrict__ blocks, int nblocks,
+                                                                    const int32_t* __restrict__ slots,
+                                                                    int32_t* __restrict__ order) {
+    __shared__ int hist[258];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 258; i += kOrderThreads) hist[i] = 0;
+    __syncthreads();
+    auto key = [&](int b) {
+        const int32_t s0 = slots[blocks[b].begin];
+        return s0 < 0 ? 256 : slot_class(s0);
+    };
+    for (int b = tid; b < nblocks; b += kOrderThreads) atomicAdd(&hist[key(b) + 1], 1);
+    __syncthreads();
+    if (tid == 0)
+        for (int i = 1; i < 258; ++i) hist[i] += hist[i - 1];  // hist[k] = first position of bucket k
+    __syncthreads();
+    for (int b = tid; b < nblocks; b += kOrderThreads) order[atomicAdd(&hist[key(b)], 1)] = b;
 }
 
 // ---------------------------------------------------------------- K6: query images
@@ -543,10 +580,22 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
     const float* sim = pout + J.sim_off;
     const float* M = pout + J.m_off;
     double s = 0.0;
-    for (int j = 0; j < J.nf; ++j) {
-        const int r = fpos[j];
-        if (r < 0) continue;
-        s += (double)sim[r] * (double)M[(size_t)r * J.cap + c];
+    // 32 friend positions at a time: their loads are issued together (one round trip per 32
+    // friends on a hub's long row), the adds stay in order
+    constexpr int U = 32;
+    for (int j0 = 0; j0 < J.nf; j0 += U) {
+        int r[U];
+        float w[U], m[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) r[k] = j0 + k < J.nf ? fpos[j0 + k] : -1;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            w[k] = r[k] >= 0 ? sim[r[k]] : 0.0f;
+            m[k] = r[k] >= 0 ? M[(size_t)r[k] * J.cap + c] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (r[k] >= 0) s += (double)w[k] * (double)m[k];
     }
     score[J.out_off + c] = (float)s;
 }
@@ -836,14 +885,20 @@ hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nb
     return hipGetLastError();
 }
 
+hipError_t launch_order_pairs(const PairBlock* blocks, int nblocks, const int32_t* slots, int32_t n_slots,
+                              int32_t* order, hipStream_t s) {
+    if (nblocks <= 0) return hipSuccess;
+    (void)n_slots;
+    hipLaunchKernelGGL(order_pairs_kernel, dim3(1), dim3(kOrderThreads), 0, s, blocks, nblocks, slots, order);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
                          int32_t* ncand, hipStream_t s) {
     if (njobs <= 0) return hipSuccess;
-    int shift = 0;
-    while ((g.n >> shift) >= 256) ++shift;
     hipLaunchKernelGGL(gather_kernel, dim3(njobs), dim3(kGatherThreads), 0, s, g, v, jobs, pool, ht, seq, cand_slot,
-                       cand_id, ncand, pool64, shift);
+                       cand_id, ncand, pool64);
     return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "pf_batch.h"
+#include "pf_debug.h"
 #include "pf_ctx.h"
 #include "pf_kernels.h"
 
@@ -62,10 +63,8 @@ hipError_t up(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
 
 int a16(int64_t x) { return (int)((x + 15) & ~15ll); }
 
-// candidates per collaborative pair block (a multiple of 256): one staged image per block.
-// 256 measured best (r2r, cfg 3 pair kernel: 256 -> 360 us, 512 -> 367, 1024 -> 391, 2048 ->
-// 433: wider blocks stage fewer images but balance worse).
-constexpr int64_t kPairSpan = 256;
+// candidates per pair block = the pair kernel's block (one pair per thread, pf_kernels.h)
+constexpr int64_t kPairSpan = kPairThreads;
 size_t a16z(size_t x) { return (x + 15) & ~(size_t)15; }
 
 int pow2_lg(int64_t n) {
@@ -84,6 +83,7 @@ int jobs_open(pf_ctx* c) {
     const int32_t n = hc.n, T = hc.T;
     const bool packed = hs.packed;
     J.ok = false;
+    StageClock sc;
     // image-builder tables: QConst template, region rows, completion / age rows (glibc exp)
     QConst tmpl;
     qconst_template(hc, packed, tmpl);
@@ -118,6 +118,7 @@ int jobs_open(pf_ctx* c) {
         dense.insert(dense.end(), hc.idf[t].begin(), hc.idf[t].end());
     }
     if (dense.empty()) dense.push_back(1.0f);
+    sc.lap("image-builder tables");
     // graph: nodes 0..n-1 = profiles (idx), then adj_list uids without a profile
     J.xnode.clear();
     J.g_uid.assign(hc.uid.begin(), hc.uid.end());
@@ -146,6 +147,7 @@ int jobs_open(pf_ctx* c) {
     }
     const int32_t M = (int32_t)J.g_uid.size();
     J.g_len.assign(M, -1);
+    sc.lap("graph nodes");
     // uid -> node as a dense table when the uids are non-negative and not too sparse
     J.dense_node.clear();
     {
@@ -175,6 +177,7 @@ int jobs_open(pf_ctx* c) {
         g_off[rnode[r]] = roff[r];
         J.g_len[rnode[r]] = (int32_t)rows[r]->second.size();
     }
+    sc.lap("graph CSR");
     // clubs as dense indices (K7), per profile idx in profile order
     std::vector<int32_t> club_id(hc.clubs.begin(), hc.clubs.end());
     std::sort(club_id.begin(), club_id.end());
@@ -183,6 +186,7 @@ int jobs_open(pf_ctx* c) {
     par_jobs(hc.clubs.size(), [&](size_t k) {
         club_dense[k] = (int32_t)(std::lower_bound(club_id.begin(), club_id.end(), (int32_t)hc.clubs[k]) - club_id.begin());
     }, 1 << 16);
+    sc.lap("club indices");
     // per profile: query-table size (pf_store.cpp build_query) and its raw set words
     J.img_lg.assign(n, 0);
     J.img_nset.assign(n, 0);
@@ -200,6 +204,7 @@ int jobs_open(pf_ctx* c) {
         J.img_nset[i] = (int32_t)((hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]));
     }, 4096);
     std::vector<int32_t> slot_of(hs.slot_of_idx.begin(), hs.slot_of_idx.end());
+    sc.lap("image sizes");
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = up(c, J.d_tmpl, tv);
     if (e == hipSuccess) e = up(c, J.d_sigreg, sreg);
@@ -220,6 +225,7 @@ int jobs_open(pf_ctx* c) {
     if (e == hipSuccess) e = up(c, J.d_club_id, club_id);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the host vectors die here
     if (e != hipSuccess) return c->hip_fail(e, "job pipeline upload");
+    sc.lap("upload");
     DevJobsStore& g = J.js;
     g.tmpl = J.d_tmpl.as<QConst>();
     g.sig_reg = J.d_sigreg.as<double>();
@@ -525,8 +531,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     };
     std::vector<PairBlock> blocks;
     auto add_blocks = [&](int32_t im, int64_t begin, int64_t count, int64_t out) {
-        for (int64_t x = 0; x < count; x += 256)
-            blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(256, count - x),
+        for (int64_t x = 0; x < count; x += kPairSpan)
+            blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(kPairSpan, count - x),
                                        (int32_t)(out + x)});
     };
     std::vector<int32_t> jix_collab, jix_clubs, jix_topk;
@@ -536,8 +542,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (size_t i = b; i < e; ++i) {
             const JP& p = P[i];
             if (p.kind < 0) continue;
-            const size_t ch = (size_t)(p.cap + 255) / 256;
-            nb += ch * (1 + p.fd.size()) + 1 + p.fd.size() + (size_t)p.seqlen / 256;
+            const size_t ch = (size_t)(p.cap + kPairSpan - 1) / kPairSpan;
+            nb += ch * (1 + p.fd.size()) + 1 + p.fd.size() + (size_t)p.seqlen / kPairSpan;
             words += p.own.size() + p.F.size() + 2 * p.fd.size();
         }
         blocks.reserve(nb);
@@ -675,8 +681,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
         r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;
         gtab = gtab || r.lds_bytes == 0;
-        const uint32_t need = (uint32_t)sizeof(QConst) + r.lds_bytes + (kHitCap + 1) * (packed ? 4u : 8u) * 256u +
-                              4u * 256u + 2048u;
+        const uint32_t need = (uint32_t)sizeof(QConst) + r.lds_bytes + kHitSlots * (packed ? 4u : 8u) * kPairThreads +
+                              4u * kPairThreads + 2048u;
         max_lds = std::max(max_lds, need);
     }
     hl.lap(kHpImages);
@@ -711,7 +717,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
     std::memset(h + o_res, 0, 16);
-    HIPCHK(c, W.d_plan.reserve(o_res + res_b));
+    const size_t o_ord = a16z(o_res + res_b);  // the pair blocks' dispatch order (device-written)
+    HIPCHK(c, W.d_plan.reserve(o_ord + std::max<size_t>(blocks.size(), 1) * 4));
     HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
     uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
@@ -724,6 +731,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
     int32_t* d_fail = reinterpret_cast<int32_t*>(d + o_res);
+    int32_t* d_ord = reinterpret_cast<int32_t*>(d + o_ord);
     int32_t* d_ncand = reinterpret_cast<int32_t*>(d + o_rcnt);
     uint64_t* d_keys = reinterpret_cast<uint64_t*>(d + o_rkeys);
     hl.lap(kHpPack);
@@ -752,6 +760,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
                             d_ncand, c->stream));
+    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, c->stream));
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && !blocks.empty()) {
         if (J.stat_used == J.stat_ev.size()) {
@@ -765,7 +774,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         ++J.stat_used;
         HIPCHK(c, hipEventRecord(pe0, c->stream));
     }
-    HIPCHK(c, launch_pairs(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(),
+    HIPCHK(c, launch_pairs(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(), d_ord,
                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
     if (pe1) {
         HIPCHK(c, hipEventRecord(pe1, c->stream));

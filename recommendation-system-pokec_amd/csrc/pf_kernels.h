@@ -6,8 +6,11 @@
 
 namespace pf {
 
-// one 256-thread block of the pair kernel: FAS(image qimg, slots[begin + i]) -> out[out + i]
-// for i < count; a slot < 0 is skipped (its output is not written)
+// One block of the pair kernel, kPairThreads threads, one pair each: FAS(image qimg,
+// slots[begin + i]) -> out[out + i] for i < count <= kPairThreads; a slot < 0 is skipped (its
+// output is not written).  512: one staged image serves eight waves, and two workgroups per CU
+// hold 16 waves where 256-thread ones held 12 (their LDS, mostly the per-lane hit lists).
+constexpr int kPairThreads = 512;
 struct PairBlock {
     int32_t qimg, begin, count, out;
 };
@@ -32,9 +35,10 @@ int post_blocks_per_cu(uint32_t var_lds);
 // plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
                         uint64_t* out, hipStream_t s);
+// order (nullable): the dispatch order, block blockIdx.x scores blocks[order[blockIdx.x]]
 hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
-                        bool gtab, const PairBlock* blocks, int nblocks, const int32_t* slots, float* out,
-                        hipStream_t s);
+                        bool gtab, const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
+                        float* out, hipStream_t s);
 // one collaborative query of a K4 batch: M rows at moff ([rows][nc]), w / row at woff ([F]),
 // scores to out + coff ([nc])
 struct CollabSum {

@@ -81,7 +81,7 @@ __device__ __forceinline__ void walk_step_p(Walk& W, const uint4& cw, int sj, in
         tok[i] = sj + i >= tb;
         uint32_t key = tok[i] ? (kTagTok | (w[i] & 0xFFFFFFu)) : w[i];
         if (MASKED) key = sj + i < lim ? key : kPadWord;
-        val[i] = probe_p(v, 0u, v.lg, key);
+        val[i] = probe_p(v, key);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -162,7 +162,7 @@ __device__ __forceinline__ double text_terms_slow(const QView& v, const Rec& rec
             key = kTagTok | (w & 0xFFFFFFu);
             col = (w >> kTidBits) & 63u;
             tf = (int32_t)(w >> 24);
-            val = probe_p(v, 0u, v.lg, key);
+            val = probe_p(v, key);
             if (val == 0u) val = kEmptyVal;
         } else {
             const uint32_t w = rec.word(j + 1);
@@ -178,6 +178,47 @@ __device__ __forceinline__ double text_terms_slow(const QView& v, const Rec& rec
             dot = 0.0;
         }
         if (val != kEmptyVal) dot += hit_product(v, PACKED ? (val & kTidMask) : (val >> 8), tf);
+    }
+    close();
+    return sum;
+}
+
+// The same for a record in the row store (the pair kernel's overflowed hit lists): the token
+// words in 16-B steps, four steps in flight (a lane alone walks its record here, so the
+// loads' latency is the cost).
+__device__ __forceinline__ double text_terms_row(const QView& v, const uint4* base, const double* norms, uint32_t nset,
+                                              uint32_t len, uint64_t cmask, double sum) {
+    const QConst& q = *v.q;
+    int cur = -1;
+    double dot = 0.0;
+    auto close = [&]() {
+        if (cur >= 0 && ((q.colmask >> cur) & 1ull))
+            sum += dot == 0.0 ? q.sig0_col[cur]
+                              : text_term(q, cur, dot, norms[__popcll(cmask & ((1ull << cur) - 1ull))]);
+    };
+    const uint32_t steps = (len + 3) >> 2, s0 = nset >> 2;
+    if (len <= nset) return sum;
+    auto ld = [&](uint32_t s) { return base[s < steps ? s : steps - 1]; };
+    uint4 r0 = ld(s0), r1 = ld(s0 + 1), r2 = ld(s0 + 2), r3 = ld(s0 + 3);
+    for (uint32_t s = s0; s < steps; ++s) {
+        const uint4 cw = r0;
+        r0 = r1; r1 = r2; r2 = r3;
+        r3 = ld(s + 4);
+        const uint32_t w4[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t j = 4 * s + (uint32_t)i;
+            if (j < nset || j >= len) continue;
+            const uint32_t w = w4[i];
+            const int col = (int)((w >> kTidBits) & 63u);
+            if (col != cur) {
+                close();
+                cur = col;
+                dot = 0.0;
+            }
+            const uint32_t val = probe_p(v, kTagTok | (w & 0xFFFFFFu));
+            if (val != 0u) dot += hit_product(v, val & kTidMask, (int32_t)(w >> 24));
+        }
     }
     close();
     return sum;
@@ -222,9 +263,13 @@ __device__ __forceinline__ void walk_chunk(Walk& W, const uint4* base, uint32_t 
 // FAS(A = staged query, B = slot p) from the walk's results: the reference's terms in the
 // reference's order.  The candidate's token hits are the hit lists of threads
 // first .. first + nl - 1 (its chunks, in record order); nh_of(g) = hits of thread first + g.
-template <bool PACKED, class Rec, class NH>
+// RAW (packed only): the list holds the hit record words themselves (the pair walk), whose
+// values are probed again here.
+template <bool PACKED, bool RAW = false, class Rec, class NH>
 __device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, const uint4& h0, const uint4& h1,
-                                              const uint4& h2, uint32_t cnt, uint32_t first, uint32_t nl, NH nh_of) {
+                                              const uint4& h2, uint32_t cnt, uint32_t first, uint32_t nl, NH nh_of,
+                                              uint64_t* tep = nullptr) {
+    static_assert(PACKED || !RAW, "raw hit words: packed corpora only");
     using H = HitT<PACKED>;
     const QConst& q = *v.q;
     const uint32_t hstride = blockDim.x;
@@ -244,6 +289,10 @@ __device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, co
             nhg = nh_of(g);
         }
         e = hits[h * hstride + first + g];
+        if constexpr (RAW) {
+            const uint32_t w = (uint32_t)e;
+            e = (w & 0xFF000000u) | (probe_p(v, kTagTok | (w & 0xFFFFFFu)) & 0xFFFFFFu);
+        }
         ++h;
         return true;
     };
@@ -276,6 +325,7 @@ __device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, co
         ++used;
     }
     used += __popcll(common);
+    if (tep) tep[0] = clock64();
     if (!overflow) {
         // One pass in the reference's column order, driven by the HIT columns: the wave's
         // i-th iteration computes every lane's i-th hit column (the only place the
@@ -305,9 +355,12 @@ __device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, co
             common &= common - 1;
             sum += q.sig0_col[c];
         }
+    } else if constexpr (RAW) {
+        sum = text_terms_row(v, reinterpret_cast<const uint4*>(rec.w), rec.n, nc + nf, record_words(h2, true), cmask, sum);
     } else {
         sum = text_terms_slow<PACKED>(v, rec, nc + nf, record_words(h2, PACKED), cmask, sum);
     }
+    if (tep) tep[1] = clock64();
     if (used == 0) return 0.0f;
     // recommender_similarity.cpp:114-123
     const double S = sum / (double)used;
@@ -316,12 +369,80 @@ __device__ __forceinline__ float fas_epilogue(const QView& v, const Rec& rec, co
     return (float)((2.0 * S * F) / (S + F));
 }
 
+// ---------------------------------------------------------------- K1' record walk (packed)
+// A pair-kernel lane walks one candidate's contiguous row-store record against the staged
+// query table.  The probe compares keys only (one 4-B read per cuckoo choice, the value is
+// probed again for the few hits in the epilogue) and every word stores itself, the raw record
+// word, at the lane's next hit slot, which only a token hit advances; so a token word costs
+// its key, hash, two addresses, two reads, two compares and the slot pointer.  Groups of 4
+// steps past every lane's last club / friend word take the token-only step (no set
+// bookkeeping).  A lane past its record loads the padding line (kPadWord never matches, and
+// build_store pads the record's last step with it), so no word needs a mask.
+struct RowWalk {
+    uint32_t cnt;  // clubs intersections (low 16 bits) + friends intersections << 16
+    uint32_t ptr;  // the lane's next hit slot, hit list word index (slot * kPairThreads + lane)
+};
+
+__device__ __forceinline__ bool has_key(const QView& v, uint32_t key, uint32_t x) {
+    const uint32_t k1 = v.tab[cuckoo_h1(x, v.lg)].x;
+    const uint32_t k2 = v.tab[cuckoo_h2(x, v.lg)].x;
+    return (k1 == key) | (k2 == key);
+}
+
+// words j0 .. j0 + 3; SETS: the step may hold club / friend words (j < nset; clubs j < nc)
+template <bool SETS>
+__device__ __forceinline__ void row_step(RowWalk& W, const uint4& cw, uint32_t j0, uint32_t nc, uint32_t nset,
+                                         const QView& v, uint32_t pcap) {
+    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
+    bool hit[4], tok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        tok[i] = !SETS || j0 + i >= nset;
+        const uint32_t key = tok[i] ? (kTagTok | (w[i] & 0xFFFFFFu)) : w[i];
+        hit[i] = has_key(v, key, cuckoo_x(key, v.hmul));
+    }
+    uint32_t* hl = reinterpret_cast<uint32_t*>(v.hits);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (SETS) W.cnt += (hit[i] && !tok[i]) ? (j0 + i < nc ? 1u : 0x10000u) : 0u;
+        hl[W.ptr] = w[i];
+        W.ptr += (hit[i] && tok[i]) ? kPairThreads : 0u;
+    }
+    W.ptr = W.ptr < pcap ? W.ptr : pcap;  // <= 3 writes past pcap per step: the dump slots
+}
+
+__device__ __forceinline__ void walk_row(RowWalk& W, const uint4* base, const uint4* pad, uint32_t len, uint32_t nc,
+                                         uint32_t nset, const QView& v, uint32_t pcap) {
+    const uint32_t steps = (len + 3) >> 2;
+    const uint32_t smax = wave_max_u32(steps);
+    const uint32_t sset = wave_max_u32((nset + 3) >> 2);  // steps holding a set word on some lane
+    auto ld = [&](uint32_t s) { return *(s < steps ? base + s : pad); };
+    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
+    uint32_t s = 0;
+    for (; s < sset; s += 4) {
+        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
+        row_step<true>(W, c0, 4 * s, nc, nset, v, pcap);
+        row_step<true>(W, c1, 4 * s + 4, nc, nset, v, pcap);
+        row_step<true>(W, c2, 4 * s + 8, nc, nset, v, pcap);
+        row_step<true>(W, c3, 4 * s + 12, nc, nset, v, pcap);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    for (; s < smax; s += 4) {
+        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
+        row_step<false>(W, c0, 0, 0, 0, v, pcap);
+        row_step<false>(W, c1, 0, 0, 0, v, pcap);
+        row_step<false>(W, c2, 0, 0, 0, v, pcap);
+        row_step<false>(W, c3, 0, 0, 0, v, pcap);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+}
+
 // FAS of slot p by one lane alone (pairs kernel): the lane walks the slot's record in the row
 // store (contiguous 16-B steps, so the lane's loads consume whole cache lines), its own hit list
 // then holds the whole record's hits in order; the column norms follow the record in the row
 // store, so no tile lookup sits in front of them.
 template <bool PACKED>
-__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active) {
+__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active, uint64_t* twalk = nullptr) {
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
     uint64_t ro = 0;
     if (active) {
@@ -332,14 +453,26 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
     }
     const uint32_t nc = h2.y, nset = h2.y + h2.z;
     const uint32_t len = active ? record_words(h2, PACKED) : 0u;
-    Walk W;
-    W.cnt = 0; W.nh = 0; W.pend = 0;
-    walk_chunk<PACKED, true, 1>(W, st.rows + ro, 0u, len, nc, nset, v, blockDim.x);
-    if (!active) return 0.0f;
-    const uint32_t nh = W.nh;
     const RowRec rec{reinterpret_cast<const uint32_t*>(st.rows + ro),
                      reinterpret_cast<const double*>(st.rows + ro + ((len + 3) >> 2))};
-    return fas_epilogue<PACKED>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+    if constexpr (PACKED) {
+        const uint32_t pcap = kHitCap * kPairThreads + threadIdx.x;
+        RowWalk W{0u, threadIdx.x};
+        walk_row(W, st.rows + ro, st.row_pad, len, nc, active ? nset : 0u, v, pcap);
+        if (twalk) twalk[0] = clock64();
+        if (!active) return 0.0f;
+        // a list that reached kHitCap reads as overflowed (the slow path re-walks the record)
+        const uint32_t nh = W.ptr >= pcap ? kHitCap + 1 : (W.ptr - threadIdx.x) / kPairThreads;
+        return fas_epilogue<true, true>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [nh](uint32_t) { return nh; },
+                                        twalk ? twalk + 1 : nullptr);
+    } else {
+        Walk W;
+        W.cnt = 0; W.nh = 0; W.pend = 0;
+        walk_chunk<false, true, 1>(W, st.rows + ro, 0u, len, nc, nset, v, kPairThreads);
+        if (!active) return 0.0f;
+        const uint32_t nh = W.nh;
+        return fas_epilogue<false>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
+    }
 }
 
 // ---------------------------------------------------------------- LDS staging
@@ -767,6 +900,7 @@ __device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng,
 // profiling build only (make K5T=1): per-phase clock64() sums over every wave, printed by
 // launch_post every 10th launch
 __device__ unsigned long long g_k5t[16];
+__device__ unsigned long long g_k1t[8];  // K1': staging, walk, epilogue, total, fixed, columns, fas, waves
 #define K5T(slot) do { const uint64_t t_ = clock64(); tacc[slot] += t_ - tprev; tprev = t_; } while (0)
 #else
 #define K5T(slot) do { } while (0)
@@ -1097,24 +1231,59 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
 
 // ---------------------------------------------------------------- K1': pairs
 template <bool PACKED, bool GTAB>
-__global__ __launch_bounds__(256) void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
+__global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                         const QImageRef* __restrict__ refs,
                                                         const PairBlock* __restrict__ blocks,
+                                                        const int32_t* __restrict__ order,
                                                         const int32_t* __restrict__ slots, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const PairBlock b = blocks[blockIdx.x];
+#ifdef PF_K5_TIMERS
+    const uint64_t t0 = clock64();
+    uint64_t tw[3] = {0, 0, 0};
+    uint64_t* twp = tw;
+#else
+    uint64_t* twp = nullptr;
+#endif
+    const PairBlock b = blocks[order ? order[blockIdx.x] : (int)blockIdx.x];
+    // a block scores b.count <= kPairThreads pairs against its one staged image; the plan sizes
+    // candidate blocks by the candidate bound, so a block past a job's candidates has none
+    const int i = (int)threadIdx.x;
+    int p = i < b.count ? slots[b.begin + i] : -1;
+    const bool active = p >= 0;
+    if (!__syncthreads_or(active)) return;
     char* scratch;
     const QView v = stage_query<GTAB>(smem, pool, refs[b.qimg], &scratch);
-    // a block scores b.count pairs (a multiple of 256 except the last of a run) against the
-    // one staged image, 256 at a time: wider blocks stage the image fewer times
-    for (int base = 0; base < b.count; base += 256) {
-        const int i = base + (int)threadIdx.x;
-        int p = i < b.count ? slots[b.begin + i] : -1;
-        const bool active = p >= 0;
-        if (!active) p = 0;
-        const float f = fas_slot<PACKED>(st, v, p, active);
-        if (active) out[b.out + i] = f;
+#ifdef PF_K5_TIMERS
+    const uint64_t t1 = clock64();
+#endif
+    if (!active) p = 0;
+    const float f = fas_slot<PACKED>(st, v, p, active, twp);
+    if (active) out[b.out + i] = f;
+#ifdef PF_K5_TIMERS
+    const uint64_t t3 = clock64();
+    // the wave's phase ends: the walk is wave-uniform; the epilogue's phases end at the wave's
+    // last lane (max over the lanes that ran it)
+    uint64_t we = tw[0], fe = active ? tw[1] : 0, he = active ? tw[2] : 0;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = (uint64_t)__shfl_xor((long long)we, o), f2 = (uint64_t)__shfl_xor((long long)fe, o),
+                       h2 = (uint64_t)__shfl_xor((long long)he, o);
+        we = a > we ? a : we;
+        fe = f2 > fe ? f2 : fe;
+        he = h2 > he ? h2 : he;
     }
+    if (fe == 0) fe = we;
+    if (he == 0) he = fe;
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_k1t[0], (unsigned long long)(t1 - t0));
+        atomicAdd(&g_k1t[1], (unsigned long long)(we - t1));
+        atomicAdd(&g_k1t[2], (unsigned long long)(t3 - we));
+        atomicAdd(&g_k1t[3], (unsigned long long)(t3 - t0));
+        atomicAdd(&g_k1t[4], (unsigned long long)(fe - we));
+        atomicAdd(&g_k1t[5], (unsigned long long)(he - fe));
+        atomicAdd(&g_k1t[6], (unsigned long long)(t3 - he));
+        atomicAdd(&g_k1t[7], 1ull);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- K4: collaborative sum
@@ -1221,14 +1390,30 @@ hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int
 }
 
 hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
-                        bool gtab, const PairBlock* blocks, int nblocks, const int32_t* slots, float* out,
-                        hipStream_t s) {
+                        bool gtab, const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
+                        float* out, hipStream_t s) {
     if (nblocks <= 0) return hipSuccess;
-#define PF_PAIRS(P, G) hipLaunchKernelGGL((fas_pairs_kernel<P, G>), dim3(nblocks), dim3(256), max_lds, s, st, pool, \
-                                          refs_dev, blocks, slots, out)
+#define PF_PAIRS(P, G) hipLaunchKernelGGL((fas_pairs_kernel<P, G>), dim3(nblocks), dim3(kPairThreads), max_lds, s, st, pool, \
+                                          refs_dev, blocks, order, slots, out)
     if (st.packed) { if (gtab) PF_PAIRS(true, true); else PF_PAIRS(true, false); }
     else { if (gtab) PF_PAIRS(false, true); else PF_PAIRS(false, false); }
 #undef PF_PAIRS
+#ifdef PF_K5_TIMERS
+    {
+        static int calls = 0;
+        unsigned long long t[8];
+        hipStreamSynchronize(s);
+        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k1t), sizeof(t));
+        if (++calls % 10 == 0 && t[7])
+            fprintf(stderr,
+                    "k1pt per wave (clock64): staging=%.0f walk=%.0f epilogue=%.0f (fixed=%.0f columns=%.0f fas=%.0f) "
+                    "total=%.0f waves=%llu blocks=%d\n",
+                    (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[4] / t[7],
+                    (double)t[5] / t[7], (double)t[6] / t[7], (double)t[3] / t[7], t[7], nblocks);
+        const unsigned long long z[8] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_k1t), z, sizeof(z));
+    }
+#endif
     return hipGetLastError();
 }
 

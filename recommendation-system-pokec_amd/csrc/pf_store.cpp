@@ -34,6 +34,17 @@ void par_for(int64_t n, F f) {
 }
 
 
+// true when pred(k) holds for some k in [0, n), on the par_for threads
+template <class P>
+bool par_any(int64_t n, P pred) {
+    std::atomic<bool> hit{false};
+    par_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi && !hit.load(std::memory_order_relaxed); ++k)
+            if (pred(k)) { hit = true; break; }
+    });
+    return hit;
+}
+
 }  // namespace
 
 // recommender_similarity.cpp:18-26 (stable two-branch logistic, double)
@@ -77,10 +88,12 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
     }
     hc.n = n;
     hc.T = T;
+    StageClock sc;
     // candidate index = rank of uid (ascending)
     std::vector<int32_t> order(n);
     std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(), [&](int a, int b) { return d->user_id[a] < d->user_id[b]; });
+    if (par_any(n > 0 ? n - 1 : 0, [&](int64_t i) { return d->user_id[i + 1] < d->user_id[i]; }))  // loaders hand uid order
+        std::sort(order.begin(), order.end(), [&](int a, int b) { return d->user_id[a] < d->user_id[b]; });
     for (int i = 1; i < n; ++i)
         if (d->user_id[order[i]] == d->user_id[order[i - 1]]) { err = "duplicate user id"; return PF_EINVAL; }
     hc.uid.resize(n); hc.pub.resize(n); hc.comp.resize(n); hc.gen.resize(n); hc.age.resize(n);
@@ -98,6 +111,7 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
             hc.tok_off[(size_t)i * T + t + 1] = hc.tok_off[(size_t)i * T + t] + (d->tok_off[r + 1] - d->tok_off[r]);
         }
     }
+    sc.lap("uid order + offsets");
     hc.clubs.resize(hc.club_off[n]); hc.friends.resize(hc.friend_off[n]);
     hc.tid.resize(hc.tok_off[(size_t)n * T]); hc.tf.resize(hc.tok_off[(size_t)n * T]);
     par_for(n, [&](int64_t lo, int64_t hi) {
@@ -118,10 +132,17 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
             }
         }
     });
-    for (int64_t r = 0; r < (int64_t)n * T; ++r)
-        for (int64_t k = hc.tok_off[r] + 1; k < hc.tok_off[r + 1]; ++k)
-            if (hc.tid[k] == hc.tid[k - 1]) { err = "duplicate token id within a (user, column) row"; return PF_EINVAL; }
+    sc.lap("rows copied + sorted");
+    if (par_any((int64_t)n * T, [&](int64_t r) {
+            for (int64_t k = hc.tok_off[r] + 1; k < hc.tok_off[r + 1]; ++k)
+                if (hc.tid[k] == hc.tid[k - 1]) return true;
+            return false;
+        })) {
+        err = "duplicate token id within a (user, column) row";
+        return PF_EINVAL;
+    }
 
+    sc.lap("duplicate-token check");
     // ---- IDF ------------------------------------------------------------
     hc.idf.assign(T, {});
     hc.idf_explicit.assign(T, {});
@@ -137,6 +158,7 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
     // sqrt(sum (tf*idf)^2) per (user, col) row: on the device (F3, pf_idf.hip)
     const int rc = device_idf_norms(hc, d->idf_mode != PF_IDF_EXPLICIT, err);
     if (rc != PF_OK) return rc;
+    sc.lap("device ranks / idf / norms");
     // ---- normalisers -----------------------------------------------------
     const int K = kNumFixed + T;
     hc.npres.assign(K, 0); hc.nmean.assign(K, 0.f); hc.nsd.assign(K, 0.f);
@@ -163,6 +185,7 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
         auto& row = hc.adj[d->adj_uid[a]];
         row.insert(row.end(), d->adj_nbr + d->adj_off[a], d->adj_nbr + d->adj_off[a + 1]);
     }
+    sc.lap("codes + adjacency map");
     return PF_OK;
 }
 
@@ -173,16 +196,19 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     // and club / friend ids below 2^30 (bits 30-31 are the kind tags)
     bool packed = true;
     for (int t = 0; t < T && packed; ++t) packed = (uint32_t)hc.n_ranks(t) < kTidMask;
-    for (size_t k = 0; k < hc.tf.size() && packed; ++k) packed = hc.tf[k] >= 0 && hc.tf[k] <= 255;
-    for (size_t k = 0; k < hc.clubs.size() && packed; ++k) packed = hc.clubs[k] < kIdLimit;
-    for (size_t k = 0; k < hc.friends.size() && packed; ++k) packed = hc.friends[k] < kIdLimit;
+    packed = packed && !par_any((int64_t)hc.tf.size(), [&](int64_t k) { return hc.tf[k] < 0 || hc.tf[k] > 255; });
+    packed = packed && !par_any((int64_t)hc.clubs.size(), [&](int64_t k) { return hc.clubs[k] >= kIdLimit; });
+    packed = packed && !par_any((int64_t)hc.friends.size(), [&](int64_t k) { return hc.friends[k] >= kIdLimit; });
     if (!packed) {
         for (int t = 0; t < T; ++t)
             if ((uint32_t)hc.n_ranks(t) > kWideTidMask + 1u) { err = "more than 2^26 distinct token ids in a column"; return PF_EUNSUPP; }
-        for (size_t k = 0; k < hc.tf.size(); ++k)
-            if (hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23)) { err = "token count outside [-2^23, 2^23)"; return PF_EUNSUPP; }
+        if (par_any((int64_t)hc.tf.size(), [&](int64_t k) { return hc.tf[k] < -(1 << 23) || hc.tf[k] >= (1 << 23); })) {
+            err = "token count outside [-2^23, 2^23)";
+            return PF_EUNSUPP;
+        }
     }
     hs.packed = packed;
+    StageClock sc;
     // record length in words: clubs, friends, tokens
     std::vector<uint32_t> len(n), ncols(n);
     int64_t alg = 0;
@@ -201,6 +227,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
         alg += 32 + 4 * nc + 4 * nf + 8 * nt;
     }
     hs.alg_bytes = alg;
+    sc.lap("record lengths");
     // slots: longest records first, so the 64 records of a tile have near-equal length
     hs.idx_of_slot.resize(n);
     std::iota(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), 0);
@@ -236,6 +263,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
         noff += (uint64_t)mr * kTileSlots;
         s0 += cnt;
     }
+    sc.lap("slot order + tiles");
     // + one group of padding steps past the end: the scan's walk prefetches the group
     // after a tile's last one (never used), and a lane with an empty chunk still loads
     hs.norm_off.push_back(noff);  // sentinel: a tile's rank count = (norm_off[t+1] - norm_off[t]) / 64
@@ -252,6 +280,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     hs.rows.assign(hs.row_off[n] + 1, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     hs.norms.assign(noff, 0.0);
     hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
+    sc.lap("stream / rows / norms allocated");
     par_for(n, [&](int64_t lo, int64_t hi) {
         std::vector<uint32_t> w;
         for (int64_t p = lo; p < hi; ++p) {
@@ -309,6 +338,7 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
                                     (uint32_t)nc, (uint32_t)nf, (uint32_t)nt);
         }
     });
+    sc.lap("records written");
     return PF_OK;
 }
 
@@ -377,7 +407,7 @@ void qconst_template(const HostCorpus& hc, bool packed, QConst& c) {
     c.sig0_clubs = term(hc, PF_F_CLUBS, 0.0);
     c.sig0_friends = term(hc, PF_F_FRIENDS, 0.0);
     for (int t = 0; t < T; ++t) c.sig0_col[t] = term(hc, kNumFixed + t, 0.0);
-    c.n_hits_max = (kHitCap + 1) * (packed ? 4u : 8u);  // + the dump slot
+    c.n_hits_max = kHitSlots * (packed ? 4u : 8u);  // + the dump slots
 }
 
 void qconst_sig_reg(const HostCorpus& hc, int a_regcnt, double out[4][4]) {
@@ -535,6 +565,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
         hp.club_list.clear(); hp.friend_list.clear();
     };
     if (n <= 0) return bail("empty corpus");
+    StageClock sc;
     if ((uint32_t)n >= kPostIdxLimit) return bail("more than 2^24 candidates");
     if (T > kPostMaxCols) return bail("more than 48 text columns");
     for (int32_t i = 0; i < n; ++i) {
@@ -545,8 +576,8 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     }
     for (int t = 0; t < T; ++t)
         if (hc.n_ranks(t) >= (1 << 22)) return bail("more than 2^22 distinct token ids in a column");
-    for (size_t k = 0; k < hc.tf.size(); ++k)
-        if (hc.tf[k] < 0 || hc.tf[k] > 255) return bail("token count outside the packed encoding");
+    if (par_any((int64_t)hc.tf.size(), [&](int64_t k) { return hc.tf[k] < 0 || hc.tf[k] > 255; }))
+        return bail("token count outside the packed encoding");
     // ---- token lists: (column, tid rank) ascending; entries idx << 8 | tf, tf > 0 only (a tf = 0
     // token adds +0 to a dot and never decides a hit: recommender.cpp:74-85)
     hp.tok_list.assign(T, {});
@@ -562,6 +593,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
             });
         for (auto& x : ts) x.join();
     }
+    sc.lap("checks + token counts");
     uint64_t off = 0;
     std::vector<uint64_t> col_off(T + 1, 0);
     for (int t = 0; t < T; ++t) {
@@ -613,8 +645,10 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     };
     if (!collect(hc.club_off, hc.clubs, ckeys) || !collect(hc.friend_off, hc.friends, fkeys))
         return bail("a club / friend id repeats more than 255 times in one profile");
+    sc.lap("token lists + set keys");
     radix_sort_u64(ckeys, 64);
     radix_sort_u64(fkeys, 64);
+    sc.lap("set keys sorted");
     const uint64_t set_off = off;
     if (off + ckeys.size() + fkeys.size() >= (1ull << 32)) return bail("more than 2^32 postings");
     hp.post.resize(off + ckeys.size() + fkeys.size());
@@ -635,6 +669,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     add_sets(ckeys, hp.club_list);
     add_sets(fkeys, hp.friend_list);
     (void)set_off;
+    sc.lap("set lists");
     // ---- token entries and their norms, per column in idx order (lists come out sorted)
     hp.pnorm.resize(hp.tok_entries);
     {
@@ -656,6 +691,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
             });
         for (auto& x : ts) x.join();
     }
+    sc.lap("token entries");
     // ---- cells
     uint64_t coff = 0;
     for (auto& L : hp.lists) {
@@ -677,6 +713,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
             }
         }
     });
+    sc.lap("cells");
     // ---- headers
     hp.hdr.resize(2 * (size_t)n);
     par_for(n, [&](int64_t lo, int64_t hi) {
@@ -694,6 +731,7 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
                                            (uint32_t)hc.reg[3 * i + 2], (uint32_t)hc.uid[i]);
         }
     });
+    sc.lap("headers");
     hp.ok = true;
 }
 

@@ -17,6 +17,7 @@ constexpr int kValTab = 128;        // completion/age sigmoid tables cover value
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
 constexpr uint32_t kHitCap = 16;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
+constexpr uint32_t kHitSlots = kHitCap + 4;  // + dump slots: the pair walk clamps its list once per 4-word step
 constexpr int kMaxHashLog2 = 16;    // cuckoo tables <= 65536 slots (h1/h2 from one 32-bit product)
 constexpr uint32_t kMaxTileSteps = 48;  // a record longer than 48 steps (192 words) is split over lanes
 
@@ -168,6 +169,7 @@ struct DevStore {
     const uint4* rows;         // row store: slot p's record contiguous from rows[row_off[p]], padded to 16 B,
                                // then its column norms (double per non-empty column, ascending) (pair kernel)
     const uint64_t* row_off;   // [n_slots + 1]
+    const uint4* row_pad;      // one 16-B line of kPadWord (a pair-kernel lane past its record reads it)
     int32_t n_slots;
     int32_t n_tiles;
     int32_t packed;

@@ -257,8 +257,9 @@ inline void par_jobs(size_t n, F f, size_t grain = 4) {
 // otherwise run between the timed kernels and perturb them (r2fe: 1.6 us of kernel time).
 inline hipError_t timing_event(hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableSystemFence); }
 
-template <class T>
-inline hipError_t upload(pf_ctx* c, DBuf& b, const std::vector<T>& v) {
+template <class V>  // std::vector or PodVec
+inline hipError_t upload(pf_ctx* c, DBuf& b, const V& v) {
+    using T = typename V::value_type;
     hipError_t e = b.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
     if (e != hipSuccess) return e;
     if (v.empty()) return hipSuccess;

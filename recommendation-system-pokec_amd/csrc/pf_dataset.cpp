@@ -17,6 +17,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <memory>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -120,6 +122,11 @@ struct pf_dataset {
     std::vector<uint8_t> npres;
     std::vector<float> nmean, nsd;
     pf_corpus_desc desc{};
+    // the hold-out drivers' sampled plans: a pure function of the loaded maps and the sample
+    // size (test.cpp:13-60, recommendation_tests.cpp:68-100 sampling), so built once per
+    // (driver, size) and shared by every later call and engine context
+    mutable std::mutex plan_mu;
+    mutable std::unordered_map<int64_t, std::shared_ptr<const void>> plans;
 };
 
 namespace {
@@ -1145,6 +1152,16 @@ struct PlanEntry {
     std::unordered_set<int> held;
 };
 
+using Plan = std::vector<PlanEntry>;
+
+template <class F>
+std::shared_ptr<const Plan> cached_plan(const pf_dataset* ds, int driver, int32_t sample_size, F build) {
+    std::lock_guard<std::mutex> g(ds->plan_mu);
+    auto& slot = ds->plans[((int64_t)driver << 32) | (uint32_t)sample_size];
+    if (!slot) slot = std::make_shared<const Plan>(build());
+    return std::static_pointer_cast<const Plan>(slot);
+}
+
 // test.cpp:13-60 (candidates with >= 20 friends, shuffled; hold F/5 per user)
 std::vector<PlanEntry> plan_friends(const pf_dataset* ds, int32_t sample_size) {
     std::vector<PlanEntry> plan;
@@ -1235,7 +1252,8 @@ int eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size,
         return PF_EINVAL;
     pf::HpLap hl;
     ViewScope scope(ctx);
-    const std::vector<PlanEntry> plan = plan_friends(ds, sample_size);
+    const auto planp = cached_plan(ds, 0, sample_size, [&]() { return plan_friends(ds, sample_size); });
+    const Plan& plan = *planp;
     hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
     // one adj_mod for the whole run (test.cpp:35,73): user i sees the rows of users 0..i edited
@@ -1281,7 +1299,8 @@ int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_
         return PF_EINVAL;
     pf::HpLap hl;
     ViewScope scope(ctx);
-    const std::vector<PlanEntry> plan = plan_rec(ds, sample_size);
+    const auto planp = cached_plan(ds, 1, sample_size, [&]() { return plan_rec(ds, sample_size); });
+    const Plan& plan = *planp;
     hl.lap(pf::kHpPlan);
     *n_plan = (int32_t)plan.size();
     const auto& base = pf::base_adj(ctx);

@@ -119,7 +119,7 @@ int device_idf_norms(HostCorpus& hc, bool from_profiles, std::string& err) {
     const int64_t rows = (int64_t)hc.n * hc.T;
     const int64_t nt = hc.tok_off.empty() ? 0 : hc.tok_off.back();
     const int T = hc.T;
-    hc.sqrt_nb.assign((size_t)rows, 0.0);
+    hc.sqrt_nb.resize_uninit((size_t)rows);  // the device writes every row
     if (rows == 0) return PF_OK;
     if (nt > (int64_t)INT32_MAX) { err = "more than 2^31 tokens"; return PF_EUNSUPP; }
     hipStream_t s = nullptr;

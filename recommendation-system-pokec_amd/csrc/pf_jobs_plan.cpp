@@ -126,15 +126,26 @@ int jobs_open(pf_ctx* c) {
     rows.reserve(hc.adj.size());
     for (auto& kv : hc.adj) rows.push_back(&kv);
     {
+        // uid -> profile idx: a dense table when the uids are non-negative and not too sparse
+        // (hc.uid is ascending), else bisection
+        std::vector<int32_t> dense_idx;
+        if (n > 0 && hc.uid.front() >= 0 && (int64_t)hc.uid.back() < 4 * (int64_t)n + 4096) {
+            dense_idx.assign((size_t)hc.uid.back() + 1, -1);
+            par_jobs((size_t)n, [&](size_t i) { dense_idx[hc.uid[i]] = (int32_t)i; }, 1 << 16);
+        }
+        auto profile = [&](int32_t u) -> bool {
+            if (dense_idx.empty()) return hc.idx_of(u) >= 0;
+            return u >= 0 && (size_t)u < dense_idx.size() && dense_idx[u] >= 0;
+        };
         std::vector<std::vector<int32_t>> unknown(16);
         const size_t R = rows.size();
         std::vector<std::thread> ts;
         for (int w = 0; w < 16; ++w)
             ts.emplace_back([&, w]() {
                 for (size_t r = w; r < R; r += 16) {
-                    if (hc.idx_of(rows[r]->first) < 0) unknown[w].push_back(rows[r]->first);
+                    if (!profile(rows[r]->first)) unknown[w].push_back(rows[r]->first);
                     for (int32_t x : rows[r]->second)
-                        if (hc.idx_of(x) < 0) unknown[w].push_back(x);
+                        if (!profile(x)) unknown[w].push_back(x);
                 }
             });
         for (auto& t : ts) t.join();
@@ -179,9 +190,23 @@ int jobs_open(pf_ctx* c) {
     }
     sc.lap("graph CSR");
     // clubs as dense indices (K7), per profile idx in profile order
-    std::vector<int32_t> club_id(hc.clubs.begin(), hc.clubs.end());
-    std::sort(club_id.begin(), club_id.end());
-    club_id.erase(std::unique(club_id.begin(), club_id.end()), club_id.end());
+    std::vector<int32_t> club_id;
+    {  // the distinct club ids: each thread's chunk sorted and de-duplicated, then the (short) union
+        const size_t N = hc.clubs.size(), th = 16, ch = (N + th - 1) / th;
+        std::vector<std::vector<int32_t>> part(th);
+        std::vector<std::thread> ts;
+        for (size_t w = 0; w < th; ++w)
+            ts.emplace_back([&, w]() {
+                const size_t lo = std::min(N, w * ch), hi = std::min(N, lo + ch);
+                part[w].assign(hc.clubs.begin() + lo, hc.clubs.begin() + hi);
+                std::sort(part[w].begin(), part[w].end());
+                part[w].erase(std::unique(part[w].begin(), part[w].end()), part[w].end());
+            });
+        for (auto& t : ts) t.join();
+        for (auto& p : part) club_id.insert(club_id.end(), p.begin(), p.end());
+        std::sort(club_id.begin(), club_id.end());
+        club_id.erase(std::unique(club_id.begin(), club_id.end()), club_id.end());
+    }
     std::vector<int32_t> club_dense(hc.clubs.size());
     par_jobs(hc.clubs.size(), [&](size_t k) {
         club_dense[k] = (int32_t)(std::lower_bound(club_id.begin(), club_id.end(), (int32_t)hc.clubs[k]) - club_id.begin());
@@ -256,6 +281,7 @@ int jobs_open(pf_ctx* c) {
     J.view_over_n = 0;
     J.nodes_dirty = false;
     J.ok = true;
+    sc.lap("handles");
     return PF_OK;
 }
 

@@ -482,6 +482,27 @@ __device__ __forceinline__ void stage(void* dst, const void* src, uint32_t bytes
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
 }
 
+// The same with every thread's loads of a round (4 per thread) issued before its stores, so a
+// round costs one memory round trip (the pair kernel stages a 5-20 KB image per block)
+__device__ __forceinline__ void stage4(void* dst, const void* src, uint32_t bytes) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    const uint32_t n = bytes / 16;
+    for (uint32_t base = 0; base < n; base += 4 * blockDim.x) {
+        uint4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            if (i < n) r[u] = s[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            if (i < n) d[i] = r[u];
+        }
+    }
+}
+
 // LDS carve: [QConst][tables][vals][hit lists kHitCap x blockDim][merge scratch 2 KiB].
 // GTAB = false: the cuckoo table and the token values are staged in LDS, so every probe
 // is a ds_read (pointer provenance is the LDS symbol only, never merged with a global
@@ -489,7 +510,21 @@ __device__ __forceinline__ void stage(void* dst, const void* src, uint32_t bytes
 // HBM prefetch).  GTAB = true (query too large for LDS): probes read global memory.
 template <bool GTAB>
 __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, const QImageRef& r, char** scratch) {
-    stage(smem, pool + r.const_off, sizeof(QConst));
+    if constexpr (!GTAB) {
+        // the sizes from the image in global memory; QConst | tables | values are contiguous in
+        // every image pool (tables of >= 2^4 8-B entries keep the values 16-B aligned)
+        const QConst* g = reinterpret_cast<const QConst*>(pool + r.const_off);
+        const uint32_t kb = 8u * (g->excl_off + (1u << g->lg_excl)), vb = (uint32_t)g->n_vals * 16u;
+        if (r.keys_off == r.const_off + sizeof(QConst) && r.vals_off == r.keys_off + kb) {
+            stage4(smem, g, (uint32_t)sizeof(QConst) + kb + vb);
+        } else {
+            stage4(smem, g, sizeof(QConst));
+            stage4(smem + sizeof(QConst), pool + r.keys_off, kb);
+            stage4(smem + sizeof(QConst) + kb, pool + r.vals_off, vb);
+        }
+    } else {
+        stage(smem, pool + r.const_off, sizeof(QConst));
+    }
     __syncthreads();
     const QConst* q = reinterpret_cast<const QConst*>(smem);
     QView v;
@@ -501,8 +536,6 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     const uint32_t kb = 8u * (q->excl_off + (1u << q->lg_excl)), vb = (uint32_t)q->n_vals * 16u;
     char* p = smem + sizeof(QConst);
     if constexpr (!GTAB) {
-        stage(p, pool + r.keys_off, kb);
-        stage(p + kb, pool + r.vals_off, vb);
         v.tab = reinterpret_cast<const uint2*>(p);
         v.vals = reinterpret_cast<const QVal*>(p + kb);
         p += kb + vb;
@@ -515,7 +548,6 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     v.nh = reinterpret_cast<uint32_t*>(p);     // per-thread hit counts (split records)
     p += 4u * blockDim.x;
     *scratch = p;
-    __syncthreads();
     return v;
 }
 

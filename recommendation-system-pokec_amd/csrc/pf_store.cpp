@@ -34,6 +34,62 @@ void par_for(int64_t n, F f) {
 }
 
 
+// f(lo, hi) over [0, n) in chunks handed out dynamically (uneven work per item)
+template <class F>
+void par_dyn(int64_t n, int64_t chunk, F f) {
+    const int th = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int64_t lo = next.fetch_add(chunk);
+            if (lo >= n) return;
+            f(lo, std::min(n, lo + chunk));
+        }
+    };
+    std::vector<std::thread> ts;
+    for (int w = 1; w < th; ++w) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+}
+
+// v[k] = x for every k, on the par_for threads (the first touch of freshly mapped pages)
+template <class V, class X>
+void par_fill(V& v, const X& x) {
+    auto* p = v.data();
+    par_for((int64_t)v.size(), [&](int64_t lo, int64_t hi) { std::fill(p + lo, p + hi, x); });
+}
+
+// a[0] = 0 and a[k] = the length of item k - 1 (k >= 1) -> a[k] = the offset of item k, on threads
+template <class V>
+void par_offsets(V& a) {
+    const int64_t n = (int64_t)a.size();
+    const int th = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < (1 << 16) || th <= 1) {
+        for (int64_t k = 1; k < n; ++k) a[k] += a[k - 1];
+        return;
+    }
+    const int64_t chunk = (n + th - 1) / th;
+    std::vector<int64_t> part(th + 1, 0);
+    std::vector<std::thread> ts;
+    for (int w = 0; w < th; ++w)
+        ts.emplace_back([&, w]() {
+            const int64_t lo = w * chunk, hi = std::min(n, lo + chunk);
+            int64_t s = 0;
+            for (int64_t k = lo; k < hi; ++k) s += a[k];
+            part[w + 1] = s;
+        });
+    for (auto& t : ts) t.join();
+    ts.clear();
+    for (int w = 0; w < th; ++w) part[w + 1] += part[w];
+    for (int w = 0; w < th; ++w)
+        ts.emplace_back([&, w]() {
+            const int64_t lo = w * chunk, hi = std::min(n, lo + chunk);
+            int64_t s = part[w];
+            for (int64_t k = lo; k < hi; ++k) { s += a[k]; a[k] = s; }
+        });
+    for (auto& t : ts) t.join();
+}
+
 // true when pred(k) holds for some k in [0, n), on the par_for threads
 template <class P>
 bool par_any(int64_t n, P pred) {
@@ -98,22 +154,29 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
         if (d->user_id[order[i]] == d->user_id[order[i - 1]]) { err = "duplicate user id"; return PF_EINVAL; }
     hc.uid.resize(n); hc.pub.resize(n); hc.comp.resize(n); hc.gen.resize(n); hc.age.resize(n);
     hc.reg.resize(3 * (size_t)n);
-    hc.club_off.assign(n + 1, 0); hc.friend_off.assign(n + 1, 0); hc.tok_off.assign((size_t)n * T + 1, 0);
-    for (int i = 0; i < n; ++i) {
-        int s = order[i];
-        hc.uid[i] = d->user_id[s]; hc.pub[i] = d->public_flag[s]; hc.comp[i] = d->completion[s];
-        hc.gen[i] = d->gender[s]; hc.age[i] = d->age[s];
-        for (int k = 0; k < 3; ++k) hc.reg[3 * (size_t)i + k] = d->region[3 * (size_t)s + k];
-        hc.club_off[i + 1] = hc.club_off[i] + (d->club_off[s + 1] - d->club_off[s]);
-        hc.friend_off[i + 1] = hc.friend_off[i] + (d->friend_off[s + 1] - d->friend_off[s]);
-        for (int t = 0; t < T; ++t) {
-            int64_t r = (int64_t)s * T + t;
-            hc.tok_off[(size_t)i * T + t + 1] = hc.tok_off[(size_t)i * T + t] + (d->tok_off[r + 1] - d->tok_off[r]);
+    hc.club_off.assign(n + 1, 0); hc.friend_off.assign(n + 1, 0);
+    hc.tok_off.resize_uninit((size_t)n * T + 1);  // every entry is written below
+    hc.tok_off[0] = 0;
+    par_for(n, [&](int64_t lo, int64_t hi) {  // fields and lengths, then the offsets
+        for (int64_t i = lo; i < hi; ++i) {
+            const int s = order[i];
+            hc.uid[i] = d->user_id[s]; hc.pub[i] = d->public_flag[s]; hc.comp[i] = d->completion[s];
+            hc.gen[i] = d->gender[s]; hc.age[i] = d->age[s];
+            for (int k = 0; k < 3; ++k) hc.reg[3 * (size_t)i + k] = d->region[3 * (size_t)s + k];
+            hc.club_off[i + 1] = d->club_off[s + 1] - d->club_off[s];
+            hc.friend_off[i + 1] = d->friend_off[s + 1] - d->friend_off[s];
+            for (int t = 0; t < T; ++t) {
+                const int64_t r = (int64_t)s * T + t;
+                hc.tok_off[(size_t)i * T + t + 1] = d->tok_off[r + 1] - d->tok_off[r];
+            }
         }
-    }
+    });
+    par_offsets(hc.club_off);
+    par_offsets(hc.friend_off);
+    par_offsets(hc.tok_off);
     sc.lap("uid order + offsets");
     hc.clubs.resize(hc.club_off[n]); hc.friends.resize(hc.friend_off[n]);
-    hc.tid.resize(hc.tok_off[(size_t)n * T]); hc.tf.resize(hc.tok_off[(size_t)n * T]);
+    hc.tid.resize_uninit(hc.tok_off[(size_t)n * T]); hc.tf.resize_uninit(hc.tok_off[(size_t)n * T]);
     par_for(n, [&](int64_t lo, int64_t hi) {
         std::vector<std::pair<int32_t, int32_t>> row;
         for (int64_t i = lo; i < hi; ++i) {
@@ -122,13 +185,22 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
                 std::memcpy(&hc.clubs[hc.club_off[i]], d->club_ids + d->club_off[s], sizeof(uint32_t) * (hc.club_off[i + 1] - hc.club_off[i]));
             if (hc.friend_off[i + 1] > hc.friend_off[i])
                 std::memcpy(&hc.friends[hc.friend_off[i]], d->friend_ids + d->friend_off[s], sizeof(uint32_t) * (hc.friend_off[i + 1] - hc.friend_off[i]));
+            // the user's rows are contiguous in both: one copy, then each (short) row sorted by tid
+            const int64_t r0 = (int64_t)s * T, o0 = hc.tok_off[(size_t)i * T];
+            const int64_t len = d->tok_off[r0 + T] - d->tok_off[r0];
+            if (len > 0) {
+                std::memcpy(&hc.tid[o0], d->tok_tid + d->tok_off[r0], sizeof(int32_t) * len);
+                std::memcpy(&hc.tf[o0], d->tok_tf + d->tok_off[r0], sizeof(int32_t) * len);
+            }
             for (int t = 0; t < T; ++t) {
-                int64_t r = (int64_t)s * T + t;
+                const int64_t a = hc.tok_off[(size_t)i * T + t], b = hc.tok_off[(size_t)i * T + t + 1];
+                bool sorted = true;
+                for (int64_t k = a + 1; k < b && sorted; ++k) sorted = hc.tid[k - 1] <= hc.tid[k];
+                if (sorted) continue;
                 row.clear();
-                for (int64_t k = d->tok_off[r]; k < d->tok_off[r + 1]; ++k) row.emplace_back(d->tok_tid[k], d->tok_tf[k]);
+                for (int64_t k = a; k < b; ++k) row.emplace_back(hc.tid[k], hc.tf[k]);
                 std::sort(row.begin(), row.end());
-                int64_t o = hc.tok_off[(size_t)i * T + t];
-                for (size_t k = 0; k < row.size(); ++k) { hc.tid[o + k] = row[k].first; hc.tf[o + k] = row[k].second; }
+                for (int64_t k = a; k < b; ++k) { hc.tid[k] = row[k - a].first; hc.tf[k] = row[k - a].second; }
             }
         }
     });
@@ -181,6 +253,7 @@ int build_host_corpus(const pf_corpus_desc* d, HostCorpus& hc, std::string& err)
     // ---- adjacency ---------------------------------------------------------
     hc.adj.clear();
     if (d->n_adj > 0 && (!d->adj_uid || !d->adj_off || !d->adj_nbr)) { err = "missing adjacency arrays"; return PF_EINVAL; }
+    hc.adj.reserve((size_t)d->n_adj);
     for (int a = 0; a < d->n_adj; ++a) {
         auto& row = hc.adj[d->adj_uid[a]];
         row.insert(row.end(), d->adj_nbr + d->adj_off[a], d->adj_nbr + d->adj_off[a + 1]);
@@ -229,9 +302,16 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     hs.alg_bytes = alg;
     sc.lap("record lengths");
     // slots: longest records first, so the 64 records of a tile have near-equal length
+    // (a stable counting sort by length, longest first: ties keep idx order)
     hs.idx_of_slot.resize(n);
-    std::iota(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), 0);
-    std::stable_sort(hs.idx_of_slot.begin(), hs.idx_of_slot.end(), [&](int a, int b) { return len[a] > len[b]; });
+    {
+        uint32_t mx = 0;
+        for (int i = 0; i < n; ++i) mx = std::max(mx, len[i]);
+        std::vector<int32_t> start((size_t)mx + 2, 0);
+        for (int i = 0; i < n; ++i) ++start[mx - len[i] + 1];
+        for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
+        for (int i = 0; i < n; ++i) hs.idx_of_slot[start[mx - len[i]]++] = i;
+    }
     hs.slot_of_idx.resize(n);
     for (int p = 0; p < n; ++p) hs.slot_of_idx[hs.idx_of_slot[p]] = p;
     // tiles: take the next 64 >> lgk slots, lgk the smallest split that keeps the tile's
@@ -267,7 +347,8 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
     // + one group of padding steps past the end: the scan's walk prefetches the group
     // after a tile's last one (never used), and a lane with an empty chunk still loads
     hs.norm_off.push_back(noff);  // sentinel: a tile's rank count = (norm_off[t+1] - norm_off[t]) / 64
-    hs.stream.assign(off + 4 * kTileSlots, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
+    hs.stream.resize_uninit(off + 4 * kTileSlots);
+    par_fill(hs.stream, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
     // row store (the pair kernel K1'): each slot's record contiguous, padded to 16 B, so a lane
     // walking one candidate reads whole cache lines (the tile stream strides a record by 1 KiB),
     // then the slot's column norms (one double per non-empty column, 16-B padded): the epilogue
@@ -277,8 +358,10 @@ int build_store(const HostCorpus& hc, HostStore& hs, std::string& err) {
         const int i = hs.idx_of_slot[p];
         hs.row_off[p + 1] = hs.row_off[p] + (len[i] + 3) / 4 + (ncols[i] + 1) / 2;
     }
-    hs.rows.assign(hs.row_off[n] + 1, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
-    hs.norms.assign(noff, 0.0);
+    hs.rows.resize_uninit(hs.row_off[n] + 1);
+    par_fill(hs.rows, make_uint4(kPadWord, kPadWord, kPadWord, kPadWord));
+    hs.norms.resize_uninit(noff);
+    par_fill(hs.norms, 0.0);
     hs.hdr0.resize(n); hs.hdr1.resize(n); hs.hdr2.resize(n);
     sc.lap("stream / rows / norms allocated");
     par_for(n, [&](int64_t lo, int64_t hi) {
@@ -531,14 +614,43 @@ namespace pf {
 
 namespace {
 
-// LSD radix sort of 64-bit keys on their low `bits` bits (16-bit digits)
-void radix_sort_u64(std::vector<uint64_t>& a, int bits) {
-    std::vector<uint64_t> b(a.size());
-    for (int sh = 0; sh < bits; sh += 16) {
-        std::vector<size_t> cnt(65537, 0);
-        for (uint64_t x : a) ++cnt[((x >> sh) & 0xFFFF) + 1];
-        for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
-        for (uint64_t x : a) b[cnt[(x >> sh) & 0xFFFF]++] = x;
+constexpr int kBuildThreads = 16;  // host threads of the postings build
+
+// Stable LSD radix sort of 64-bit keys on bits [lo_bit, 64) (16-bit digits), each pass on
+// kBuildThreads threads: per-thread digit counts of its chunk, the global digit x thread prefix,
+// then every thread scatters its chunk in order.
+void par_radix_sort_u64(std::vector<uint64_t>& a, int lo_bit) {
+    const size_t n = a.size();
+    if (n == 0) return;
+    std::vector<uint64_t> b(n);
+    const int th = kBuildThreads;
+    const size_t chunk = (n + th - 1) / th;
+    std::vector<std::vector<size_t>> cnt(th, std::vector<size_t>(65536));
+    for (int sh = lo_bit; sh < 64; sh += 16) {
+        std::vector<std::thread> ts;
+        for (int w = 0; w < th; ++w)
+            ts.emplace_back([&, w]() {
+                auto& c = cnt[w];
+                std::fill(c.begin(), c.end(), 0);
+                const size_t lo = w * chunk, hi = std::min(n, lo + chunk);
+                for (size_t i = lo; i < hi; ++i) ++c[(a[i] >> sh) & 0xFFFF];
+            });
+        for (auto& t : ts) t.join();
+        ts.clear();
+        size_t run = 0;  // digit-major, thread-minor: a thread's items of a digit follow the lower threads'
+        for (int d = 0; d < 65536; ++d)
+            for (int w = 0; w < th; ++w) {
+                const size_t x = cnt[w][d];
+                cnt[w][d] = run;
+                run += x;
+            }
+        for (int w = 0; w < th; ++w)
+            ts.emplace_back([&, w]() {
+                auto& c = cnt[w];
+                const size_t lo = w * chunk, hi = std::min(n, lo + chunk);
+                for (size_t i = lo; i < hi; ++i) b[c[(a[i] >> sh) & 0xFFFF]++] = a[i];
+            });
+        for (auto& t : ts) t.join();
         a.swap(b);
     }
 }
@@ -581,17 +693,34 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     // ---- token lists: (column, tid rank) ascending; entries idx << 8 | tf, tf > 0 only (a tf = 0
     // token adds +0 to a dot and never decides a hit: recommender.cpp:74-85)
     hp.tok_list.assign(T, {});
-    std::vector<std::vector<uint32_t>> cnt(T);
+    // per thread (a contiguous range of users) the entries of every (column, rank) key: the counts,
+    // later each thread's first entry in every list (its cursors)
+    std::vector<int64_t> kbase((size_t)T + 1, 0);
+    for (int t = 0; t < T; ++t) kbase[t + 1] = kbase[t] + hc.n_ranks(t);
+    const int th = kBuildThreads;
+    const int64_t uchunk = ((int64_t)n + th - 1) / th;
+    std::vector<std::vector<uint32_t>> tcnt(th);
+    auto users = [&](int w, auto f) {
+        const int64_t lo = w * uchunk, hi = std::min<int64_t>(n, lo + uchunk);
+        for (int64_t i = lo; i < hi; ++i)
+            for (int t = 0; t < T; ++t)
+                for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
+                    if (hc.tf[k] > 0) f(i, t, k, (size_t)(kbase[t] + hc.tid[k]));
+    };
     {
         std::vector<std::thread> ts;
-        for (int t = 0; t < T; ++t)
-            ts.emplace_back([&, t]() {
-                cnt[t].assign((size_t)hc.n_ranks(t), 0u);
-                for (int32_t i = 0; i < n; ++i)
-                    for (int64_t k = hc.tok_off[(size_t)i * T + t]; k < hc.tok_off[(size_t)i * T + t + 1]; ++k)
-                        if (hc.tf[k] > 0) ++cnt[t][hc.tid[k]];
+        for (int w = 0; w < th; ++w)
+            ts.emplace_back([&, w]() {
+                tcnt[w].assign((size_t)kbase[T], 0u);
+                users(w, [&](int64_t, int, int64_t, size_t key) { ++tcnt[w][key]; });
             });
         for (auto& x : ts) x.join();
+    }
+    std::vector<std::vector<uint32_t>> cnt(T);
+    for (int t = 0; t < T; ++t) {
+        cnt[t].assign((size_t)hc.n_ranks(t), 0u);
+        for (int w = 0; w < th; ++w)
+            for (size_t r = 0; r < cnt[t].size(); ++r) cnt[t][r] += tcnt[w][kbase[t] + r];
     }
     sc.lap("checks + token counts");
     uint64_t off = 0;
@@ -646,20 +775,27 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     if (!collect(hc.club_off, hc.clubs, ckeys) || !collect(hc.friend_off, hc.friends, fkeys))
         return bail("a club / friend id repeats more than 255 times in one profile");
     sc.lap("token lists + set keys");
-    radix_sort_u64(ckeys, 64);
-    radix_sort_u64(fkeys, 64);
+    // (id, idx, multiplicity) keys arrive in idx order: a stable sort by id puts each id's
+    // entries in idx order
+    par_radix_sort_u64(ckeys, 32);
+    par_radix_sort_u64(fkeys, 32);
     sc.lap("set keys sorted");
     const uint64_t set_off = off;
     if (off + ckeys.size() + fkeys.size() >= (1ull << 32)) return bail("more than 2^32 postings");
-    hp.post.resize(off + ckeys.size() + fkeys.size());
+    hp.post.resize_uninit(off + ckeys.size() + fkeys.size());
     auto add_sets = [&](const std::vector<uint64_t>& keys, std::unordered_map<uint32_t, int32_t>& m) {
+        uint32_t* dst = hp.post.data() + off;
+        par_for((int64_t)keys.size(), [&](int64_t lo, int64_t hi) {
+            for (int64_t x = lo; x < hi; ++x) dst[x] = (uint32_t)keys[x];
+        });
+        size_t nid = 0;
+        for (size_t a = 1; a <= keys.size(); ++a) nid += a == keys.size() || (keys[a] >> 32) != (keys[a - 1] >> 32);
+        m.reserve(nid);
+        hp.lists.reserve(hp.lists.size() + nid);
         for (size_t a = 0; a < keys.size();) {
             const uint32_t id = (uint32_t)(keys[a] >> 32);
-            size_t b = a;
-            while (b < keys.size() && (uint32_t)(keys[b] >> 32) == id) {
-                hp.post[off + (b - a)] = (uint32_t)keys[b];
-                ++b;
-            }
+            size_t b = a + 1;
+            while (b < keys.size() && (uint32_t)(keys[b] >> 32) == id) ++b;
             m[id] = (int32_t)hp.lists.size();
             hp.lists.push_back(PList{(uint32_t)off, 0u, 0u, (uint32_t)(b - a)});
             off += b - a;
@@ -671,23 +807,32 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     (void)set_off;
     sc.lap("set lists");
     // ---- token entries and their norms, per column in idx order (lists come out sorted)
-    hp.pnorm.resize(hp.tok_entries);
+    hp.pnorm.resize_uninit(hp.tok_entries);
     {
-        std::vector<std::thread> ts;
-        for (int t = 0; t < T; ++t)
-            ts.emplace_back([&, t]() {
-                std::vector<uint32_t> cur(cnt[t].size(), 0u);
-                for (size_t tid = 0; tid < cnt[t].size(); ++tid)
-                    if (hp.tok_list[t][tid] >= 0) cur[tid] = hp.lists[hp.tok_list[t][tid]].off;
-                for (int32_t i = 0; i < n; ++i) {
-                    const size_t r = (size_t)i * T + t;
-                    for (int64_t k = hc.tok_off[r]; k < hc.tok_off[r + 1]; ++k) {
-                        if (hc.tf[k] <= 0) continue;
-                        const uint32_t x = cur[hc.tid[k]]++;
-                        hp.post[x] = ((uint32_t)i << 8) | (uint32_t)hc.tf[k];
-                        hp.pnorm[x] = hc.sqrt_nb[r];
-                    }
+        // each thread's cursor in every list: the list's start + the lower threads' entries; the
+        // threads own ascending user ranges, so every list comes out in idx order
+        par_for((int64_t)kbase[T], [&](int64_t lo, int64_t hi) {
+            int t = 0;
+            for (int64_t key = lo; key < hi; ++key) {
+                while (kbase[t + 1] <= key) ++t;
+                const int32_t li = hp.tok_list[t][key - kbase[t]];
+                uint32_t x = li >= 0 ? hp.lists[li].off : 0u;
+                for (int w = 0; w < th; ++w) {
+                    const uint32_t c = tcnt[w][key];
+                    tcnt[w][key] = x;
+                    x += c;
                 }
+            }
+        });
+        std::vector<std::thread> ts;
+        for (int w = 0; w < th; ++w)
+            ts.emplace_back([&, w]() {
+                auto& cur = tcnt[w];
+                users(w, [&](int64_t i, int t, int64_t k, size_t key) {
+                    const uint32_t x = cur[key]++;
+                    hp.post[x] = ((uint32_t)i << 8) | (uint32_t)hc.tf[k];
+                    hp.pnorm[x] = hc.sqrt_nb[(size_t)i * T + t];
+                });
             });
         for (auto& x : ts) x.join();
     }
@@ -700,8 +845,8 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
         coff += (((uint64_t)(n - 1) >> L.shift) + 1) + 1;
         if (coff >= (1ull << 32)) return bail("cell table beyond 2^32 entries");
     }
-    hp.cells.resize(coff);
-    par_for((int64_t)hp.lists.size(), [&](int64_t lo, int64_t hi) {
+    hp.cells.resize_uninit(coff);
+    par_dyn((int64_t)hp.lists.size(), 64, [&](int64_t lo, int64_t hi) {  // the token lists come first and are long
         for (int64_t li = lo; li < hi; ++li) {
             const PList& L = hp.lists[li];
             const uint32_t nc = (uint32_t)(((uint64_t)(n - 1) >> L.shift) + 1);

@@ -2,7 +2,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -18,13 +22,68 @@ namespace pf {
 // replaced at open by their rank among the column's distinct ids (F3 on the device,
 // pf_idf.hip).  Ranks keep the ids' order, and the path only compares ids for equality and
 // looks up their idf, so every score is unchanged; the device layouts then see dense ids.
+// A vector of trivially copyable T whose resize leaves the elements uninitialised: the store
+// builders write every element (or fill them on threads), so the pages of these multi-GB
+// arrays are first touched by the threads that write them, not by a serial value-initialisation.
+template <class T>
+class PodVec {
+  public:
+    using value_type = T;
+    PodVec() = default;
+    PodVec(const PodVec&) = delete;
+    PodVec& operator=(const PodVec&) = delete;
+    PodVec(PodVec&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+    PodVec& operator=(PodVec&& o) noexcept { swap(o); return *this; }
+    ~PodVec() { std::free(p_); }
+    // arrays of 32 MB and more sit on 2 MB pages where the kernel offers them (madvise mode of
+    // transparent huge pages): 512x fewer first-touch faults, and unmapping them is cheap
+    void resize_uninit(size_t n) {
+        if (n == n_) return;
+        std::free(p_);
+        p_ = nullptr;
+        n_ = 0;
+        if (n == 0) return;
+        const size_t bytes = n * sizeof(T);
+        if (bytes >= (32u << 20)) {
+            const size_t huge = 2u << 20, rounded = (bytes + huge - 1) & ~(huge - 1);
+            void* q = nullptr;
+            if (posix_memalign(&q, huge, rounded) == 0) {
+                madvise(q, rounded, MADV_HUGEPAGE);  // advisory: ignored where THP is off
+                p_ = static_cast<T*>(q);
+            }
+        } else {
+            p_ = static_cast<T*>(std::malloc(bytes));
+        }
+        if (!p_) throw std::bad_alloc();
+        n_ = n;
+    }
+    void clear() { std::free(p_); p_ = nullptr; n_ = 0; }
+    void swap(PodVec& o) noexcept { std::swap(p_, o.p_); std::swap(n_, o.n_); }
+    T* data() { return p_; }
+    const T* data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T& operator[](size_t i) { return p_[i]; }
+    const T& operator[](size_t i) const { return p_[i]; }
+    const T& back() const { return p_[n_ - 1]; }
+    T* begin() { return p_; }
+    T* end() { return p_ + n_; }
+    const T* begin() const { return p_; }
+    const T* end() const { return p_ + n_; }
+
+  private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+};
+
 struct HostCorpus {
     int32_t n = 0, T = 0;
     std::vector<int32_t> uid, pub, comp, gen, age, reg;  // reg: 3 per user
-    std::vector<int64_t> club_off, friend_off, tok_off;  // tok_off: n*T+1, rows sorted by tid
+    std::vector<int64_t> club_off, friend_off;
+    PodVec<int64_t> tok_off;                             // n*T+1, rows sorted by tid
     std::vector<uint32_t> clubs, friends;
-    std::vector<int32_t> tid, tf;                        // tid: the column rank of the token id
-    std::vector<double> sqrt_nb;                         // per (user, col) row
+    PodVec<int32_t> tid, tf;                             // tid: the column rank of the token id
+    PodVec<double> sqrt_nb;                              // per (user, col) row
     std::vector<uint8_t> has_idf;                        // per column
     std::vector<std::vector<int32_t>> tid_of_rank;       // per column: the caller's id of each rank
     std::vector<std::vector<float>> idf;                 // per column, by rank (empty: no idf map)
@@ -44,16 +103,16 @@ struct HostCorpus {
 };
 
 struct HostStore {
-    std::vector<uint4> stream;
+    PodVec<uint4> stream;
     std::vector<uint64_t> tile_off;
     std::vector<uint32_t> tile_steps;
     std::vector<uint32_t> tile_slot0;   // first slot of each tile
     std::vector<uint8_t> tile_lgk;      // log2 of the lanes per candidate (long records are split)
     std::vector<uint32_t> slot_tile;    // tile of each slot
-    std::vector<double> norms;
+    PodVec<double> norms;
     std::vector<uint64_t> norm_off;
     std::vector<uint4> hdr0, hdr1, hdr2;
-    std::vector<uint4> rows;            // row store: slot p's record at rows[row_off[p]], 16-B padded
+    PodVec<uint4> rows;                 // row store: slot p's record at rows[row_off[p]], 16-B padded
     std::vector<uint64_t> row_off;      // [n + 1]
     std::vector<int32_t> slot_of_idx;
     std::vector<int32_t> idx_of_slot;
@@ -73,9 +132,9 @@ struct HostPost {
     bool ok = false;
     std::string why;                                   // reason when !ok
     std::vector<uint4> hdr;                            // [2 * n]
-    std::vector<uint32_t> post;                        // token lists, then club lists, then friend lists
-    std::vector<double> pnorm;                         // [token entries]
-    std::vector<uint32_t> cells;
+    PodVec<uint32_t> post;                             // token lists, then club lists, then friend lists
+    PodVec<double> pnorm;                              // [token entries]
+    PodVec<uint32_t> cells;
     std::vector<PList> lists;
     std::vector<std::vector<int32_t>> tok_list;        // [col][tid] -> list (-1: none)
     std::unordered_map<uint32_t, int32_t> club_list, friend_list;

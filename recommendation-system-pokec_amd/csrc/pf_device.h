@@ -33,11 +33,14 @@ __device__ __forceinline__ double term_of(const QConst& q, int slot, double s) {
 // recommender.cpp:119-128: inter counted over B (with duplicates) / (sqrt|A| sqrt|B|), as float
 // (out of line, like ratio_term: the fixed-term phase calls them for four candidates per thread,
 // and eight inlined exp + division chains made the scan's hot code larger than the instruction cache)
-static __device__ __attribute__((noinline)) double set_term(const QConst& q, int slot, int inter, int nb,
-                                                             double sqrt_na) {
+__device__ __forceinline__ double set_term_inl(const QConst& q, int slot, int inter, int nb, double sqrt_na) {
     const double den = sqrt_na * sqrt((double)nb);
     const double s = den <= 0.0 ? 0.0 : (double)(float)((double)inter / den);
     return term_of(q, slot, s);
+}
+static __device__ __attribute__((noinline)) double set_term(const QConst& q, int slot, int inter, int nb,
+                                                             double sqrt_na) {
+    return set_term_inl(q, slot, inter, nb, sqrt_na);
 }
 
 // recommender.cpp:114-116: (float)(dot / (sqrt(na) * sqrt(nb)))

@@ -30,6 +30,14 @@ namespace pf {
 static_assert(sizeof(QConst) % 16 == 0, "QConst must keep the LDS carve 16-B aligned");
 static_assert(sizeof(QVal) == 16, "QVal is one 16-B load");
 
+// Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
+// this keeps the compiler from moving accesses across the point).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Per-lane record walk state
 struct Walk {
     uint32_t cnt;        // clubs intersections (low 16 bits) + friends intersections << 16
@@ -437,6 +445,206 @@ __device__ __forceinline__ void walk_row(RowWalk& W, const uint4* base, const ui
     }
 }
 
+// K1' epilogue, wave-dense (packed).  fas_epilogue's per-lane loop runs the expensive terms (two
+// FP64 divisions and an exp per text column, a sqrt more per set term) once per hit column of
+// the lane with the most, so a wave pays ~8 rounds for a mean of ~4 hit columns per pair.  Here
+// every lane turns its hit words (held in registers) into items — one per hit column (its dot,
+// in the record's ascending-tid order) and one per nonzero club / friend intersection — written
+// as 16-B entries to a queue in the wave's strip of the (now consumed) hit lists; the wave then
+// computes every item's term one per lane, and each lane adds its terms in the reference's order
+// (public .. friends, then the common columns ascending, s = 0 terms between).  A wave whose
+// items exceed its strip (320) takes fas_epilogue; overflowed hit lists take its record re-walk.
+enum : uint32_t { kItemText = 0, kItemClubs = 1, kItemFriends = 2 };
+
+__device__ __forceinline__ double item_term(const QConst& q, const DevStore& st, const uint4& it) {
+    const uint32_t kind = it.w >> 16;
+    if (kind == kItemText) {
+        const int t = (int)(it.w & 0xFFu), rank = (int)((it.w >> 8) & 0xFFu);
+        const double dot = __hiloint2double((int)it.y, (int)it.x);
+        const double nrm = reinterpret_cast<const double*>(st.rows + it.z)[rank];
+        return dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm);
+    }
+    const bool cl = kind == kItemClubs;  // one inlined chain for both (a call here would spill the loop)
+    return set_term_inl(q, cl ? PF_F_CLUBS : PF_F_FRIENDS, (int)it.x, (int)it.y, cl ? q.sqrt_clubs : q.sqrt_friends);
+}
+
+__device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& st, const RowRec& rec, uint64_t ro,
+                                               uint32_t len, const uint4& h0, const uint4& h1, const uint4& h2,
+                                               uint32_t cnt, uint32_t nh, bool active, uint64_t* tep) {
+    const QConst& q = *v.q;
+    const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+    const bool overflow = nh > kHitCap;
+    uint32_t* hl = reinterpret_cast<uint32_t*>(v.hits);
+    const uint32_t nhl = (active && !overflow) ? nh : 0u;
+    uint32_t hw[kHitCap];
+#pragma unroll
+    for (int i = 0; i < (int)kHitCap; ++i) hw[i] = (uint32_t)i < nhl ? hl[i * kPairThreads + threadIdx.x] : 0u;
+    auto colw = [](uint32_t w) { return (w >> kTidBits) & 63u; };
+    uint32_t ncol = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kHitCap; ++i)
+        ncol += ((uint32_t)i < nhl && (i == 0 || colw(hw[i]) != colw(hw[i > 0 ? i - 1 : 0]))) ? 1u : 0u;
+    const uint32_t nc = h2.y, nf = h2.z;
+    const int ic = (int)(cnt & 0xFFFFu), ifr = (int)(cnt >> 16);
+    const bool dense = active && !overflow;
+    const bool club_it = dense && q.n_clubs > 0 && nc > 0 && ic > 0;
+    const bool fr_it = dense && q.n_friends > 0 && nf > 0 && ifr > 0;
+    const uint32_t nit = dense ? ncol + (club_it ? 1u : 0u) + (fr_it ? 1u : 0u) : 0u;
+    uint32_t x = nit;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    const uint32_t base = x - nit, total = (uint32_t)__shfl((int)x, 63);
+    constexpr uint32_t kQueue = kHitSlots * 64u / 4u;
+    if (total > kQueue) {  // (wave-uniform) the per-lane epilogue, hit lists intact
+        if (!active) return 0.0f;
+        return fas_epilogue<true, true>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u, [nh](uint32_t) { return nh; }, tep);
+    }
+    auto item = [&](uint32_t k) {  // 16-B entry k of the wave's strip (rows of 64 words)
+        return reinterpret_cast<uint4*>(hl + ((4u * k) >> 6) * kPairThreads + (uint32_t)wv * 64u + ((4u * k) & 63u));
+    };
+    wave_sync();  // every lane holds its hit words: the strip is free
+    const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    uint32_t k = base;
+    if (club_it) *item(k++) = make_uint4((uint32_t)ic, nc, 0u, kItemClubs << 16);
+    if (fr_it) *item(k++) = make_uint4((uint32_t)ifr, nf, 0u, kItemFriends << 16);
+    const uint32_t nbase = (uint32_t)(ro + ((len + 3u) >> 2));  // the record's column norms (uint4 index)
+    double dot = 0.0;
+#pragma unroll
+    for (int i = 0; i < (int)kHitCap; ++i) {
+        if ((uint32_t)i < nhl) {
+            const uint32_t w = hw[i], col = colw(w);
+            const uint32_t val = probe_p(v, kTagTok | (w & 0xFFFFFFu));
+            const bool first = i == 0 || col != colw(hw[i > 0 ? i - 1 : 0]);
+            dot = (first ? 0.0 : dot) + hit_product(v, val & kTidMask, (int32_t)(w >> 24));
+            const bool last = (uint32_t)(i + 1) == nhl || col != colw(hw[i + 1 < (int)kHitCap ? i + 1 : i]);
+            if (last) {
+                const uint32_t rank = (uint32_t)__popcll(cmask & ((1ull << col) - 1ull));
+                *item(k++) = make_uint4((uint32_t)__double2loint(dot), (uint32_t)__double2hiint(dot), nbase,
+                                        (kItemText << 16) | (rank << 8) | col);
+            }
+        }
+    }
+    wave_sync();
+    for (uint32_t j = (uint32_t)lane; j < total; j += 64u) {  // the wave's terms, one per lane
+        uint4 it = *item(j);
+        const double term = item_term(q, st, it);
+        it.x = (uint32_t)__double2loint(term);
+        it.y = (uint32_t)__double2hiint(term);
+        *item(j) = it;
+    }
+    wave_sync();
+    if (tep) tep[0] = clock64();
+    auto term_at = [&](uint32_t kk) {
+        const uint4 it = *item(kk);
+        return __hiloint2double((int)it.y, (int)it.x);
+    };
+    // every active lane: the fixed terms (an overflowed lane computes its set terms itself)
+    double sum = 0.0;
+    int used = 0;
+    const uint32_t pb = h2.x & 0xFFu, gb = (h2.x >> 8) & 0xFFu;
+    if (q.pubcode != kCodeMissing && pb != kCodeMissing) { sum += q.sig_pub[pb == q.pubcode]; ++used; }
+    if (q.gencode != kCodeMissing && gb != kCodeMissing) { sum += q.sig_gen[gb == q.gencode]; ++used; }
+    const int cb = (int)h0.z, ab = (int)h0.w;
+    if (q.comp > 0 && cb > 0) { sum += cb <= kValTab ? q.sig_comp[cb] : ratio_term(q, PF_F_COMPLETION, q.comp, cb); ++used; }
+    if (q.age > 0 && ab > 0) { sum += ab <= kValTab ? q.sig_age[ab] : ratio_term(q, PF_F_AGE, q.age, ab); ++used; }
+    const int r0 = (int)h1.x, r1 = (int)h1.y, r2 = (int)h1.z;
+    const int bcnt = (r0 >= 0) + (r1 >= 0) + (r2 >= 0);
+    if (q.a_regcnt > 0 && bcnt > 0) {
+        const int m = (r0 >= 0 && r0 == q.reg[0]) + (r1 >= 0 && r1 == q.reg[1]) + (r2 >= 0 && r2 == q.reg[2]);
+        sum += q.sig_reg[bcnt][m];
+        ++used;
+    }
+    uint32_t kk = base;
+    if (q.n_clubs > 0 && nc > 0) {
+        sum += ic == 0 ? q.sig0_clubs : (overflow ? set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs) : term_at(kk++));
+        ++used;
+    }
+    if (q.n_friends > 0 && nf > 0) {
+        sum += ifr == 0 ? q.sig0_friends
+                        : (overflow ? set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends) : term_at(kk++));
+        ++used;
+    }
+    // the common columns ascending: a hit column's term (the items are in column order), else s = 0
+    uint64_t common = q.colmask & cmask;
+    used += __popcll(common);
+    if (active && !overflow) {
+        const uint32_t ke = base + nit;
+        uint32_t nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
+        while (common) {
+            const uint32_t c = (uint32_t)__ffsll((unsigned long long)common) - 1u;
+            common &= common - 1ull;
+            if (c == nextc) {
+                sum += term_at(kk++);
+                nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
+            } else {
+                sum += q.sig0_col[c];
+            }
+        }
+    }
+    // Overflowed hit lists (> kHitCap token hits, ~0.4 % of pairs, a quarter of the waves): the
+    // wave walks each such record together, 64 words per round (one coalesced load), and
+    // accumulates the hits' products in record order on every lane (the reference's per-column
+    // dot order); lane t then computes column t's term, and the owner's sum takes the common
+    // columns ascending.
+    uint64_t ovm = __ballot(active && overflow);
+    while (ovm) {
+        const int l = __ffsll((unsigned long long)ovm) - 1;
+        ovm &= ovm - 1ull;
+        const uint64_t rol = (uint64_t)__shfl((long long)ro, l), cml = (uint64_t)__shfl((long long)cmask, l);
+        const uint32_t lenl = (uint32_t)__shfl((int)len, l), nsetl = (uint32_t)__shfl((int)(nc + nf), l);
+        const uint32_t* wl = reinterpret_cast<const uint32_t*>(st.rows + rol);
+        int cur = -1;
+        double dot = 0.0, mydot = 0.0;
+        bool myhas = false;
+        for (uint32_t b = nsetl; b < lenl; b += 64u) {
+            const uint32_t j = b + (uint32_t)lane;
+            const uint32_t w = j < lenl ? wl[j] : kPadWord;
+            const uint32_t val = j < lenl ? probe_p(v, kTagTok | (w & 0xFFFFFFu)) : 0u;
+            const double pr = val != 0u ? hit_product(v, val & kTidMask, (int32_t)(w >> 24)) : 0.0;
+            uint64_t hm = __ballot(val != 0u);
+            while (hm) {  // the hits in record order
+                const int x = __ffsll((unsigned long long)hm) - 1;
+                hm &= hm - 1ull;
+                const int cx = (int)(((uint32_t)__shfl((int)w, x) >> kTidBits) & 63u);
+                const double px = __shfl(pr, x);
+                if (cx != cur) {
+                    if (cur >= 0 && lane == cur) { mydot = dot; myhas = true; }
+                    cur = cx;
+                    dot = 0.0;
+                }
+                dot += px;
+            }
+        }
+        if (cur >= 0 && lane == cur) { mydot = dot; myhas = true; }
+        double term = 0.0;
+        if (myhas) {
+            const double nrm = reinterpret_cast<const double*>(st.rows + rol + ((lenl + 3u) >> 2))
+                [__popcll(cml & ((1ull << lane) - 1ull))];
+            term = mydot == 0.0 ? q.sig0_col[lane] : text_term(q, lane, mydot, nrm);
+        }
+        const uint64_t hasm = __ballot(myhas);
+        uint64_t cm = q.colmask & cml;
+        double sl = __shfl(sum, l);
+        while (cm) {
+            const int c = __ffsll((unsigned long long)cm) - 1;
+            cm &= cm - 1ull;
+            const double tc = __shfl(term, c);
+            sl += ((hasm >> c) & 1ull) ? tc : q.sig0_col[c];
+        }
+        if (lane == l) sum = sl;
+    }
+    if (tep) tep[1] = clock64();
+    if (!active || used == 0) return 0.0f;
+    // recommender_similarity.cpp:114-123
+    const double S = sum / (double)used;
+    const double F = (double)used / (double)(kNumFixed + q.n_cols);
+    if (S <= 0.0 && F <= 0.0) return 0.0f;
+    return (float)((2.0 * S * F) / (S + F));
+}
+
 // FAS of slot p by one lane alone (pairs kernel): the lane walks the slot's record in the row
 // store (contiguous 16-B steps, so the lane's loads consume whole cache lines), its own hit list
 // then holds the whole record's hits in order; the column norms follow the record in the row
@@ -460,11 +668,9 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
         RowWalk W{0u, threadIdx.x};
         walk_row(W, st.rows + ro, st.row_pad, len, nc, active ? nset : 0u, v, pcap);
         if (twalk) twalk[0] = clock64();
-        if (!active) return 0.0f;
         // a list that reached kHitCap reads as overflowed (the slow path re-walks the record)
         const uint32_t nh = W.ptr >= pcap ? kHitCap + 1 : (W.ptr - threadIdx.x) / kPairThreads;
-        return fas_epilogue<true, true>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [nh](uint32_t) { return nh; },
-                                        twalk ? twalk + 1 : nullptr);
+        return pair_epilogue(v, st, rec, ro, len, h0, h1, h2, W.cnt, nh, active, twalk ? twalk + 1 : nullptr);
     } else {
         Walk W;
         W.cnt = 0; W.nh = 0; W.pend = 0;
@@ -488,18 +694,16 @@ __device__ __forceinline__ void stage4(void* dst, const void* src, uint32_t byte
     uint4* d = reinterpret_cast<uint4*>(dst);
     const uint4* s = reinterpret_cast<const uint4*>(src);
     const uint32_t n = bytes / 16;
-    for (uint32_t base = 0; base < n; base += 4 * blockDim.x) {
-        uint4 r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = base + u * blockDim.x + threadIdx.x;
-            if (i < n) r[u] = s[i];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = base + u * blockDim.x + threadIdx.x;
-            if (i < n) d[i] = r[u];
-        }
+    if (n == 0) return;
+    const uint32_t bd = blockDim.x;
+    for (uint32_t base = threadIdx.x; base < n; base += 4 * bd) {
+        // clamped loads (always in range), guarded stores: four in flight per thread
+        const uint32_t i1 = base + bd, i2 = base + 2 * bd, i3 = base + 3 * bd;
+        const uint4 r0 = s[base], r1 = s[min(i1, n - 1)], r2 = s[min(i2, n - 1)], r3 = s[min(i3, n - 1)];
+        d[base] = r0;
+        if (i1 < n) d[i1] = r1;
+        if (i2 < n) d[i2] = r2;
+        if (i3 < n) d[i3] = r3;
     }
 }
 
@@ -799,14 +1003,6 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 // tf-byte array.
 constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16 + 16 * kPostMaxCols +
                                    8 * (kNumFixed + kPostMaxCols + 1);
-
-// Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
-// this keeps the compiler from moving accesses across the point).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // A query token in LDS: its weight and idf, and the products for tf = 1 and 2 (the common
 // cases), each computed as the reference does, wq * (tf * idf) (recommender.cpp:74-85).

@@ -358,12 +358,45 @@ __global__ __launch_bounds__(kOrderThreads) void order_pairs_kernel(const PairBl
         const int32_t s0 = slots[blocks[b].begin];
         return s0 < 0 ? 256 : slot_class(s0);
     };
-    for (int b = tid; b < nblocks; b += kOrderThreads) atomicAdd(&hist[key(b) + 1], 1);
+    // a thread's first 8 blocks: keys loaded together and kept (the rest recomputed)
+    constexpr int kKeep = 8;
+    int kk[kKeep];
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) {
+        const int b = tid + u * kOrderThreads;
+        kk[u] = b < nblocks ? key(b) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u)
+        if (kk[u] >= 0) atomicAdd(&hist[kk[u] + 1], 1);
+    for (int b = tid + kKeep * kOrderThreads; b < nblocks; b += kOrderThreads) atomicAdd(&hist[key(b) + 1], 1);
     __syncthreads();
-    if (tid == 0)
-        for (int i = 1; i < 258; ++i) hist[i] += hist[i - 1];  // hist[k] = first position of bucket k
+    if (tid < 64) {  // exclusive positions of the 257 buckets: hist[k] = first position of bucket k
+        int v[5], t = 0;
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int i = tid * 5 + u;
+            v[u] = i < 258 ? hist[i] : 0;
+            t += v[u];
+        }
+        int x = t;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (tid >= o) x += y;
+        }
+        int run = x - t;
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int i = tid * 5 + u;
+            run += v[u];
+            if (i < 258) hist[i] = run;
+        }
+    }
     __syncthreads();
-    for (int b = tid; b < nblocks; b += kOrderThreads) order[atomicAdd(&hist[key(b)], 1)] = b;
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u)
+        if (kk[u] >= 0) order[atomicAdd(&hist[kk[u]], 1)] = tid + u * kOrderThreads;
+    for (int b = tid + kKeep * kOrderThreads; b < nblocks; b += kOrderThreads) order[atomicAdd(&hist[key(b)], 1)] = b;
 }
 
 // ---------------------------------------------------------------- K6: query images
@@ -419,9 +452,13 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
         q->sig_age[v] = ai >= 0 ? g.age_rows[(size_t)ai * (kValTab + 1) + v] : 0.0;
     }
     if (tid < 16) q->sig_reg[tid >> 2][tid & 3] = a_regcnt > 0 ? g.sig_reg[a_regcnt * 16 + tid] : 0.0;
-    const Loc l = loc_of(st, p);
+    // the user's record and column norms from the row store (contiguous; the tile store strides a
+    // record's 16-B steps 1 KiB apart)
+    const uint64_t ro = st.row_off[p];
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(st.rows + ro);
+    const double* rn = reinterpret_cast<const double*>(st.rows + ro + ((record_words(h2, PACKED) + 3) >> 2));
     for (int t = tid; t < kMaxCols; t += kJobThreads)
-        q->sqrt_na[t] = (t < q->n_cols && ((colmask >> t) & 1ull)) ? col_norm(st, l, colmask, t) : 0.0;
+        q->sqrt_na[t] = (t < q->n_cols && ((colmask >> t) & 1ull)) ? rn[__popcll(colmask & ((1ull << t) - 1ull))] : 0.0;
     const uint32_t nc = h2.y, nf = h2.z, ntok = h2.w;
     if (tid == 0) {
         q->colmask = colmask;
@@ -446,7 +483,6 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     }
     // 2. the record's words once (tokens: their value entries, vi = token rank, recommender.cpp:74-85)
     const uint32_t len = record_words(h2, PACKED);
-    const uint32_t qw = chunk_words(len, l.lgk, PACKED);
     const uint32_t nset = nc + nf;
     const int lg = I.lg;
     const uint32_t ntab = PACKED ? 1u : 3u;
@@ -473,15 +509,15 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
         int32_t tid_, tf;
         uint64_t e;
         if (PACKED) {
-            const uint32_t w = word_at(st, l, qw, nset + k);
+            const uint32_t w = rw[nset + k];
             t = (int)((w >> kTidBits) & 63u);
             tid_ = (int32_t)(w & kTidMask);
             tf = (int32_t)(w >> 24);
             e = make_entry(kTagTok | ((uint32_t)t << kTidBits) | (w & kTidMask), kTokVal | k | ((uint32_t)t << kTidBits));
         } else {
-            const uint32_t w0 = word_at(st, l, qw, nset + 2 * k);  // tid | col << 26
+            const uint32_t w0 = rw[nset + 2 * k];  // tid | col << 26
             tid_ = (int32_t)(w0 & kWideTidMask);
-            const uint32_t w = word_at(st, l, qw, nset + 2 * k + 1);
+            const uint32_t w = rw[nset + 2 * k + 1];
             t = (int)(w & 0xFFu);
             tf = (int32_t)w >> 8;
             e = make_entry(w0, (uint32_t)t | (k << 8)) | (2ull << 62);
@@ -496,7 +532,7 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     // 3. distinct clubs / friends: a thread owns a word it claims first in the set; items
     //    [0, nuniq) are the sets, [nset, nset + ntok) the tokens
     for (uint32_t j = tid; j < nset; j += kJobThreads) {
-        const uint32_t w = word_at(st, l, qw, j);
+        const uint32_t w = rw[j];
         const bool club = j < nc;
         const uint32_t id = PACKED ? (club ? (w & ~kTagClub) : w) : w;
         const uint32_t key = (id + 1u) | (club ? 0u : 0x80000000u);
@@ -569,35 +605,44 @@ uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed) {
 // ---------------------------------------------------------------- K4': collaborative sums
 // recommender_graph.cpp:167-180: for each candidate, sum over friend-list positions (in order,
 // duplicates included) of (double)sim_u_f * (double)FAS(f, c); friends without a profile skip
+// A workgroup takes 64 candidates of one job; its four waves compute the products of a tile of
+// 64 friend positions (16 each, loads in flight together) into LDS, then wave 0 adds them per
+// candidate in position order.  A hub's long friend row costs one memory round trip per 64
+// positions over four waves instead of one per few positions on a single lane.
+constexpr int kCollabCands = 64, kCollabTile = 64;
 __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __restrict__ jobs, const int32_t* __restrict__ jix,
                                                              const int32_t* __restrict__ pool, const float* __restrict__ pout,
                                                              const int32_t* __restrict__ cand_slot, float* __restrict__ score) {
+    static_assert(kJobThreads == 4 * kCollabCands && kCollabTile % 4 == 0, "four waves of 64 candidates");
+    __shared__ double P[kCollabTile][kCollabCands];
     const DevJob J = jobs[jix[blockIdx.y]];
-    const int c = blockIdx.x * kJobThreads + threadIdx.x;
-    if (c >= J.cap) return;
-    if (cand_slot[J.cand_off + c] < 0) return;
+    const int c0 = (int)blockIdx.x * kCollabCands;
+    if (c0 >= J.cap) return;
+    const int cl = (int)(threadIdx.x & 63u), g = (int)(threadIdx.x >> 6);
+    const int c = c0 + cl;
+    const bool live = c < J.cap && cand_slot[J.cand_off + c] >= 0;
     const int32_t* fpos = pool + J.fpos_off;
     const float* sim = pout + J.sim_off;
     const float* M = pout + J.m_off;
+    constexpr int U = kCollabTile / 4;
     double s = 0.0;
-    // 32 friend positions at a time: their loads are issued together (one round trip per 32
-    // friends on a hub's long row), the adds stay in order
-    constexpr int U = 32;
-    for (int j0 = 0; j0 < J.nf; j0 += U) {
-        int r[U];
-        float w[U], m[U];
+    for (int j0 = 0; j0 < J.nf; j0 += kCollabTile) {
+        const int nj = min(kCollabTile, J.nf - j0);
 #pragma unroll
-        for (int k = 0; k < U; ++k) r[k] = j0 + k < J.nf ? fpos[j0 + k] : -1;
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            w[k] = r[k] >= 0 ? sim[r[k]] : 0.0f;
-            m[k] = r[k] >= 0 ? M[(size_t)r[k] * J.cap + c] : 0.0f;
+        for (int u = 0; u < U; ++u) {
+            const int jj = g * U + u;
+            if (jj < nj) {
+                const int r = fpos[j0 + jj];
+                P[jj][cl] = (r >= 0 && c < J.cap) ? (double)sim[r] * (double)M[(size_t)r * J.cap + c] : 0.0;
+            }
         }
-#pragma unroll
-        for (int k = 0; k < U; ++k)
-            if (r[k] >= 0) s += (double)w[k] * (double)m[k];
+        __syncthreads();
+        if (g == 0 && live)
+            for (int jj = 0; jj < nj; ++jj)
+                if (fpos[j0 + jj] >= 0) s += P[jj][cl];  // friends without a profile are skipped
+        __syncthreads();
     }
-    score[J.out_off + c] = (float)s;
+    if (g == 0 && live) score[J.out_off + c] = (float)s;
 }
 
 // ---------------------------------------------------------------- K7: clubs
@@ -929,7 +974,7 @@ hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int 
     if (njobs <= 0 || max_cap <= 0) return hipSuccess;
     for (int b = 0; b < njobs; b += 65535) {
         const int nb = njobs - b < 65535 ? njobs - b : 65535;
-        hipLaunchKernelGGL(collab_kernel, dim3((max_cap + kJobThreads - 1) / kJobThreads, nb), dim3(kJobThreads), 0, s,
+        hipLaunchKernelGGL(collab_kernel, dim3((max_cap + kCollabCands - 1) / kCollabCands, nb), dim3(kJobThreads), 0, s,
                            jobs, jix + b, pool, pout, cand_slot, score);
     }
     return hipGetLastError();

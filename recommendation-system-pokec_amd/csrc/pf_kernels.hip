@@ -393,7 +393,8 @@ struct RowWalk {
 
 __device__ __forceinline__ bool has_key(const QView& v, uint32_t key, uint32_t x) {
     const uint32_t k1 = v.tab[cuckoo_h1(x, v.lg)].x;
-    const uint32_t k2 = v.tab[cuckoo_h2(x, v.lg)].x;
+    // cuckoo_h2 as one bit-field extract (the compiler emits a shift and a mask)
+    const uint32_t k2 = v.tab[__builtin_amdgcn_ubfe(x, 32u - 2u * (uint32_t)v.lg, (uint32_t)v.lg)].x;
     return (k1 == key) | (k2 == key);
 }
 

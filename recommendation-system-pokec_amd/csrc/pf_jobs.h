@@ -20,7 +20,10 @@ hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* 
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
                          int32_t* ncand, hipStream_t s);
 // images [0, n_lds) are built in LDS (qimage_lds(...) > 0), the next n_glob in global memory
-hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_lds, int n_glob,
+// images [0, n_small) build with kImgLdsSmall bytes of LDS, the next n_big with kImgLds, the next n_glob in
+// global memory
+constexpr uint32_t kImgLdsSmall = 16 * 1024;
+hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_small, int n_big, int n_glob,
                           uint8_t* pool, uint32_t* scratch, int32_t* fail, hipStream_t s);
 uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed);
 hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,

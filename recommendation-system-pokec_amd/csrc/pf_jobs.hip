@@ -947,17 +947,23 @@ hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* 
     return hipGetLastError();
 }
 
-hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_lds, int n_glob,
+hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_small, int n_big, int n_glob,
                           uint8_t* pool, uint32_t* scratch, int32_t* fail, hipStream_t s) {
-    // images [0, n_lds) build in LDS (kImgLds bytes each), [n_lds, n_lds + n_glob) in global memory
-    if (n_lds > 0) {
+    // images [0, n_small) build in kImgLdsSmall bytes of LDS (most users: ~6 KB, so eight
+    // workgroups per CU instead of the three that kImgLds allows), [n_small, + n_big) in kImgLds,
+    // then n_glob in global memory
+    auto lds_launch = [&](int first, int n, uint32_t bytes) {
+        if (n <= 0) return;
         if (st.packed)
-            hipLaunchKernelGGL((qimage_kernel<true, true>), dim3(n_lds), dim3(kJobThreads), kImgLds, s, st, g, ij, pool,
+            hipLaunchKernelGGL((qimage_kernel<true, true>), dim3(n), dim3(kJobThreads), bytes, s, st, g, ij + first, pool,
                                scratch, fail);
         else
-            hipLaunchKernelGGL((qimage_kernel<false, true>), dim3(n_lds), dim3(kJobThreads), kImgLds, s, st, g, ij,
+            hipLaunchKernelGGL((qimage_kernel<false, true>), dim3(n), dim3(kJobThreads), bytes, s, st, g, ij + first,
                                pool, scratch, fail);
-    }
+    };
+    lds_launch(0, n_small, kImgLdsSmall);
+    lds_launch(n_small, n_big, kImgLds);
+    const int n_lds = n_small + n_big;
     if (n_glob > 0) {
         if (st.packed)
             hipLaunchKernelGGL((qimage_kernel<true, false>), dim3(n_glob), dim3(kJobThreads), 0, s, st, g, ij + n_lds,

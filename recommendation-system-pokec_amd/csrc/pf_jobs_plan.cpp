@@ -660,18 +660,23 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int lge = lg_for(0);
     auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
     auto dlg_of = [&](int32_t idx) { return pow2_lg(2 * (int64_t)J.img_nset[idx] + 2); };
-    int n_lds = 0;
+    // K6 builds the images in three launches: small LDS builds (<= kImgLdsSmall, many workgroups
+    // per CU), large LDS builds (<= kImgLds), hub users in global memory
+    int n_lds = 0, n_small = 0;
     {
         std::vector<int32_t> order(img_idx.size()), pos(img_idx.size());
-        std::vector<uint8_t> in_lds(img_idx.size());
+        std::vector<uint8_t> cls(img_idx.size());  // 0 small, 1 large, 2 global
         for (size_t k = 0; k < img_idx.size(); ++k) {
             const int32_t idx = img_idx[k];
-            in_lds[k] = J.img_lg[idx] && qimage_lds(J.img_lg[idx], lge, dlg_of(idx),
-                                                    (uint32_t)(J.img_nset[idx] + ntok_of(idx)), packed) > 0;
-            n_lds += in_lds[k];
+            const uint32_t need = J.img_lg[idx] ? qimage_lds(J.img_lg[idx], lge, dlg_of(idx),
+                                                             (uint32_t)(J.img_nset[idx] + ntok_of(idx)), packed)
+                                                : 0u;
+            cls[k] = need == 0 ? 2 : (need <= kImgLdsSmall ? 0 : 1);
+            n_lds += cls[k] < 2;
+            n_small += cls[k] == 0;
         }
-        int a = 0, g2 = n_lds;
-        for (size_t k = 0; k < img_idx.size(); ++k) pos[k] = in_lds[k] ? a++ : g2++;
+        int a = 0, b2 = n_small, g2 = n_lds;
+        for (size_t k = 0; k < img_idx.size(); ++k) pos[k] = cls[k] == 0 ? a++ : (cls[k] == 1 ? b2++ : g2++);
         for (size_t k = 0; k < img_idx.size(); ++k) order[pos[k]] = img_idx[k];
         img_idx.swap(order);
         for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
@@ -781,7 +786,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         }
     }
     // ---- the stages, in stream order
-    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_lds, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
+    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
                              W.d_scr.as<uint32_t>(), d_fail, c->stream));
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),

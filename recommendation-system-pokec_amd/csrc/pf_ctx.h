@@ -94,6 +94,7 @@ struct JobsState {
     bool nodes_dirty = false;
     std::vector<uint8_t> img_lg;                 // per idx: query-table log2 (0 = outside the device limits)
     std::vector<int32_t> img_nset;               // per idx: clubs + friends words of the record
+    std::vector<uint32_t> img_rows;              // per idx: ImgJob::rows (its completion / age table rows)
     std::vector<uint32_t> img_stamp;             // per idx: the layout pass that last gave it an image ...
     std::vector<int32_t> img_pos;                // ... and that image's index (no hash map per call)
     uint32_t img_gen = 0;

@@ -12,14 +12,15 @@ namespace pf {
 // de-duplication table in scratch (u32 words from scr_off; the item list follows it).
 struct ImgJob {
     int32_t idx, lg, lge, dlg;
-    uint32_t const_off, keys_off, vals_off, pad;
+    uint32_t const_off, keys_off, vals_off;
+    uint32_t rows;  // (completion row + 1) | (age row + 1) << 16 in the image-builder tables (0: none;
+                    // 0xFFFFFFFF: too many distinct values, K6 bisects the tables)
     int64_t scr_off;
 };
 
 hipError_t launch_gather(const DevJobsStore& g, const DevView& v, const DevJob* jobs, int njobs, const int32_t* pool,
                          const int64_t* pool64, int32_t* ht, int32_t* seq, int32_t* cand_slot, int32_t* cand_id,
                          int32_t* ncand, hipStream_t s);
-// images [0, n_lds) are built in LDS (qimage_lds(...) > 0), the next n_glob in global memory
 // images [0, n_small) build with kImgLdsSmall bytes of LDS, the next n_big with kImgLds, the next n_glob in
 // global memory
 constexpr uint32_t kImgLdsSmall = 16 * 1024;

@@ -58,6 +58,34 @@ __device__ __forceinline__ int block_rank(bool flag, int* wsum, int& total) {
     return before + r;
 }
 
+// block_rank for two flags per thread whose items are ordered all-f0-items first (thread order),
+// then all f1-items: one LDS exchange (wsum holds 2 * NW words)
+template <int NW>
+__device__ __forceinline__ void block_rank2(bool f0, bool f1, int* wsum, int& r0, int& r1, int& t0, int& t1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+    const uint64_t below = (1ull << lane) - 1ull;
+    r0 = __popcll(m0 & below);
+    r1 = __popcll(m1 & below);
+    if (lane == 0) {
+        wsum[wave] = __popcll(m0);
+        wsum[NW + wave] = __popcll(m1);
+    }
+    __syncthreads();
+    int b0 = 0, b1 = 0;
+    t0 = t1 = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        const int x0 = wsum[w], x1 = wsum[NW + w];
+        if (w < wave) { b0 += x0; b1 += x1; }
+        t0 += x0;
+        t1 += x1;
+    }
+    __syncthreads();
+    r0 += b0;
+    r1 += t0 + b1;
+}
+
 // inclusive prefix of v over the block; total in `total`
 template <int NW = kJobWaves>
 __device__ __forceinline__ int block_scan_incl(int v, int* wsum, int& total) {
@@ -140,7 +168,7 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
                                                              int32_t* __restrict__ seq, int32_t* __restrict__ cand_slot,
                                                              int32_t* __restrict__ cand_id, int32_t* __restrict__ ncand,
                                                              const int64_t* __restrict__ pool64) {
-    __shared__ int wsum[kGatherWaves];
+    __shared__ int wsum[2 * kGatherWaves];
     __shared__ int s_count, s_keep, s_done;
     const DevJob J = jobs[blockIdx.x];
     const int tid = threadIdx.x;
@@ -240,54 +268,66 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
         s_done = 0;
     }
     __syncthreads();
-    for (int base = 0; base < total; base += kGatherThreads) {
-        const int p = base + tid;
-        int32_t x = -1;
-        if (p < total) {
-            int lo = 0, hi = J.nf;  // last friend j with seg[j] <= p
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (seg[mid] <= p) lo = mid; else hi = mid;
-            }
-            const int32_t f = frow[lo];
-            const int k = p - seg[lo];
-            if (graph && k == 0) x = f;
-            else {
-                int32_t rl;
-                const int32_t* row = row_of(g, vw, J, pool, f, rl);
-                x = row[graph ? k - 1 : k];
-            }
-            if (x == u) x = -1;  // :22 / :120
+    // two sequence elements per thread per round (positions base + tid and base + 1024 + tid): a
+    // round's table claims go out together and its ranks take one exchange per flag pair
+    auto element = [&](int p) -> int32_t {
+        if (p >= total) return -1;
+        int lo = 0, hi = J.nf;  // last friend j with seg[j] <= p
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (seg[mid] <= p) lo = mid; else hi = mid;
         }
-        uint32_t h = 0;
-        if (x >= 0) {
-            h = ht_claim(keys, mask, x);
-            atomicMin(&pos[h], p);
+        const int32_t f = frow[lo];
+        const int k = p - seg[lo];
+        int32_t x;
+        if (graph && k == 0) x = f;
+        else {
+            int32_t rl;
+            const int32_t* row = row_of(g, vw, J, pool, f, rl);
+            x = row[graph ? k - 1 : k];
         }
+        return x == u ? -1 : x;  // :22 / :120
+    };
+    for (int base = 0; base < total; base += 2 * kGatherThreads) {
+        const int p0 = base + tid, p1 = base + kGatherThreads + tid;
+        const int32_t x0 = element(p0), x1 = element(p1);
+        uint32_t h0 = 0, h1 = 0;
+        if (x0 >= 0) h0 = ht_claim(keys, mask, x0);
+        if (x1 >= 0) h1 = ht_claim(keys, mask, x1);
+        if (x0 >= 0) atomicMin(&pos[h0], p0);
+        if (x1 >= 0) atomicMin(&pos[h1], p1);
         __syncthreads();
         // the table lives at L2 (device-scope atomics): read it past the CU's L1
-        const bool first = x >= 0 && __hip_atomic_load(&pos[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p;
-        int nfirst;
-        const int rf = block_rank<kGatherWaves>(first, wsum, nfirst);
+        const bool first0 = x0 >= 0 && __hip_atomic_load(&pos[h0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p0;
+        const bool first1 = x1 >= 0 && __hip_atomic_load(&pos[h1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p1;
+        int rf0, rf1, nf0, nf1;
+        block_rank2<kGatherWaves>(first0, first1, wsum, rf0, rf1, nf0, nf1);
         const int cnt = s_count;
-        const bool in = first && cnt + rf < J.L;
-        bool keep = in;
-        if (!raw) {
-            if (interest)  // :46-54
-                keep = keep && __hip_atomic_load(&flag[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && x < g.n;
-            else keep = keep && x < g.n;                           // :167-170
-        }
-        int nkeep;
-        const int rk = block_rank<kGatherWaves>(keep, wsum, nkeep);
+        auto kept = [&](bool first, int rf, int32_t x, uint32_t h) {
+            bool keep = first && cnt + rf < J.L;
+            if (!raw) {
+                if (interest)  // :46-54
+                    keep = keep && __hip_atomic_load(&flag[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && x < g.n;
+                else keep = keep && x < g.n;                           // :167-170
+            }
+            return keep;
+        };
+        const bool keep0 = kept(first0, rf0, x0, h0), keep1 = kept(first1, rf1, x1, h1);
+        int rk0, rk1, nk0, nk1;
+        block_rank2<kGatherWaves>(keep0, keep1, wsum, rk0, rk1, nk0, nk1);
         const int kb = s_keep;
-        if (keep) {
-            slots[kb + rk] = raw ? 0 : g.slot_of[x];
-            ids[kb + rk] = g.g_uid[x];
+        if (keep0) {
+            slots[kb + rk0] = raw ? 0 : g.slot_of[x0];
+            ids[kb + rk0] = g.g_uid[x0];
+        }
+        if (keep1) {
+            slots[kb + rk1] = raw ? 0 : g.slot_of[x1];
+            ids[kb + rk1] = g.g_uid[x1];
         }
         __syncthreads();
         if (tid == 0) {
-            s_count = cnt + nfirst;
-            s_keep = kb + nkeep;
+            s_count = cnt + nf0 + nf1;
+            s_keep = kb + nk0 + nk1;
         }
         __syncthreads();
         if (s_count >= J.L) break;
@@ -445,8 +485,10 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     const int32_t reg0 = (int32_t)h1.x, reg1 = (int32_t)h1.y, reg2 = (int32_t)h1.z;
     const int a_regcnt = (reg0 >= 0) + (reg1 >= 0) + (reg2 >= 0);
     const uint64_t colmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
-    const int ci = comp > 0 ? find_val(g.comp_vals, g.n_comp, comp) : -1;
-    const int ai = age > 0 ? find_val(g.age_vals, g.n_age, age) : -1;
+    // the completion / age rows, looked up on the host (a device bisection is 7 dependent loads)
+    const bool rows16 = I.rows != 0xFFFFFFFFu;
+    const int ci = comp > 0 ? (rows16 ? (int)(I.rows & 0xFFFFu) - 1 : find_val(g.comp_vals, g.n_comp, comp)) : -1;
+    const int ai = age > 0 ? (rows16 ? (int)(I.rows >> 16) - 1 : find_val(g.age_vals, g.n_age, age)) : -1;
     for (int v = tid; v <= kValTab; v += kJobThreads) {
         q->sig_comp[v] = ci >= 0 ? g.comp_rows[(size_t)ci * (kValTab + 1) + v] : 0.0;
         q->sig_age[v] = ai >= 0 ? g.age_rows[(size_t)ai * (kValTab + 1) + v] : 0.0;

@@ -28,8 +28,8 @@ constexpr int64_t kChunkElems = 192ll << 20; // element workspace per chunk (x 1
 constexpr int64_t kChunkHt = 128ll << 20;    // gather hash tables per chunk (int32 words)
 constexpr size_t kPipeJobs = 1024;           // calls of this many jobs or more run as pipelined chunks
 constexpr uint32_t kStageLimitJobs = 48 * 1024;  // as pf_api.cpp kStageLimit (LDS-staged tables)
-constexpr int64_t kGatherChunk = 1024;          // K3's chunk (pf_jobs.hip kGatherThreads): the last chunk
-                                                // claims up to this many table slots past the limit
+constexpr int64_t kGatherChunk = 2048;          // K3's round (2 x pf_jobs.hip kGatherThreads): the last
+                                                // round claims up to this many table slots past the limit
 
 int32_t node_of(const pf_ctx* c, int32_t uid) {
     const auto& dn = c->jb.dense_node;  // uids of a dense range: one load (built at open)
@@ -228,6 +228,18 @@ int jobs_open(pf_ctx* c) {
         J.img_lg[i] = ok ? (uint8_t)lg : 0;
         J.img_nset[i] = (int32_t)((hc.club_off[i + 1] - hc.club_off[i]) + (hc.friend_off[i + 1] - hc.friend_off[i]));
     }, 4096);
+    // per profile: its completion / age rows in the image-builder tables (ImgJob::rows)
+    // (0xFFFFFFFF: more than 65534 distinct values, K6 looks the rows up itself)
+    const bool rows16 = comp_vals.size() < 0xFFFFu && age_vals.size() < 0xFFFFu;
+    J.img_rows.assign(n, rows16 ? 0u : 0xFFFFFFFFu);
+    if (rows16) par_jobs((size_t)n, [&](size_t i) {
+        auto row = [](const std::vector<int32_t>& vals, int32_t v) -> uint32_t {
+            if (v <= 0) return 0u;
+            auto it = std::lower_bound(vals.begin(), vals.end(), v);
+            return (it != vals.end() && *it == v) ? (uint32_t)(it - vals.begin()) + 1u : 0u;
+        };
+        J.img_rows[i] = row(comp_vals, hc.comp[i]) | (row(age_vals, hc.age[i]) << 16);
+    }, 1 << 14);
     std::vector<int32_t> slot_of(hs.slot_of_idx.begin(), hs.slot_of_idx.end());
     sc.lap("image sizes");
     hipError_t e = hipSuccess;
@@ -697,6 +709,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         m.lg = lg;
         m.lge = lge;
         m.dlg = dlg_of(idx);
+        m.rows = J.img_rows[idx];
         m.const_off = (uint32_t)ipool;
         m.keys_off = (uint32_t)(ipool + sizeof(QConst));
         const size_t nkeys = ((size_t)ntab << lg) + ((size_t)1 << lge);

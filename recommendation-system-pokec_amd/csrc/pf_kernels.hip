@@ -572,19 +572,27 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     uint64_t common = q.colmask & cmask;
     used += __popcll(common);
     if (active && !overflow) {
+        // a uniform loop over the query's columns (scalar control, the s = 0 term a broadcast
+        // read), adding where the candidate has the column too
         const uint32_t ke = base + nit;
         uint32_t nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
-        while (common) {
-            const uint32_t c = (uint32_t)__ffsll((unsigned long long)common) - 1u;
-            common &= common - 1ull;
-            if (c == nextc) {
-                sum += term_at(kk++);
-                nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
-            } else {
-                sum += q.sig0_col[c];
+        uint64_t qm = __builtin_amdgcn_readfirstlane((uint32_t)q.colmask) |
+                      ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(q.colmask >> 32)) << 32);
+        while (qm) {
+            const uint32_t c = (uint32_t)__ffsll((unsigned long long)qm) - 1u;
+            qm &= qm - 1ull;
+            const double s0 = q.sig0_col[c];
+            if ((common >> c) & 1ull) {
+                if (c == nextc) {
+                    sum += term_at(kk++);
+                    nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
+                } else {
+                    sum += s0;
+                }
             }
         }
     }
+    if (tep) tep[1] = clock64();
     // Overflowed hit lists (> kHitCap token hits, ~0.4 % of pairs, a quarter of the waves): the
     // wave walks each such record together, 64 words per round (one coalesced load), and
     // accumulates the hits' products in record order on every lane (the reference's per-column
@@ -637,7 +645,7 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
         }
         if (lane == l) sum = sl;
     }
-    if (tep) tep[1] = clock64();
+    if (tep) tep[2] = clock64();
     if (!active || used == 0) return 0.0f;
     // recommender_similarity.cpp:114-123
     const double S = sum / (double)used;
@@ -1129,7 +1137,7 @@ __device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng,
 // profiling build only (make K5T=1): per-phase clock64() sums over every wave, printed by
 // launch_post every 10th launch
 __device__ unsigned long long g_k5t[16];
-__device__ unsigned long long g_k1t[8];  // K1': staging, walk, epilogue, total, fixed, columns, fas, waves
+__device__ unsigned long long g_k1t[9];  // K1': staging, walk, epilogue, total, dense, assembly, overflow, waves, fas
 #define K5T(slot) do { const uint64_t t_ = clock64(); tacc[slot] += t_ - tprev; tprev = t_; } while (0)
 #else
 #define K5T(slot) do { } while (0)
@@ -1468,7 +1476,7 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
     extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef PF_K5_TIMERS
     const uint64_t t0 = clock64();
-    uint64_t tw[3] = {0, 0, 0};
+    uint64_t tw[4] = {0, 0, 0, 0};
     uint64_t* twp = tw;
 #else
     uint64_t* twp = nullptr;
@@ -1492,16 +1500,15 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
     const uint64_t t3 = clock64();
     // the wave's phase ends: the walk is wave-uniform; the epilogue's phases end at the wave's
     // last lane (max over the lanes that ran it)
-    uint64_t we = tw[0], fe = active ? tw[1] : 0, he = active ? tw[2] : 0;
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t a = (uint64_t)__shfl_xor((long long)we, o), f2 = (uint64_t)__shfl_xor((long long)fe, o),
-                       h2 = (uint64_t)__shfl_xor((long long)he, o);
-        we = a > we ? a : we;
-        fe = f2 > fe ? f2 : fe;
-        he = h2 > he ? h2 : he;
-    }
+    // (the epilogue's clocks are taken by every lane at wave-uniform points: lane 0's are the wave's)
+    uint64_t we = tw[0], fe = tw[1], he = tw[2], oe = tw[3];
+    we = (uint64_t)__shfl((long long)we, 0);
+    fe = (uint64_t)__shfl((long long)fe, 0);
+    he = (uint64_t)__shfl((long long)he, 0);
+    oe = (uint64_t)__shfl((long long)oe, 0);
     if (fe == 0) fe = we;
     if (he == 0) he = fe;
+    if (oe == 0) oe = he;
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(&g_k1t[0], (unsigned long long)(t1 - t0));
         atomicAdd(&g_k1t[1], (unsigned long long)(we - t1));
@@ -1509,7 +1516,8 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
         atomicAdd(&g_k1t[3], (unsigned long long)(t3 - t0));
         atomicAdd(&g_k1t[4], (unsigned long long)(fe - we));
         atomicAdd(&g_k1t[5], (unsigned long long)(he - fe));
-        atomicAdd(&g_k1t[6], (unsigned long long)(t3 - he));
+        atomicAdd(&g_k1t[6], (unsigned long long)(oe - he));
+        atomicAdd(&g_k1t[8], (unsigned long long)(t3 - oe));
         atomicAdd(&g_k1t[7], 1ull);
     }
 #endif
@@ -1630,16 +1638,16 @@ hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;
-        unsigned long long t[8];
+        unsigned long long t[9];
         hipStreamSynchronize(s);
         hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k1t), sizeof(t));
         if (++calls % 10 == 0 && t[7])
             fprintf(stderr,
-                    "k1pt per wave (clock64): staging=%.0f walk=%.0f epilogue=%.0f (fixed=%.0f columns=%.0f fas=%.0f) "
-                    "total=%.0f waves=%llu blocks=%d\n",
+                    "k1pt per wave (clock64): staging=%.0f walk=%.0f epilogue=%.0f (dense=%.0f assembly=%.0f "
+                    "overflow=%.0f fas=%.0f) total=%.0f waves=%llu blocks=%d\n",
                     (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[4] / t[7],
-                    (double)t[5] / t[7], (double)t[6] / t[7], (double)t[3] / t[7], t[7], nblocks);
-        const unsigned long long z[8] = {0};
+                    (double)t[5] / t[7], (double)t[6] / t[7], (double)t[8] / t[7], (double)t[3] / t[7], t[7], nblocks);
+        const unsigned long long z[9] = {0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_k1t), z, sizeof(z));
     }
 #endif

@@ -269,10 +269,12 @@ int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* ou
 /* Statistics of the recommenders' device job pipeline (pf_recommend_collab / _clubs /
  * _interest FoF and the batched drivers) since pf_jobs_stats_reset(ctx, 1): jobs run,
  * candidate-list entries scored, FAS pairs scored by the pair kernel (K1'), their
- * SURVEY 8(d) D3 bytes (b_c of each pair's candidate), the tile-store bytes the kernel
- * reads for them (48-B headers + record words), the staged query-image bytes (one image
- * per 256-pair block), and the pair kernel's device time (HIP events around each launch)
- * and launch count.  enable: bit 0 = time the pair kernel (HIP events around each
+ * SURVEY 8(d) D3 bytes (b_c of each pair's candidate), the bytes the pair-scoring stage
+ * reads / writes for them by access pattern (pair_record_bytes: headers + record words for a
+ * pair that walks its record; for collaborative friend groups the K1u walk's record words
+ * once per group plus the per-pair hit lists it writes and K1' reads), the staged query-image
+ * and union-table bytes (one per 512-pair / walk block), and the pair-scoring stage's device
+ * time (HIP events around K1u + K1' in each launch) and launch count.  enable: bit 0 = time the pair kernel (HIP events around each
  * launch), bit 1 = count pairs and bytes (one extra small kernel per launch); 0 stops
  * both.  Fields of a part that is off read 0. */
 typedef struct pf_jobs_stats {

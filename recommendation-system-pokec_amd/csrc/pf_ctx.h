@@ -98,6 +98,8 @@ struct JobsState {
     std::vector<uint32_t> img_stamp;             // per idx: the layout pass that last gave it an image ...
     std::vector<int32_t> img_pos;                // ... and that image's index (no hash map per call)
     uint32_t img_gen = 0;
+    bool union_on = true;                        // collaborative friend groups walk each record once (K6u / K1u;
+                                                 // PF_DEBUG union=0: every pair walks its own record)
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
     std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;
@@ -108,11 +110,19 @@ struct JobsState {
     DevView view{};
     DBuf d_view_node, d_view_ver, d_view_off, d_view_len, d_view_nbr;
     // per-chunk workspaces, double-buffered: chunk i + 1 is planned and launched while chunk i
-    // runs (run_all in pf_jobs_plan.cpp); the clubs accumulators are shared (stream order)
+    // runs (run_all in pf_jobs_plan.cpp).  Both slots queue on the context's stream: a stream per
+    // slot, so that consecutive calls overlap on the device, measured slower (r3y: the pair kernel
+    // 0.344 -> 0.385 ms beside the next call's images and gathers; cfg 3 1.93e9 -> 1.71e9).
     struct Ws {
         DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr;  // d_plan: the plan, then the results
+        DBuf d_upool, d_hb, d_hc;  // K6u union tables; K1u walk results (hit words, counts) per pair index
+        DBuf d_acc;                // clubs accumulators (zero between uses)
+        int64_t acc_jobs = 0;      // clubs jobs the accumulators hold
         PinBuf h_plan, h_out;
         hipEvent_t done = nullptr;  // recorded after the chunk's result copies
+        ~Ws() {
+            if (done) (void)hipEventDestroy(done);
+        }
         // what the chunk's unpack needs (host)
         bool active = false;
         std::vector<DevJob> dj;
@@ -134,8 +144,6 @@ struct JobsState {
     };
     std::deque<Pending> pending;                 // launch order
     uint64_t next_ticket = 1;
-    DBuf d_acc;
-    int64_t acc_jobs = 0;                        // clubs accumulators allocated (and zero)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
     bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)
     bool stats_count = false;                    // pair counters (bit 1)

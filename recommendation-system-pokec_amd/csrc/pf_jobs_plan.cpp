@@ -292,6 +292,7 @@ int jobs_open(pf_ctx* c) {
     J.view_over = nullptr;
     J.view_over_n = 0;
     J.nodes_dirty = false;
+    J.union_on = packed && debug_long("union", 0) != 0;
     J.ok = true;
     sc.lap("handles");
     return PF_OK;
@@ -575,6 +576,14 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     };
     std::vector<int32_t> jix_collab, jix_clubs, jix_topk;
     int max_cap_collab = 0, ktop = 1;
+    // collaborative friend groups (K6u / K1u): their pairs' walks happen once per group in K1u,
+    // and K1' runs only their epilogues (pblocks)
+    const int lge = lg_for(0);
+    auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
+    std::vector<UnionJob> ujobs;
+    std::vector<PairBlock> wblocks, pblocks;
+    size_t upool = 0;
+    uint32_t max_ulds = 0, max_wlds = 0;
     {
         size_t nb = 0, words = 0;  // the blocks and pool words this chunk appends (one allocation)
         for (size_t i = b; i < e; ++i) {
@@ -647,10 +656,58 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                 const int64_t span = kPairSpan;
                 std::vector<int32_t> fimg(d.nfd);
                 for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
-                for (int64_t x = 0; x < p.cap; x += span)
+                // friend groups: consecutive friends whose images are LDS-staged, up to kUnionMax of
+                // them and kUnionKeys record words (a group of one walks as a plain pair)
+                std::vector<std::pair<int, int>> grp;
+                std::vector<uint8_t> in_grp(d.nfd, 0);
+                if (J.union_on && p.cap > 0) {
+                    auto words = [&](int r) { return (int64_t)J.img_nset[p.fd[r]] + ntok_of(p.fd[r]); };
+                    auto ok = [&](int r) {
+                        const int32_t idx = p.fd[r];
+                        const int lgi = J.img_lg[idx];
+                        if (lgi == 0 || words(r) > kUnionKeys) return false;
+                        const size_t kv = 8 * (((size_t)1 << lgi) + ((size_t)1 << lge)) + (size_t)ntok_of(idx) * sizeof(QVal);
+                        return kv <= kStageLimitJobs;
+                    };
+                    for (int r = 0; r < d.nfd;) {
+                        int r1 = r;
+                        int64_t w = 0;
+                        while (r1 < d.nfd && r1 - r < kUnionMax && ok(r1) && w + words(r1) <= kUnionKeys) w += words(r1++);
+                        if (r1 - r >= 2) {
+                            grp.emplace_back(r, r1);
+                            for (int q = r; q < r1; ++q) in_grp[q] = 1;
+                            UnionJob U{};
+                            U.n = r1 - r;
+                            U.words = (int32_t)w;
+                            U.lg = pow2_lg(w * 5 / 2 + 1);  // load <= 0.4
+                            U.dlg = std::max(U.lg, pow2_lg(2 * w));
+                            U.tab_off = (uint32_t)upool;
+                            U.ostride = (int32_t)p.cap;
+                            for (int q = r; q < r1; ++q) U.idx[q - r] = p.fd[q];
+                            upool += (size_t)8 << U.lg;
+                            max_ulds = std::max(max_ulds, union_lds(U.dlg, U.words));
+                            max_wlds = std::max(max_wlds, 8u << U.lg);
+                            ujobs.push_back(U);
+                        }
+                        r = r1 > r ? r1 : r + 1;
+                    }
+                }
+                const int32_t u0 = (int32_t)ujobs.size() - (int32_t)grp.size();
+                for (int64_t x = 0; x < p.cap; x += span) {
+                    const int32_t cnt = (int32_t)std::min<int64_t>(span, p.cap - x);
                     for (int r = 0; r < d.nfd; ++r)
-                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), (int32_t)std::min<int64_t>(span, p.cap - x),
-                                                   (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
+                        if (!in_grp[r])
+                            blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
+                                                       (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
+                    for (size_t gi = 0; gi < grp.size(); ++gi) {
+                        const int r0 = grp[gi].first;
+                        wblocks.push_back(PairBlock{u0 + (int32_t)gi, (int32_t)(d.cand_off + x), cnt,
+                                                    (int32_t)(d.m_off + (int64_t)r0 * p.cap + x)});
+                        for (int r = r0; r < grp[gi].second; ++r)
+                            pblocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
+                                                        (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
+                    }
+                }
                 jix_collab.push_back(jn);
                 max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);
             } else if (p.kind == kDjInterest || p.kind == kDjAll) {
@@ -666,11 +723,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     if (dj.empty()) return PF_OK;
     if (W.done == nullptr) HIPCHK(c, hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    const hipStream_t s = c->stream;
     if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
     // ---- images (pf_api.cpp plan_images layout); the ones K6 builds in LDS first
     const uint32_t ntab = packed ? 1u : 3u;
-    const int lge = lg_for(0);
-    auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
     auto dlg_of = [&](int32_t idx) { return pow2_lg(2 * (int64_t)J.img_nset[idx] + 2); };
     // K6 builds the images in three launches: small LDS builds (<= kImgLdsSmall, many workgroups
     // per CU), large LDS builds (<= kImgLds), hub users in global memory
@@ -692,6 +748,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (size_t k = 0; k < img_idx.size(); ++k) order[pos[k]] = img_idx[k];
         img_idx.swap(order);
         for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
+        for (PairBlock& pb : pblocks) pb.qimg = pos[pb.qimg];
     }
     std::vector<ImgJob> ij(img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
@@ -741,7 +798,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_ij = a16z(o_p64 + pool64.size() * 8);
     const size_t o_refs = a16z(o_ij + ij.size() * sizeof(ImgJob));
     const size_t o_blk = a16z(o_refs + refs.size() * sizeof(QImageRef));
-    const size_t o_jc = a16z(o_blk + blocks.size() * sizeof(PairBlock));
+    const size_t o_uj = a16z(o_blk + blocks.size() * sizeof(PairBlock));
+    const size_t o_wb = a16z(o_uj + ujobs.size() * sizeof(UnionJob));
+    const size_t o_pb = a16z(o_wb + wblocks.size() * sizeof(PairBlock));
+    const size_t o_jc = a16z(o_pb + pblocks.size() * sizeof(PairBlock));
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
     const size_t o_res = a16z(o_jt + jix_topk.size() * 4);
@@ -757,13 +817,17 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_ij, ij.data(), ij.size() * sizeof(ImgJob));
     put(o_refs, refs.data(), refs.size() * sizeof(QImageRef));
     put(o_blk, blocks.data(), blocks.size() * sizeof(PairBlock));
+    put(o_uj, ujobs.data(), ujobs.size() * sizeof(UnionJob));
+    put(o_wb, wblocks.data(), wblocks.size() * sizeof(PairBlock));
+    put(o_pb, pblocks.data(), pblocks.size() * sizeof(PairBlock));
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
     std::memset(h + o_res, 0, 16);
-    const size_t o_ord = a16z(o_res + res_b);  // the pair blocks' dispatch order (device-written)
-    HIPCHK(c, W.d_plan.reserve(o_ord + std::max<size_t>(blocks.size(), 1) * 4));
-    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, c->stream));
+    const size_t o_ord = a16z(o_res + res_b);  // the pair / walk blocks' dispatch orders (device-written)
+    const size_t o_word = a16z(o_ord + std::max<size_t>(blocks.size(), 1) * 4);
+    HIPCHK(c, W.d_plan.reserve(o_word + std::max<size_t>(wblocks.size(), 1) * 4));
+    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, s));
     uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
     const int32_t* d_p32 = reinterpret_cast<const int32_t*>(d + o_p32);
@@ -771,6 +835,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const ImgJob* d_ij = reinterpret_cast<const ImgJob*>(d + o_ij);
     const QImageRef* d_refs = reinterpret_cast<const QImageRef*>(d + o_refs);
     const PairBlock* d_blk = reinterpret_cast<const PairBlock*>(d + o_blk);
+    UnionJob* d_uj = reinterpret_cast<UnionJob*>(d + o_uj);
+    const PairBlock* d_wb = reinterpret_cast<const PairBlock*>(d + o_wb);
+    const PairBlock* d_pb = reinterpret_cast<const PairBlock*>(d + o_pb);
+    int32_t* d_word = reinterpret_cast<int32_t*>(d + o_word);
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
@@ -788,25 +856,35 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
     HIPCHK(c, W.d_img.reserve(std::max<size_t>(ipool, 16)));
     HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
+    if (!ujobs.empty()) {  // K1u's results per pair index (E: every output slot of the chunk)
+        HIPCHK(c, W.d_upool.reserve(upool));
+        HIPCHK(c, W.d_hb.reserve(nE * kHitCap * 4));
+        HIPCHK(c, W.d_hc.reserve(nE * 8));
+    }
     hl.lap(kHpPlan);  // workspaces
     if (!jix_clubs.empty()) {
         const int64_t want = (int64_t)jix_clubs.size();
-        if (want > J.acc_jobs) {
+        if (want > W.acc_jobs) {
             const size_t words = (size_t)want * (size_t)std::max(J.js.n_club_ids, 1);
-            HIPCHK(c, J.d_acc.ensure(words * 8));
-            HIPCHK(c, hipMemsetAsync(J.d_acc.p, 0, J.d_acc.cap, c->stream));
-            J.acc_jobs = want;
+            HIPCHK(c, W.d_acc.ensure(words * 8));
+            HIPCHK(c, hipMemsetAsync(W.d_acc.p, 0, W.d_acc.cap, s));
+            W.acc_jobs = want;
         }
     }
     // ---- the stages, in stream order
     HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
-                             W.d_scr.as<uint32_t>(), d_fail, c->stream));
+                             W.d_scr.as<uint32_t>(), d_fail, s));
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
-                            d_ncand, c->stream));
-    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, c->stream));
+                            d_ncand, s));
+    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, s));
+    if (!ujobs.empty()) {
+        HIPCHK(c, launch_unions(c->ds, J.js, d_uj, (int)ujobs.size(), max_ulds, W.d_upool.as<uint8_t>(), d_fail, s));
+        HIPCHK(c, launch_order_pairs(d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), hc.n, d_word, s));
+    }
+    const bool any_pairs = !blocks.empty() || !pblocks.empty();
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
-    if ((J.stats_on || J.stats_count) && !blocks.empty()) {
+    if ((J.stats_on || J.stats_count) && any_pairs) {
         if (J.stat_used == J.stat_ev.size()) {
             hipEvent_t a, b2;
             HIPCHK(c, timing_event(&a));
@@ -816,33 +894,45 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         pe0 = J.stat_ev[J.stat_used].first;
         pe1 = J.stat_ev[J.stat_used].second;
         ++J.stat_used;
-        HIPCHK(c, hipEventRecord(pe0, c->stream));
+        HIPCHK(c, hipEventRecord(pe0, s));
+    }
+    if (!ujobs.empty()) {  // the pair-scoring stage (timed): K1u walks, K1' pairs, K1' pre-walked pairs
+        HIPCHK(c, launch_union_walk(c->ds, W.d_upool.as<uint8_t>(), d_uj, max_wlds, d_wb, (int)wblocks.size(), d_word,
+                                    W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(), s));
     }
     HIPCHK(c, launch_pairs(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(), d_ord,
-                           W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
+                           W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
+    HIPCHK(c, launch_pairs_prewalked(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, d_pb, (int)pblocks.size(),
+                                     W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(),
+                                     W.d_fl.as<float>(), s));
     if (pe1) {
-        HIPCHK(c, hipEventRecord(pe1, c->stream));
+        HIPCHK(c, hipEventRecord(pe1, s));
         ++J.st_launches;
     }
-    if (J.stats_count && !blocks.empty()) {
-        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(),
-                                    J.d_stats.as<unsigned long long>(), c->stream));
-        for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
-            const QImageRef& r = refs[pb.qimg];
-            J.st_img_bytes += (int64_t)(r.vals_off - r.const_off) +
-                              (int64_t)(ij[pb.qimg].idx >= 0 ? (hc.tok_off[(size_t)(ij[pb.qimg].idx + 1) * hc.T] -
-                                                               hc.tok_off[(size_t)ij[pb.qimg].idx * hc.T]) * 16 : 0);
-        }
+    if (J.stats_count && any_pairs) {
+        unsigned long long* acc = J.d_stats.as<unsigned long long>();
+        const uint2* hcv = W.d_hc.as<uint2>();
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), acc, 0, hcv, d_uj, s));
+        HIPCHK(c, launch_pair_stats(c->ds, d_pb, (int)pblocks.size(), W.d_slots.as<int32_t>(), acc, 1, hcv, d_uj, s));
+        HIPCHK(c, launch_pair_stats(c->ds, d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), acc, 2, hcv, d_uj, s));
+        for (const PairBlock& wb : wblocks) J.st_img_bytes += (int64_t)8 << ujobs[wb.qimg].lg;  // the staged union table
+        for (const auto* bl : {&blocks, &pblocks})
+            for (const PairBlock& pb : *bl) {  // the staged image per pair block (QConst + tables)
+                const QImageRef& r = refs[pb.qimg];
+                J.st_img_bytes += (int64_t)(r.vals_off - r.const_off) +
+                                  (int64_t)(ij[pb.qimg].idx >= 0 ? (hc.tok_off[(size_t)(ij[pb.qimg].idx + 1) * hc.T] -
+                                                                   hc.tok_off[(size_t)ij[pb.qimg].idx * hc.T]) * 16 : 0);
+            }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
-                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), c->stream));
+                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
-                           J.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                           d_ncand, (int64_t)J.js.n_club_ids, c->stream));
+                           W.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
+                           d_ncand, (int64_t)J.js.n_club_ids, s));
     HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                               W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop,
-                              c->stream));
+                              s));
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
     for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;
@@ -858,17 +948,17 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.h_out.ensure(ob));
     uint8_t* ho = W.h_out.as<uint8_t>();
     const size_t o_fail = 0, o_cnt = o_rcnt - o_res, o_keys = o_rkeys - o_res;
-    HIPCHK(c, hipMemcpyAsync(ho, d + o_res, res_b, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ho, d + o_res, res_b, hipMemcpyDeviceToHost, s));
     for (size_t q = 0; q < full.size(); ++q) {
         const DevJob& x = dj[full[q]];
         const size_t cnt = (size_t)std::max(x.cap, x.kind == kDjClubs ? J.js.n_club_ids : 0);
         uint8_t* dst = ho + full_off[q];
-        HIPCHK(c, hipMemcpyAsync(dst, W.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, W.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dst, W.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, W.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, W.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
-                                 c->stream));
+                                 s));
     }
-    HIPCHK(c, hipEventRecord(W.done, c->stream));
+    HIPCHK(c, hipEventRecord(W.done, s));
     hl.lap(kHpStage2);  // launches issued
     W.active = true;
     W.o_cnt = o_cnt;

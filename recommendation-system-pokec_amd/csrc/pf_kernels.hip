@@ -30,6 +30,15 @@ namespace pf {
 static_assert(sizeof(QConst) % 16 == 0, "QConst must keep the LDS carve 16-B aligned");
 static_assert(sizeof(QVal) == 16, "QVal is one 16-B load");
 
+#ifdef PF_K5_TIMERS
+// profiling build only (make K5T=1): per-phase clock64() sums over every wave (K5: launch_post,
+// K1': launch_pairs print them every 10th launch)
+__device__ unsigned long long g_k5t[16];
+// K1': staging, walk, epilogue, total, dense, assembly, overflow, waves, fas, then the epilogue's
+// waves past the item queue (per-lane fallback), items, epilogue waves
+__device__ unsigned long long g_k1t[12];
+#endif
+
 // Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
 // this keeps the compiler from moving accesses across the point).
 __device__ __forceinline__ void wave_sync() {
@@ -457,12 +466,16 @@ __device__ __forceinline__ void walk_row(RowWalk& W, const uint4* base, const ui
 // items exceed its strip (320) takes fas_epilogue; overflowed hit lists take its record re-walk.
 enum : uint32_t { kItemText = 0, kItemClubs = 1, kItemFriends = 2 };
 
-__device__ __forceinline__ double item_term(const QConst& q, const DevStore& st, const uint4& it) {
+// the candidate's column norm a text item needs (row store), 0 for a set item
+__device__ __forceinline__ double item_norm(const DevStore& st, const uint4& it) {
+    return (it.w >> 16) == kItemText ? reinterpret_cast<const double*>(st.rows + it.z)[(it.w >> 8) & 0xFFu] : 0.0;
+}
+
+__device__ __forceinline__ double item_term(const QConst& q, const uint4& it, double nrm) {
     const uint32_t kind = it.w >> 16;
     if (kind == kItemText) {
-        const int t = (int)(it.w & 0xFFu), rank = (int)((it.w >> 8) & 0xFFu);
+        const int t = (int)(it.w & 0xFFu);
         const double dot = __hiloint2double((int)it.y, (int)it.x);
-        const double nrm = reinterpret_cast<const double*>(st.rows + it.z)[rank];
         return dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm);
     }
     const bool cl = kind == kItemClubs;  // one inlined chain for both (a call here would spill the loop)
@@ -471,15 +484,18 @@ __device__ __forceinline__ double item_term(const QConst& q, const DevStore& st,
 
 __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& st, const RowRec& rec, uint64_t ro,
                                                uint32_t len, const uint4& h0, const uint4& h1, const uint4& h2,
-                                               uint32_t cnt, uint32_t nh, bool active, uint64_t* tep) {
+                                               uint32_t cnt, uint32_t nh, bool active, uint64_t* tep,
+                                               const uint32_t* hin = nullptr) {
     const QConst& q = *v.q;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const bool overflow = nh > kHitCap;
     uint32_t* hl = reinterpret_cast<uint32_t*>(v.hits);
     const uint32_t nhl = (active && !overflow) ? nh : 0u;
+    // the hit words: the lane's LDS hit list (its own walk), or hin (registers: K1u's walk)
     uint32_t hw[kHitCap];
 #pragma unroll
-    for (int i = 0; i < (int)kHitCap; ++i) hw[i] = (uint32_t)i < nhl ? hl[i * kPairThreads + threadIdx.x] : 0u;
+    for (int i = 0; i < (int)kHitCap; ++i)
+        hw[i] = (uint32_t)i < nhl ? (hin ? hin[i] : hl[i * kPairThreads + threadIdx.x]) : 0u;
     auto colw = [](uint32_t w) { return (w >> kTidBits) & 63u; };
     uint32_t ncol = 0;
 #pragma unroll
@@ -499,8 +515,19 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     }
     const uint32_t base = x - nit, total = (uint32_t)__shfl((int)x, 63);
     constexpr uint32_t kQueue = kHitSlots * 64u / 4u;
+#ifdef PF_K5_TIMERS
+    if (lane == 0) {
+        atomicAdd(&g_k1t[9], total > kQueue ? 1ull : 0ull);
+        atomicAdd(&g_k1t[10], (unsigned long long)total);
+        atomicAdd(&g_k1t[11], 1ull);
+    }
+#endif
     if (total > kQueue) {  // (wave-uniform) the per-lane epilogue, hit lists intact
         if (!active) return 0.0f;
+        if (hin)  // K1u's hit words: into the lane's list, where fas_epilogue reads them
+#pragma unroll
+            for (int i = 0; i < (int)kHitCap; ++i)
+                if ((uint32_t)i < nhl) hl[i * kPairThreads + threadIdx.x] = hw[i];
         return fas_epilogue<true, true>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u, [nh](uint32_t) { return nh; }, tep);
     }
     auto item = [&](uint32_t k) {  // 16-B entry k of the wave's strip (rows of 64 words)
@@ -531,7 +558,7 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     wave_sync();
     for (uint32_t j = (uint32_t)lane; j < total; j += 64u) {  // the wave's terms, one per lane
         uint4 it = *item(j);
-        const double term = item_term(q, st, it);
+        const double term = item_term(q, it, item_norm(st, it));
         it.x = (uint32_t)__double2loint(term);
         it.y = (uint32_t)__double2hiint(term);
         *item(j) = it;
@@ -688,6 +715,46 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
         const uint32_t nh = W.nh;
         return fas_epilogue<false>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
     }
+}
+
+// FAS of pair P = (staged image, slot p) whose record walk K1u already did (packed): its set
+// counts and hit words come from hc[P] / hb[P * kHitCap ..] (64 B, four 16-B loads in flight),
+// and only the epilogue runs here.  An overflowed list (> kHitCap hits) takes the epilogue's
+// record re-walk against the staged image, as after a walk of its own.
+__device__ __forceinline__ float fas_slot_pre(const DevStore& st, const QView& v, int p, bool active, uint64_t P,
+                                              const uint32_t* __restrict__ hb, const uint2* __restrict__ hc,
+                                              uint64_t* twalk = nullptr) {
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
+    uint64_t ro = 0;
+    uint2 wr = make_uint2(0u, 0u);
+    if (active) {
+        h0 = st.hdr0[p];
+        h1 = st.hdr1[p];
+        h2 = st.hdr2[p];
+        ro = st.row_off[p];
+        wr = hc[P];
+    }
+    const uint32_t nh = wr.y > kHitCap ? kHitCap + 1 : wr.y;
+    uint32_t hw[kHitCap];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(hb + P * kHitCap);
+        uint4 r[kHitCap / 4];
+#pragma unroll
+        for (int k = 0; k < (int)kHitCap / 4; ++k)
+            r[k] = (active && nh <= kHitCap && (uint32_t)(4 * k) < nh) ? src[k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < (int)kHitCap / 4; ++k) {
+            hw[4 * k] = r[k].x;
+            hw[4 * k + 1] = r[k].y;
+            hw[4 * k + 2] = r[k].z;
+            hw[4 * k + 3] = r[k].w;
+        }
+    }
+    if (twalk) twalk[0] = clock64();
+    const uint32_t len = active ? record_words(h2, true) : 0u;
+    const RowRec rec{reinterpret_cast<const uint32_t*>(st.rows + ro),
+                     reinterpret_cast<const double*>(st.rows + ro + ((len + 3) >> 2))};
+    return pair_epilogue(v, st, rec, ro, len, h0, h1, h2, wr.x, nh, active, twalk ? twalk + 1 : nullptr, hw);
 }
 
 // ---------------------------------------------------------------- LDS staging
@@ -1136,8 +1203,6 @@ __device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng,
 #ifdef PF_K5_TIMERS
 // profiling build only (make K5T=1): per-phase clock64() sums over every wave, printed by
 // launch_post every 10th launch
-__device__ unsigned long long g_k5t[16];
-__device__ unsigned long long g_k1t[9];  // K1': staging, walk, epilogue, total, dense, assembly, overflow, waves, fas
 #define K5T(slot) do { const uint64_t t_ = clock64(); tacc[slot] += t_ - tprev; tprev = t_; } while (0)
 #else
 #define K5T(slot) do { } while (0)
@@ -1467,12 +1532,16 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
 }
 
 // ---------------------------------------------------------------- K1': pairs
-template <bool PACKED, bool GTAB>
+// PRE (packed, LDS-staged images): the blocks' pairs were walked by K1u; their walk results are
+// read from hb / hc (pair index = the output slot) instead of walking the records here.
+template <bool PACKED, bool GTAB, bool PRE = false>
 __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                         const QImageRef* __restrict__ refs,
                                                         const PairBlock* __restrict__ blocks,
                                                         const int32_t* __restrict__ order,
-                                                        const int32_t* __restrict__ slots, float* __restrict__ out) {
+                                                        const int32_t* __restrict__ slots, float* __restrict__ out,
+                                                        const uint32_t* __restrict__ hb = nullptr,
+                                                        const uint2* __restrict__ hc = nullptr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef PF_K5_TIMERS
     const uint64_t t0 = clock64();
@@ -1494,7 +1563,9 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
     const uint64_t t1 = clock64();
 #endif
     if (!active) p = 0;
-    const float f = fas_slot<PACKED>(st, v, p, active, twp);
+    float f;
+    if constexpr (PRE) f = fas_slot_pre(st, v, p, active, (uint64_t)b.out + (uint64_t)i, hb, hc, twp);
+    else f = fas_slot<PACKED>(st, v, p, active, twp);
     if (active) out[b.out + i] = f;
 #ifdef PF_K5_TIMERS
     const uint64_t t3 = clock64();
@@ -1521,6 +1592,122 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
         atomicAdd(&g_k1t[7], 1ull);
     }
 #endif
+}
+
+// ---------------------------------------------------------------- K1u: union walk
+// A collaborative job's friends g < n of one group score the same candidate span
+// (recommender_graph.cpp:167-180).  K6u merged their records' keys into one table, key -> mask of
+// the friends holding it, so a lane walks its candidate's record ONCE for the whole group (the pair
+// walk walked it once per friend) and writes, for every friend g, what walk_row produces for the
+// pair (g, candidate): the clubs / friends intersection counts (each candidate word counted once
+// per friend holding it, duplicates on the candidate's side as the reference counts them,
+// recommender.cpp:119-128) and the token-hit record words in record order (kHitCap kept; more
+// reads as overflowed, and K1' re-walks that pair against the friend's own image).
+__device__ __forceinline__ uint32_t union_mask(const uint2* tab, int lg, uint32_t hmul, uint32_t key) {
+    const uint32_t x = cuckoo_x(key, hmul);
+    const uint2 e1 = tab[cuckoo_h1(x, lg)];
+    const uint2 e2 = tab[__builtin_amdgcn_ubfe(x, 32u - 2u * (uint32_t)lg, (uint32_t)lg)];
+    return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
+}
+
+struct UnionWalk {
+    uint32_t cnt[kUnionMax];  // per friend: clubs intersections (low 16 bits) + friends << 16
+    uint64_t nh;              // per friend: token hits, 8 bits each (saturating at kHitCap + 1)
+};
+
+// words j0 .. j0 + 3 of the lane's record; SETS: the step may hold club / friend words
+template <bool SETS>
+__device__ __forceinline__ void union_step(UnionWalk& W, const uint4& cw, uint32_t j0, uint32_t nc, uint32_t nset,
+                                           const uint2* tab, int lg, uint32_t hmul, uint32_t* __restrict__ hb,
+                                           uint64_t pbase, uint32_t ostride) {
+    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
+    uint32_t m[4];
+    bool tok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        tok[i] = !SETS || j0 + i >= nset;
+        m[i] = union_mask(tab, lg, hmul, tok[i] ? (kTagTok | (w[i] & 0xFFFFFFu)) : w[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (SETS && !tok[i] && m[i]) {
+            const uint32_t inc = j0 + i < nc ? 1u : 0x10000u;
+#pragma unroll
+            for (int g = 0; g < kUnionMax; ++g) W.cnt[g] += ((m[i] >> g) & 1u) ? inc : 0u;
+        }
+        uint32_t mm = tok[i] ? m[i] : 0u;
+        while (mm) {  // the friends holding this token: its word goes to each one's hit list
+            const uint32_t g = (uint32_t)__builtin_ctz(mm);
+            mm &= mm - 1u;
+            const uint32_t c = (uint32_t)(W.nh >> (8u * g)) & 0xFFu;
+            if (c < kHitCap) hb[(pbase + (uint64_t)g * ostride) * kHitCap + c] = w[i];
+            if (c <= kHitCap) W.nh += 1ull << (8u * g);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPairThreads) void union_walk_kernel(DevStore st, const uint8_t* __restrict__ upool,
+                                                                const UnionJob* __restrict__ ujobs,
+                                                                const PairBlock* __restrict__ blocks,
+                                                                const int32_t* __restrict__ order,
+                                                                const int32_t* __restrict__ slots,
+                                                                uint32_t* __restrict__ hb, uint2* __restrict__ hc) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const PairBlock b = blocks[order ? order[blockIdx.x] : (int)blockIdx.x];
+    const int i = (int)threadIdx.x;
+    const int p = i < b.count ? slots[b.begin + i] : -1;
+    const bool active = p >= 0;
+    if (!__syncthreads_or(active)) return;
+    const UnionJob U = ujobs[b.qimg];
+    stage4(smem, upool + U.tab_off, 8u << U.lg);
+    uint4 h2 = make_uint4(0, 0, 0, 0);
+    uint64_t ro = 0;
+    if (active) {
+        h2 = st.hdr2[p];
+        ro = st.row_off[p];
+    }
+    __syncthreads();
+    const uint2* tab = reinterpret_cast<const uint2*>(smem);
+    const int lg = U.lg;
+    const uint32_t hmul = U.hmul, ostride = (uint32_t)U.ostride;
+    const uint32_t nc = h2.y, nset = active ? h2.y + h2.z : 0u;
+    const uint32_t len = active ? record_words(h2, true) : 0u;
+    const uint64_t pbase = (uint64_t)b.out + (uint64_t)i;
+    UnionWalk W;
+#pragma unroll
+    for (int g = 0; g < kUnionMax; ++g) W.cnt[g] = 0u;
+    W.nh = 0ull;
+    // walk_row's loop: groups of 4 steps, the next group's loads in flight; a lane past its record
+    // reads the padding line (kPadWord and its token key never match)
+    const uint4* base = st.rows + ro;
+    const uint4* pad = st.row_pad;
+    const uint32_t steps = (len + 3) >> 2;
+    const uint32_t smax = wave_max_u32(steps);
+    const uint32_t sset = wave_max_u32((nset + 3) >> 2);
+    auto ld = [&](uint32_t s) { return *(s < steps ? base + s : pad); };
+    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
+    uint32_t s = 0;
+    for (; s < sset; s += 4) {
+        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
+        union_step<true>(W, c0, 4 * s, nc, nset, tab, lg, hmul, hb, pbase, ostride);
+        union_step<true>(W, c1, 4 * s + 4, nc, nset, tab, lg, hmul, hb, pbase, ostride);
+        union_step<true>(W, c2, 4 * s + 8, nc, nset, tab, lg, hmul, hb, pbase, ostride);
+        union_step<true>(W, c3, 4 * s + 12, nc, nset, tab, lg, hmul, hb, pbase, ostride);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    for (; s < smax; s += 4) {
+        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
+        union_step<false>(W, c0, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
+        union_step<false>(W, c1, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
+        union_step<false>(W, c2, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
+        union_step<false>(W, c3, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    if (active) {
+#pragma unroll
+        for (int g = 0; g < kUnionMax; ++g)
+            if (g < U.n) hc[pbase + (uint64_t)g * ostride] = make_uint2(W.cnt[g], (uint32_t)(W.nh >> (8 * g)) & 0xFFu);
+    }
 }
 
 // ---------------------------------------------------------------- K4: collaborative sum
@@ -1638,16 +1825,54 @@ hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;
-        unsigned long long t[9];
+        unsigned long long t[12];
         hipStreamSynchronize(s);
         hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k1t), sizeof(t));
-        if (++calls % 10 == 0 && t[7])
+        if (++calls % 10 == 0 && t[7] && t[11])
+            fprintf(stderr, "k1pt epilogue: fallback waves %.3f, items per lane %.2f\n", (double)t[9] / t[11],
+                    (double)t[10] / (64.0 * t[11]));
+        if (calls % 10 == 0 && t[7])
             fprintf(stderr,
                     "k1pt per wave (clock64): staging=%.0f walk=%.0f epilogue=%.0f (dense=%.0f assembly=%.0f "
                     "overflow=%.0f fas=%.0f) total=%.0f waves=%llu blocks=%d\n",
                     (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[4] / t[7],
                     (double)t[5] / t[7], (double)t[6] / t[7], (double)t[8] / t[7], (double)t[3] / t[7], t[7], nblocks);
-        const unsigned long long z[9] = {0};
+        const unsigned long long z[12] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_k1t), z, sizeof(z));
+    }
+#endif
+    return hipGetLastError();
+}
+
+hipError_t launch_union_walk(const DevStore& st, const uint8_t* upool, const UnionJob* ujobs, uint32_t max_lds,
+                             const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
+                             uint32_t* hb, uint2* hc, hipStream_t s) {
+    if (nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(union_walk_kernel, dim3(nblocks), dim3(kPairThreads), max_lds, s, st, upool, ujobs, blocks, order,
+                       slots, hb, hc);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairs_prewalked(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
+                                  const PairBlock* blocks, int nblocks, const int32_t* slots, const uint32_t* hb,
+                                  const uint2* hc, float* out, hipStream_t s) {
+    if (nblocks <= 0) return hipSuccess;
+    if (!st.packed) return hipErrorInvalidValue;  // K1u walks packed records only
+    hipLaunchKernelGGL((fas_pairs_kernel<true, false, true>), dim3(nblocks), dim3(kPairThreads), max_lds, s, st, pool,
+                       refs_dev, blocks, (const int32_t*)nullptr, slots, out, hb, hc);
+#ifdef PF_K5_TIMERS
+    {
+        static int calls = 0;
+        unsigned long long t[12];
+        hipStreamSynchronize(s);
+        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k1t), sizeof(t));
+        if (++calls % 10 == 0 && t[7])
+            fprintf(stderr,
+                    "k1pt-pre per wave (clock64): staging=%.0f load=%.0f epilogue=%.0f (dense=%.0f assembly=%.0f "
+                    "overflow=%.0f fas=%.0f) total=%.0f waves=%llu blocks=%d\n",
+                    (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[4] / t[7],
+                    (double)t[5] / t[7], (double)t[6] / t[7], (double)t[8] / t[7], (double)t[3] / t[7], t[7], nblocks);
+        const unsigned long long z[12] = {0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_k1t), z, sizeof(z));
     }
 #endif

@@ -17,7 +17,12 @@ constexpr int kValTab = 128;        // completion/age sigmoid tables cover value
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
 constexpr uint32_t kHitCap = 16;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
-constexpr uint32_t kHitSlots = kHitCap + 4;  // + dump slots: the pair walk clamps its list once per 4-word step
+#ifndef PF_QUEUE_EXTRA
+#define PF_QUEUE_EXTRA 0
+#endif
+// + dump slots: the pair walk clamps its list once per 4-word step; the strip of a wave's lists is
+// also K1''s epilogue item queue (kHitSlots * 64 / 4 items of 16 B)
+constexpr uint32_t kHitSlots = kHitCap + 4 + PF_QUEUE_EXTRA;
 constexpr int kMaxHashLog2 = 16;    // cuckoo tables <= 65536 slots (h1/h2 from one 32-bit product)
 constexpr uint32_t kMaxTileSteps = 48;  // a record longer than 48 steps (192 words) is split over lanes
 

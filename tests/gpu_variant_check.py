@@ -1,6 +1,7 @@
 """Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_DEBUG's
-stage_limit and tile_steps once per process/context, so each forced kernel variant (global-memory
-query tables, records split over lanes) runs in its own process.  Exits non-zero on any
+stage_limit, tile_steps and union once per process/context, so each forced kernel variant
+(global-memory query tables, records split over lanes, collaborative pairs through K1u groups)
+runs in its own process.  Exits non-zero on any
 mismatch."""
 import sys
 
@@ -28,6 +29,12 @@ def main():
     if np.count_nonzero(eng.fas_pairs(a, b).view(np.uint32) != orc.fas_pairs(a, b).view(np.uint32)):
         print("pair mismatch", file=sys.stderr)
         return 1
+    # the collaborative recommender (union=1: friend groups walk each candidate record once, K1u)
+    qc = [3, 8, 1000, 15000, 19999]
+    for u, g, r in zip(qc, eng.recommend_collaborative(qc, 10, 1000), orc.collab(qc, 10, 1000)):
+        if list(g[0]) != list(r[0]) or not np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)):
+            print(f"collab mismatch uid={u}", file=sys.stderr)
+            return 1
     print("ok")
     return 0
 

@@ -66,14 +66,15 @@ void add_image(Images& im, const pf::QImageHost& q) {
     auto align = [&](size_t a) { while (im.pool.size() % a) im.pool.push_back(0); };
     align(16);
     pf::QImageRef r{};
-    r.const_off = (uint32_t)im.pool.size();
+    const size_t start = im.pool.size();
+    r.const_off = (uint32_t)(start / 16);
     const uint8_t* cp = reinterpret_cast<const uint8_t*>(&q.c);
     im.pool.insert(im.pool.end(), cp, cp + sizeof(pf::QConst));
-    r.keys_off = (uint32_t)im.pool.size();
+    r.keys_off = (uint32_t)(im.pool.size() - start);
     const uint8_t* kp = reinterpret_cast<const uint8_t*>(q.keys.data());
     im.pool.insert(im.pool.end(), kp, kp + q.keys.size() * 8);
     align(16);
-    r.vals_off = (uint32_t)im.pool.size();
+    r.vals_off = (uint32_t)(im.pool.size() - start);
     const uint8_t* vp = reinterpret_cast<const uint8_t*>(q.vals.data());
     im.pool.insert(im.pool.end(), vp, vp + q.vals.size() * sizeof(pf::QVal));
     const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
@@ -94,10 +95,10 @@ size_t plan_images(Images& im, const std::vector<pf::QImageHost>& qs) {
     size_t o = 0;
     for (const auto& q : qs) {
         pf::QImageRef r{};
-        r.const_off = (uint32_t)o;
-        r.keys_off = (uint32_t)(o + sizeof(pf::QConst));
+        r.const_off = (uint32_t)(o / 16);
+        r.keys_off = (uint32_t)sizeof(pf::QConst);
         r.vals_off = (uint32_t)a16(r.keys_off + q.keys.size() * 8);
-        o = a16(r.vals_off + q.vals.size() * sizeof(pf::QVal));
+        o = a16(o + r.vals_off + q.vals.size() * sizeof(pf::QVal));
         const size_t kv = q.keys.size() * 8 + q.vals.size() * sizeof(pf::QVal);
         r.lds_bytes = kv <= stage_limit() ? (uint32_t)kv : 0u;
         im.gtab = im.gtab || r.lds_bytes == 0;
@@ -113,12 +114,14 @@ void fill_images(const Images& im, const std::vector<pf::QImageHost>& qs, uint8_
     par_jobs(qs.size(), [&](size_t i) {
         const pf::QImageHost& q = qs[i];
         const pf::QImageRef& r = im.refs[i];
-        const size_t kend = r.keys_off + q.keys.size() * 8, vend = r.vals_off + q.vals.size() * sizeof(pf::QVal);
-        const size_t next = i + 1 < qs.size() ? im.refs[i + 1].const_off : total;
-        std::memcpy(dst + r.const_off, &q.c, sizeof(pf::QConst));
-        if (!q.keys.empty()) std::memcpy(dst + r.keys_off, q.keys.data(), q.keys.size() * 8);
-        std::memset(dst + kend, 0, r.vals_off - kend);
-        if (!q.vals.empty()) std::memcpy(dst + r.vals_off, q.vals.data(), q.vals.size() * sizeof(pf::QVal));
+        const size_t b = (size_t)r.const_off * 16;  // byte offsets from the pool start
+        const size_t ko = b + r.keys_off, vo = b + r.vals_off;
+        const size_t kend = ko + q.keys.size() * 8, vend = vo + q.vals.size() * sizeof(pf::QVal);
+        const size_t next = i + 1 < qs.size() ? (size_t)im.refs[i + 1].const_off * 16 : total;
+        std::memcpy(dst + b, &q.c, sizeof(pf::QConst));
+        if (!q.keys.empty()) std::memcpy(dst + ko, q.keys.data(), q.keys.size() * 8);
+        std::memset(dst + kend, 0, vo - kend);
+        if (!q.vals.empty()) std::memcpy(dst + vo, q.vals.data(), q.vals.size() * sizeof(pf::QVal));
         std::memset(dst + vend, 0, next - vend);
     }, 64);
 }
@@ -654,6 +657,12 @@ void pf_close(pf_ctx* c) {
         if (st.done) (void)hipEventDestroy(st.done);
         if (st.p) (void)hipHostFree(st.p);
     }
+    if (c->jb.aux) {
+        (void)hipStreamSynchronize(c->jb.aux);
+        (void)hipStreamDestroy(c->jb.aux);
+    }
+    if (c->jb.ev_fork) (void)hipEventDestroy(c->jb.ev_fork);
+    if (c->jb.ev_join) (void)hipEventDestroy(c->jb.ev_join);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

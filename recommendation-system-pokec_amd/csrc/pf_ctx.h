@@ -98,6 +98,15 @@ struct JobsState {
     std::vector<uint32_t> img_stamp;             // per idx: the layout pass that last gave it an image ...
     std::vector<int32_t> img_pos;                // ... and that image's index (no hash map per call)
     uint32_t img_gen = 0;
+    // resident query images (built at open, pf_jobs_plan.cpp build_resident_images): every user's
+    // K6 image in one pool, so no call builds images; pimg_off[idx] = its byte offset (16-aligned)
+    bool pimg = false;
+    DBuf d_pimg;
+    std::vector<int64_t> pimg_off;
+    // a chunk's K3 gathers (+ the dispatch orders) run on aux beside its K6 images on the context's
+    // stream (both latency-bound, independent), joined before the pair kernel
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool union_on = true;                        // collaborative friend groups walk each record once (K6u / K1u;
                                                  // PF_DEBUG union=0: every pair walks its own record)
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row

@@ -73,6 +73,101 @@ int pow2_lg(int64_t n) {
     return lg;
 }
 
+// Every user's query image (K6's layout: QConst | table | values) built once at open into one
+// resident pool, when it fits a third of the free HBM (at 1.63M users ~10^4 B each: a few
+// percent of 288 GB): a job batch then references the images its users and friends need instead
+// of building them (K6 left the per-call path: ~70 us of a 64-user collaborative step).  The
+// images are a function of the profiles and the idf fixed at open (pf_set_adj changes rows of
+// adj_list, which no image holds: the pair images carry no exclusions).  PF_DEBUG
+// resident_images=0 keeps the per-call builds.
+int build_resident_images(pf_ctx* c) {
+    auto& J = c->jb;
+    const HostCorpus& hc = c->hc;
+    const bool packed = c->hs.packed;
+    J.pimg = false;
+    if (debug_long("resident_images", 1) == 0 || hc.n == 0) return PF_OK;
+    const int32_t n = hc.n;
+    const int lge = lg_for(0);
+    const size_t ntab = packed ? 1u : 3u;
+    auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
+    std::vector<int64_t> off((size_t)n + 1, 0);
+    par_jobs((size_t)n, [&](size_t i) {
+        const int lg = J.img_lg[i];
+        off[i + 1] = lg ? (int64_t)(a16z(sizeof(QConst) + ((ntab << lg) + ((size_t)1 << lge)) * 8) +
+                                    a16z((size_t)ntok_of((int32_t)i) * sizeof(QVal)))
+                        : 0;
+    }, 1 << 14);
+    for (int32_t i = 0; i < n; ++i) off[i + 1] += off[i];
+    const size_t total = (size_t)off[n];
+    size_t freeb = 0, totb = 0;
+    if (hipMemGetInfo(&freeb, &totb) != hipSuccess) return PF_OK;
+    if (total == 0 || total > freeb / 3 || total >= ((size_t)1 << 36)) return PF_OK;  // 16-B units in 32 bits
+    HIPCHK(c, J.d_pimg.ensure(total));
+    // batches of images whose offsets fit K6's 32-bit pool offsets; K6 wants each batch's images
+    // ordered small LDS builds | large LDS builds | global-memory builds
+    DBuf d_ij, d_scr, d_fail;
+    HIPCHK(c, d_fail.ensure(16));
+    HIPCHK(c, hipMemsetAsync(d_fail.p, 0, 16, c->stream));
+    const size_t kBatchBytes = (size_t)1 << 31;
+    int32_t i0 = 0;
+    while (i0 < n) {
+        int32_t i1 = i0;
+        while (i1 < n && (size_t)(off[i1 + 1] - off[i0]) <= kBatchBytes && i1 - i0 < (1 << 18)) ++i1;
+        std::vector<ImgJob> ij;
+        ij.reserve((size_t)(i1 - i0));
+        std::vector<uint8_t> cls;
+        cls.reserve((size_t)(i1 - i0));
+        for (int32_t idx = i0; idx < i1; ++idx) {
+            const int lg = J.img_lg[idx];
+            if (!lg) continue;
+            ImgJob m{};
+            m.idx = idx;
+            m.lg = lg;
+            m.lge = lge;
+            m.dlg = pow2_lg(2 * (int64_t)J.img_nset[idx] + 2);
+            m.rows = J.img_rows[idx];
+            m.const_off = (uint32_t)(off[idx] - off[i0]);
+            m.keys_off = (uint32_t)(m.const_off + sizeof(QConst));
+            m.vals_off = (uint32_t)(m.const_off + a16z(sizeof(QConst) + ((ntab << lg) + ((size_t)1 << lge)) * 8));
+            const uint32_t need = qimage_lds(lg, lge, m.dlg, (uint32_t)(J.img_nset[idx] + ntok_of(idx)), packed);
+            cls.push_back(need == 0 ? 2 : (need <= kImgLdsSmall ? 0 : 1));
+            ij.push_back(m);
+        }
+        std::vector<ImgJob> ord;
+        ord.reserve(ij.size());
+        int nc[3] = {0, 0, 0};
+        int64_t scr = 0;
+        for (int k = 0; k < 3; ++k)
+            for (size_t x = 0; x < ij.size(); ++x)
+                if (cls[x] == k) {
+                    ImgJob m = ij[x];
+                    m.scr_off = scr;
+                    if (k == 2) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[m.idx] + ntok_of(m.idx));
+                    ord.push_back(m);
+                    ++nc[k];
+                }
+        if (!ord.empty()) {
+            HIPCHK(c, upload(c, d_ij, ord));
+            HIPCHK(c, d_scr.ensure((size_t)std::max<int64_t>(scr, 1) * 4));
+            HIPCHK(c, launch_qimages(c->ds, J.js, d_ij.as<ImgJob>(), nc[0], nc[1], nc[2], J.d_pimg.as<uint8_t>() + off[i0],
+                                     d_scr.as<uint32_t>(), d_fail.as<int32_t>(), c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));  // d_ij / d_scr are reused by the next batch
+        }
+        i0 = i1;
+    }
+    int32_t failed = 0;
+    HIPCHK(c, hipMemcpy(&failed, d_fail.p, 4, hipMemcpyDeviceToHost));
+    if (failed) {  // a table that did not converge: the per-call builds report it for the calls that need it
+        if (J.d_pimg.p) (void)hipFree(J.d_pimg.p);
+        J.d_pimg.p = nullptr;
+        J.d_pimg.cap = 0;
+        return PF_OK;
+    }
+    J.pimg_off.swap(off);
+    J.pimg = true;
+    return PF_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- open
@@ -293,8 +388,11 @@ int jobs_open(pf_ctx* c) {
     J.view_over_n = 0;
     J.nodes_dirty = false;
     J.union_on = packed && debug_long("union", 0) != 0;
-    J.ok = true;
     sc.lap("handles");
+    const int rc = build_resident_images(c);
+    if (rc != PF_OK) return rc;
+    sc.lap(J.pimg ? "resident images" : "resident images (off)");
+    J.ok = true;
     return PF_OK;
 }
 
@@ -725,13 +823,16 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     if (W.done == nullptr) HIPCHK(c, hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
     const hipStream_t s = c->stream;
     if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
-    // ---- images (pf_api.cpp plan_images layout); the ones K6 builds in LDS first
+    // ---- images (pf_api.cpp plan_images layout).  Resident (J.pimg, built at open): every
+    // user's image already sits in J.d_pimg and the batch only references them.  Otherwise K6
+    // builds the batch's images, the ones it builds in LDS first.
+    const bool resident = J.pimg;
     const uint32_t ntab = packed ? 1u : 3u;
     auto dlg_of = [&](int32_t idx) { return pow2_lg(2 * (int64_t)J.img_nset[idx] + 2); };
     // K6 builds the images in three launches: small LDS builds (<= kImgLdsSmall, many workgroups
     // per CU), large LDS builds (<= kImgLds), hub users in global memory
     int n_lds = 0, n_small = 0;
-    {
+    if (!resident) {
         std::vector<int32_t> order(img_idx.size()), pos(img_idx.size());
         std::vector<uint8_t> cls(img_idx.size());  // 0 small, 1 large, 2 global
         for (size_t k = 0; k < img_idx.size(); ++k) {
@@ -750,7 +851,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
         for (PairBlock& pb : pblocks) pb.qimg = pos[pb.qimg];
     }
-    std::vector<ImgJob> ij(img_idx.size());
+    std::vector<ImgJob> ij(resident ? 0 : img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
     uint32_t max_lds = 0;
     bool gtab = false;
@@ -761,24 +862,28 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         const int lg = J.img_lg[idx];
         if (lg == 0) return c->fail(PF_EUNSUPP, "query hash table too large");
         const int64_t ntok = ntok_of(idx);
-        ImgJob& m = ij[k];
-        m.idx = idx;
-        m.lg = lg;
-        m.lge = lge;
-        m.dlg = dlg_of(idx);
-        m.rows = J.img_rows[idx];
-        m.const_off = (uint32_t)ipool;
-        m.keys_off = (uint32_t)(ipool + sizeof(QConst));
         const size_t nkeys = ((size_t)ntab << lg) + ((size_t)1 << lge);
-        m.vals_off = (uint32_t)a16z(m.keys_off + nkeys * 8);
-        ipool = a16z(m.vals_off + (size_t)ntok * sizeof(QVal));
-        if (ipool >= (size_t)UINT32_MAX) return c->fail(PF_EUNSUPP, "query images of one batch exceed 4 GB");
-        m.scr_off = scr;
-        if ((int)k >= n_lds) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 items
         QImageRef& r = refs[k];
-        r.const_off = m.const_off;
-        r.keys_off = m.keys_off;
-        r.vals_off = m.vals_off;
+        r.keys_off = (uint32_t)sizeof(QConst);
+        r.vals_off = (uint32_t)a16z(sizeof(QConst) + nkeys * 8);
+        if (resident) {
+            r.const_off = (uint32_t)(J.pimg_off[idx] >> 4);
+        } else {
+            ImgJob& m = ij[k];
+            m.idx = idx;
+            m.lg = lg;
+            m.lge = lge;
+            m.dlg = dlg_of(idx);
+            m.rows = J.img_rows[idx];
+            m.const_off = (uint32_t)ipool;
+            m.keys_off = (uint32_t)(ipool + r.keys_off);
+            m.vals_off = (uint32_t)(ipool + r.vals_off);
+            r.const_off = (uint32_t)(ipool >> 4);
+            ipool = a16z(m.vals_off + (size_t)ntok * sizeof(QVal));
+            if (ipool >= (size_t)UINT32_MAX) return c->fail(PF_EUNSUPP, "query images of one batch exceed 4 GB");
+            m.scr_off = scr;
+            if ((int)k >= n_lds) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 items
+        }
         const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
         r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;
         gtab = gtab || r.lds_bytes == 0;
@@ -854,8 +959,11 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.d_fl.reserve(nE * 4));
     HIPCHK(c, W.d_ht.reserve((size_t)std::max<int64_t>(HT, 1) * 4));
     HIPCHK(c, W.d_seq.reserve((size_t)std::max<int64_t>(SEQ, 1) * 4));
-    HIPCHK(c, W.d_img.reserve(std::max<size_t>(ipool, 16)));
-    HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
+    if (!resident) {
+        HIPCHK(c, W.d_img.reserve(std::max<size_t>(ipool, 16)));
+        HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
+    }
+    const uint8_t* ipl = resident ? J.d_pimg.as<uint8_t>() : W.d_img.as<uint8_t>();  // the batch's image pool
     if (!ujobs.empty()) {  // K1u's results per pair index (E: every output slot of the chunk)
         HIPCHK(c, W.d_upool.reserve(upool));
         HIPCHK(c, W.d_hb.reserve(nE * kHitCap * 4));
@@ -871,17 +979,28 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             W.acc_jobs = want;
         }
     }
-    // ---- the stages, in stream order
-    HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds, W.d_img.as<uint8_t>(),
-                             W.d_scr.as<uint32_t>(), d_fail, s));
+    // ---- the stages, in stream order; the gathers and dispatch orders fork onto the aux stream
+    // (after the plan upload) and join before the pair kernel, beside the images
+    if (J.aux == nullptr) {
+        HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming));
+    }
+    HIPCHK(c, hipEventRecord(J.ev_fork, s));
+    HIPCHK(c, hipStreamWaitEvent(J.aux, J.ev_fork, 0));
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
-                            d_ncand, s));
-    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, s));
-    if (!ujobs.empty()) {
+                            d_ncand, J.aux));
+    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, J.aux));
+    if (!ujobs.empty())
+        HIPCHK(c, launch_order_pairs(d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), hc.n, d_word, J.aux));
+    HIPCHK(c, hipEventRecord(J.ev_join, J.aux));
+    if (!resident)
+        HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds,
+                                 W.d_img.as<uint8_t>(), W.d_scr.as<uint32_t>(), d_fail, s));
+    if (!ujobs.empty())
         HIPCHK(c, launch_unions(c->ds, J.js, d_uj, (int)ujobs.size(), max_ulds, W.d_upool.as<uint8_t>(), d_fail, s));
-        HIPCHK(c, launch_order_pairs(d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), hc.n, d_word, s));
-    }
+    HIPCHK(c, hipStreamWaitEvent(s, J.ev_join, 0));
     const bool any_pairs = !blocks.empty() || !pblocks.empty();
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && any_pairs) {
@@ -900,9 +1019,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         HIPCHK(c, launch_union_walk(c->ds, W.d_upool.as<uint8_t>(), d_uj, max_wlds, d_wb, (int)wblocks.size(), d_word,
                                     W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(), s));
     }
-    HIPCHK(c, launch_pairs(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, gtab, d_blk, (int)blocks.size(), d_ord,
+    HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, max_lds, gtab, d_blk, (int)blocks.size(), d_ord,
                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
-    HIPCHK(c, launch_pairs_prewalked(c->ds, W.d_img.as<uint8_t>(), d_refs, max_lds, d_pb, (int)pblocks.size(),
+    HIPCHK(c, launch_pairs_prewalked(c->ds, ipl, d_refs, max_lds, d_pb, (int)pblocks.size(),
                                      W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(),
                                      W.d_fl.as<float>(), s));
     if (pe1) {
@@ -919,9 +1038,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (const auto* bl : {&blocks, &pblocks})
             for (const PairBlock& pb : *bl) {  // the staged image per pair block (QConst + tables)
                 const QImageRef& r = refs[pb.qimg];
-                J.st_img_bytes += (int64_t)(r.vals_off - r.const_off) +
-                                  (int64_t)(ij[pb.qimg].idx >= 0 ? (hc.tok_off[(size_t)(ij[pb.qimg].idx + 1) * hc.T] -
-                                                                   hc.tok_off[(size_t)ij[pb.qimg].idx * hc.T]) * 16 : 0);
+                const int32_t idx = img_idx[pb.qimg];
+                J.st_img_bytes += (int64_t)r.vals_off + ntok_of(idx) * (int64_t)sizeof(QVal);
             }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched

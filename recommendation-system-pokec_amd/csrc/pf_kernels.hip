@@ -793,17 +793,18 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     if constexpr (!GTAB) {
         // the sizes from the image in global memory; QConst | tables | values are contiguous in
         // every image pool (tables of >= 2^4 8-B entries keep the values 16-B aligned)
-        const QConst* g = reinterpret_cast<const QConst*>(pool + r.const_off);
+        const uint8_t* base = pool + (size_t)r.const_off * 16u;
+        const QConst* g = reinterpret_cast<const QConst*>(base);
         const uint32_t kb = 8u * (g->excl_off + (1u << g->lg_excl)), vb = (uint32_t)g->n_vals * 16u;
-        if (r.keys_off == r.const_off + sizeof(QConst) && r.vals_off == r.keys_off + kb) {
+        if (r.keys_off == sizeof(QConst) && r.vals_off == r.keys_off + kb) {
             stage4(smem, g, (uint32_t)sizeof(QConst) + kb + vb);
         } else {
             stage4(smem, g, sizeof(QConst));
-            stage4(smem + sizeof(QConst), pool + r.keys_off, kb);
-            stage4(smem + sizeof(QConst) + kb, pool + r.vals_off, vb);
+            stage4(smem + sizeof(QConst), base + r.keys_off, kb);
+            stage4(smem + sizeof(QConst) + kb, base + r.vals_off, vb);
         }
     } else {
-        stage(smem, pool + r.const_off, sizeof(QConst));
+        stage(smem, pool + (size_t)r.const_off * 16u, sizeof(QConst));
     }
     __syncthreads();
     const QConst* q = reinterpret_cast<const QConst*>(smem);
@@ -820,8 +821,8 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
         v.vals = reinterpret_cast<const QVal*>(p + kb);
         p += kb + vb;
     } else {
-        v.tab = reinterpret_cast<const uint2*>(pool + r.keys_off);
-        v.vals = reinterpret_cast<const QVal*>(pool + r.vals_off);
+        v.tab = reinterpret_cast<const uint2*>(pool + (size_t)r.const_off * 16u + r.keys_off);
+        v.vals = reinterpret_cast<const QVal*>(pool + (size_t)r.const_off * 16u + r.vals_off);
     }
     v.hits = p;
     p += (size_t)q->n_hits_max * blockDim.x;  // n_hits_max = bytes per lane of the hit list

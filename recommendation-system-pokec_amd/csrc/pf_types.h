@@ -120,10 +120,12 @@ struct QVal {
 };
 
 // One query image in device memory: QConst + tables[excl_off + 2^lg_excl] + vals[n_vals].
+// The image starts at pool + 16 * const_off (pools up to 64 GB: the job pipeline keeps every
+// user's image resident); its tables at byte offsets keys_off / vals_off from that start.
 struct QImageRef {
-    uint32_t const_off;   // byte offset of QConst in the image pool
-    uint32_t keys_off;    // byte offset of the key table
-    uint32_t vals_off;    // byte offset of the value table
+    uint32_t const_off;   // image start in 16-B units of the image pool (QConst first)
+    uint32_t keys_off;    // byte offset of the key table from the image start
+    uint32_t vals_off;    // byte offset of the value table from the image start
     uint32_t lds_bytes;   // bytes of keys+vals staged in LDS (0 = probe global memory)
 };
 

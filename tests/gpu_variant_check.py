@@ -1,5 +1,5 @@
 """Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_DEBUG's
-stage_limit, tile_steps and union once per process/context, so each forced kernel variant
+stage_limit, tile_steps, union and resident_images once per process/context, so each forced kernel variant
 (global-memory query tables, records split over lanes, collaborative pairs through K1u groups)
 runs in its own process.  Exits non-zero on any
 mismatch."""

@@ -391,7 +391,7 @@ int jobs_open(pf_ctx* c) {
     sc.lap("handles");
     const int rc = build_resident_images(c);
     if (rc != PF_OK) return rc;
-    sc.lap(J.pimg ? "resident images" : "resident images (off)");
+    sc.lap(J.pimg ? ("resident images, " + std::to_string(J.d_pimg.cap >> 20) + " MiB").c_str() : "resident images (off)");
     J.ok = true;
     return PF_OK;
 }
@@ -932,7 +932,16 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_ord = a16z(o_res + res_b);  // the pair / walk blocks' dispatch orders (device-written)
     const size_t o_word = a16z(o_ord + std::max<size_t>(blocks.size(), 1) * 4);
     HIPCHK(c, W.d_plan.reserve(o_word + std::max<size_t>(wblocks.size(), 1) * 4));
-    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, s));
+    if (J.aux == nullptr) {
+        HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming));
+    }
+    // the plan goes up on the aux stream, where this chunk's gathers follow it at once: they run
+    // beside the previous chunk's pair kernel (their slot's buffers were released when that slot's
+    // previous chunk was unpacked); r3ab: cfg 3 +3 % over forking them from the context's stream
+    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, J.aux));
+    HIPCHK(c, hipEventRecord(J.ev_fork, J.aux));
     uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
     const int32_t* d_p32 = reinterpret_cast<const int32_t*>(d + o_p32);
@@ -979,15 +988,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             W.acc_jobs = want;
         }
     }
-    // ---- the stages, in stream order; the gathers and dispatch orders fork onto the aux stream
-    // (after the plan upload) and join before the pair kernel, beside the images
-    if (J.aux == nullptr) {
-        HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming));
-    }
-    HIPCHK(c, hipEventRecord(J.ev_fork, s));
-    HIPCHK(c, hipStreamWaitEvent(J.aux, J.ev_fork, 0));
+    // ---- the stages, in stream order; the gathers and dispatch orders run on the aux stream and
+    // join before the pair kernel, beside the images
+    HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, unions, fail word) is up
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
                             d_ncand, J.aux));

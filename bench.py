@@ -336,14 +336,17 @@ def cfg3_queries(users, warm, steps, rank=0, world=1):
     return [qs[rank::world] for qs in qstream]
 
 
-def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True):
+ASYNC_DEPTH = 3  # asynchronous calls kept in flight (the engine's workspace slots, pf_ctx.h kJobSlots)
+
+
+def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True, depth=ASYNC_DEPTH):
     """cfg 3 (BASELINE configs[2]): collaborative FoF propagation top-10 on the full corpus.  A
     step = recommend_collaborative(u, 10, 10000) for a batch of 64 seeded users (this rank's share
     at N > 1), through the device job pipeline (K3 gather, K6 images, K1' pairs, K4' sums, K8
     top-k) and back to the host.  Returns the timing and counters: pair-FAS scored (SURVEY D3's
     cfg-3 unit, |F| + |F|.|C| per user) and the pair kernel's HIP-event time per launch (its
     roofline).  One context: the steps go through the asynchronous calls (pf_recommend_collab_async,
-    two in flight), so step i + 1 is planned on the host while step i runs on the device
+    three in flight), so steps i + 1 and i + 2 are planned on the host while step i runs on the device
     (use_async=False: the synchronous calls).  With C = len(engs) > 1 contexts, step i runs on
     context i % C from its own host thread (ctypes releases the GIL)."""
     eng = engs[0]
@@ -365,7 +368,7 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True)
             pend = []
             for i in range(warm + t, warm + steps, C):
                 pend.append(e.recommend_collaborative_async(mine[i], TOPK, CFG3_LIMIT))
-                if len(pend) == 2:
+                if len(pend) == depth:
                     n += sum(len(o[0]) for o in e.wait(pend.pop(0)))
             for p in pend:
                 n += sum(len(o[0]) for o in e.wait(p))
@@ -448,7 +451,7 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, open_s):
     strong scaling); value = FAS pairs scored / s."""
     steps, warm = args.steps, args.warmup
     mine = cfg3_queries(args.users, warm, steps, rank, world)
-    st = measure_cfg3(engs, mine, warm, steps, dist, torch, use_async=not args.sync_calls)
+    st = measure_cfg3(engs, mine, warm, steps, dist, torch, use_async=not args.sync_calls, depth=args.async_depth)
     C = len(engs)
     f = cfg3_fields(st, steps, pmc)
     rec = {
@@ -461,7 +464,7 @@ def run_cfg3(args, engs, pf, torch, dist, world, rank, base, pmc, open_s):
                    "workload_key": f"cfg3_collab_top{TOPK}_{args.users}users_q{CFG3_QUERIES}_limit{CFG3_LIMIT}_world{world}",
                    "n_users": args.users, "queries_per_step": CFG3_QUERIES, "topk": TOPK, "limit": CFG3_LIMIT,
                    "parallelism": f"query-users x{world}" + (f", {C} engine contexts per GPU" if C > 1 else "")
-                                  + (", asynchronous calls (2 in flight)" if st["async"] else "")},
+                                  + (f", asynchronous calls ({args.async_depth} in flight)" if st["async"] else "")},
         **f, "open_s": open_s,
     }
     if rank == 0 and world == 1 and base is not None:
@@ -738,6 +741,8 @@ def main():
                          "3 for cfg5 (r2fk: 1 -> 39.7k, 2 -> 51.5k, 3 -> 61.7k users/s)")
     ap.add_argument("--sync-calls", action="store_true",
                     help="cfg3: the synchronous recommender calls instead of the asynchronous ones")
+    ap.add_argument("--async-depth", type=int, default=ASYNC_DEPTH,
+                    help="cfg3: asynchronous calls kept in flight (1..3, the engine's workspace slots)")
     ap.add_argument("--cfg5-batch", type=int, default=CFG5_USERS,
                     help="cfg5: users per device pass of the driver (r2o: 128 -> 15.1k, 512 -> 17.2k, 2048 -> "
                          "31.8k users/s; a 2048-user pass runs as three pipelined chunks)")

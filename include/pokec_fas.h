@@ -171,8 +171,8 @@ int pf_recommend_clubs(pf_ctx* ctx, const int32_t* query_uid, int32_t nq,
  * outputs (same layout as above) are written when pf_wait(ctx, ticket) returns, so the caller
  * keeps its buffers alive until then.  While call i runs on the device the host can plan call
  * i + 1: one context then keeps the GPU busy where the synchronous calls leave it idle during
- * planning (what several contexts per GPU were used for).  At most two calls are in flight: a
- * third waits for the oldest itself.  Any other call on the context (synchronous recommenders,
+ * planning (what several contexts per GPU were used for).  At most three calls are in flight: a
+ * fourth waits for the oldest itself.  Any other call on the context (synchronous recommenders,
  * pf_set_adj, pf_jobs_stats_*) first completes the pending ones; pf_close drops them unwritten.
  * pf_wait(ticket) completes every call up to that ticket, in launch order; it returns the first
  * failure among them (PF_OK for a ticket already completed).

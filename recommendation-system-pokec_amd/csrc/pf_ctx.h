@@ -79,6 +79,11 @@ inline void rank(Ranked& v, int topk) {  // recommender_graph.cpp:97-101
 }
 
 
+// workspace slots: two for a synchronous call's double-buffered chunks, all for asynchronous calls
+// in flight (three, so the host plans two calls ahead of the device and a short call's pair
+// kernel does not leave the device waiting for the next plan)
+constexpr int kJobSlots = 3;
+
 // The device job pipeline's state (pf_jobs.cpp): the graph and image-builder inputs on the
 // device, their host mirrors, and the per-call workspaces.
 struct JobsState {
@@ -126,6 +131,7 @@ struct JobsState {
         DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr;  // d_plan: the plan, then the results
         DBuf d_upool, d_hb, d_hc;  // K6u union tables; K1u walk results (hit words, counts) per pair index
         DBuf d_acc;                // clubs accumulators (zero between uses)
+        DBuf d_parts;              // K4''s per-block top-k lists (the fused collaborative top-k)
         int64_t acc_jobs = 0;      // clubs jobs the accumulators hold
         PinBuf h_plan, h_out;
         hipEvent_t done = nullptr;  // recorded after the chunk's result copies
@@ -139,9 +145,9 @@ struct JobsState {
         std::vector<size_t> full, full_off;
         size_t o_cnt = 0, o_keys = 0, o_fail = 0;
         int ktop = 1;
-    } ws[2];
+    } ws[kJobSlots];
     // asynchronous calls (pf_recommend_*_async): each holds one workspace slot from its launch
-    // until pf_wait unpacks it, so at most two are in flight; their jobs live here meanwhile
+    // until pf_wait unpacks it, so at most kJobSlots are in flight; their jobs live here meanwhile
     struct Pending {
         uint64_t ticket = 0;
         int slot = 0;

@@ -31,8 +31,11 @@ uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed);
 hipError_t launch_unions(const DevStore& st, const DevJobsStore& g, UnionJob* uj, int n, uint32_t max_lds, uint8_t* upool,
                          int32_t* fail, hipStream_t s);
 uint32_t union_lds(int dlg, int words);
+// K4' (+ the fused top-k of jobs with topk <= kMaxTopK: parts = gridDim.x * k keys per job,
+// tickets = one zeroed counter per job, out = the chunk's key rows, k = their width)
 hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
-                         const float* pout, const int32_t* cand_slot, float* score, hipStream_t s);
+                         const float* pout, const int32_t* cand_slot, float* score, const int32_t* ids, uint64_t* parts,
+                         unsigned int* tickets, uint64_t* out, int k, hipStream_t s);
 hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* jobs, const int32_t* jix, int njobs,
                         const int32_t* pool, const int64_t* pool64, const float* pout, double* acc,
                         float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);

@@ -747,10 +747,24 @@ uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed) {
 // 64 friend positions (16 each, loads in flight together) into LDS, then wave 0 adds them per
 // candidate in position order.  A hub's long friend row costs one memory round trip per 64
 // positions over four waves instead of one per few positions on a single lane.
+// A job with topk <= kMaxTopK also gets its top-k here (K8's keys, K8 skips the job): each block
+// publishes the k best keys of its 64 candidates (write-through stores, scan_tail's hand-off),
+// takes a ticket, and the job's last block merges every block's list into out[jn * k ..].
 constexpr int kCollabCands = 64, kCollabTile = 64;
+
+__device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __restrict__ jobs, const int32_t* __restrict__ jix,
                                                              const int32_t* __restrict__ pool, const float* __restrict__ pout,
-                                                             const int32_t* __restrict__ cand_slot, float* __restrict__ score) {
+                                                             const int32_t* __restrict__ cand_slot, float* __restrict__ score,
+                                                             const int32_t* __restrict__ ids, uint64_t* __restrict__ parts,
+                                                             unsigned int* __restrict__ tickets, uint64_t* __restrict__ out,
+                                                             int k) {
     static_assert(kJobThreads == 4 * kCollabCands && kCollabTile % 4 == 0, "four waves of 64 candidates");
     __shared__ double P[kCollabTile][kCollabCands];
     const DevJob J = jobs[jix[blockIdx.y]];
@@ -781,6 +795,23 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
         __syncthreads();
     }
     if (g == 0 && live) score[J.out_off + c] = (float)s;
+    if (J.topk > kMaxTopK || g != 0) return;  // K8 ranks this job (or another wave's work is done)
+    // the fused top-k (wave 0): score_key as K8 builds it from the stored float and the id
+    const int jn = jix[blockIdx.y];
+    uint64_t list = ~0ull;
+    topk_push(list, live ? score_key((float)s, ids[J.out_off + c]) : ~0ull, k, cl);
+    const int nb = (J.cap + kCollabCands - 1) / kCollabCands;
+    uint64_t* jp = parts + (size_t)blockIdx.y * gridDim.x * k;
+    if (cl < k) st_agent64(jp + (size_t)blockIdx.x * k + cl, list);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = 0;
+    if (cl == 0) t = atomicAdd(&tickets[blockIdx.y], 1u);
+    t = (unsigned)__shfl((int)t, 0);
+    if (t != (unsigned)nb - 1u) return;
+    uint64_t acc = ~0ull;
+    const int n = nb * k;
+    for (int b = 0; b < n; b += 64) topk_push(acc, b + cl < n ? ld_agent64(jp + b + cl) : ~0ull, k, cl);
+    if (cl < k) out[(size_t)jn * k + cl] = acc;
 }
 
 // ---------------------------------------------------------------- K7: clubs
@@ -1138,12 +1169,14 @@ hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJo
 }
 
 hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
-                         const float* pout, const int32_t* cand_slot, float* score, hipStream_t s) {
+                         const float* pout, const int32_t* cand_slot, float* score, const int32_t* ids, uint64_t* parts,
+                         unsigned int* tickets, uint64_t* out, int k, hipStream_t s) {
     if (njobs <= 0 || max_cap <= 0) return hipSuccess;
+    const int gx = (max_cap + kCollabCands - 1) / kCollabCands;
     for (int b = 0; b < njobs; b += 65535) {
         const int nb = njobs - b < 65535 ? njobs - b : 65535;
-        hipLaunchKernelGGL(collab_kernel, dim3((max_cap + kCollabCands - 1) / kCollabCands, nb), dim3(kJobThreads), 0, s,
-                           jobs, jix + b, pool, pout, cand_slot, score);
+        hipLaunchKernelGGL(collab_kernel, dim3(gx, nb), dim3(kJobThreads), 0, s, jobs, jix + b, pool, pout, cand_slot,
+                           score, ids, parts + (size_t)b * gx * k, tickets + b, out, k);
     }
     return hipGetLastError();
 }

@@ -672,7 +672,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(kPairSpan, count - x),
                                        (int32_t)(out + x)});
     };
-    std::vector<int32_t> jix_collab, jix_clubs, jix_topk;
+    std::vector<int32_t> jix_collab, jix_clubs, jix_topk, jix_fused;
     int max_cap_collab = 0, ktop = 1;
     // collaborative friend groups (K6u / K1u): their pairs' walks happen once per group in K1u,
     // and K1' runs only their epilogues (pblocks)
@@ -813,7 +813,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             }
         }
         if (p.kind != kDjRawGraph && p.kind != kDjRawCollab && jobs[i].topk <= kDevTopK) {
-            jix_topk.push_back(jn);
+            // a collaborative job with candidates gets its top-k inside K4' (collab_kernel)
+            (p.kind == kDjCollab && p.cap > 0 ? jix_fused : jix_topk).push_back(jn);
             ktop = std::max(ktop, jobs[i].topk);
         }
         dj.push_back(d);
@@ -909,7 +910,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_jc = a16z(o_pb + pblocks.size() * sizeof(PairBlock));
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
-    const size_t o_res = a16z(o_jt + jix_topk.size() * 4);
+    const size_t o_tk = a16z(o_jt + jix_topk.size() * 4);  // K4' top-k tickets (zero), one per collaborative job
+    const size_t o_res = a16z(o_tk + jix_collab.size() * 4);
     const size_t o_rcnt = o_res + 16, o_rkeys = o_rcnt + a16z(dj.size() * 4);
     const size_t res_b = o_rkeys - o_res + dj.size() * (size_t)ktop * 8;
     const size_t total = o_res + 16;  // uploaded: the plan and the zero fail word
@@ -928,6 +930,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
+    if (!jix_collab.empty()) std::memset(h + o_tk, 0, jix_collab.size() * 4);
     std::memset(h + o_res, 0, 16);
     const size_t o_ord = a16z(o_res + res_b);  // the pair / walk blocks' dispatch orders (device-written)
     const size_t o_word = a16z(o_ord + std::max<size_t>(blocks.size(), 1) * 4);
@@ -956,6 +959,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
+    unsigned int* d_tk = reinterpret_cast<unsigned int*>(d + o_tk);
     int32_t* d_fail = reinterpret_cast<int32_t*>(d + o_res);
     int32_t* d_ord = reinterpret_cast<int32_t*>(d + o_ord);
     int32_t* d_ncand = reinterpret_cast<int32_t*>(d + o_rcnt);
@@ -973,6 +977,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         HIPCHK(c, W.d_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 4));
     }
     const uint8_t* ipl = resident ? J.d_pimg.as<uint8_t>() : W.d_img.as<uint8_t>();  // the batch's image pool
+    const int collab_gx = (max_cap_collab + 63) / 64;  // K4' blocks per job (pf_jobs.hip kCollabCands)
+    if (!jix_collab.empty())
+        HIPCHK(c, W.d_parts.reserve(jix_collab.size() * (size_t)std::max(collab_gx, 1) * (size_t)ktop * 8));
     if (!ujobs.empty()) {  // K1u's results per pair index (E: every output slot of the chunk)
         HIPCHK(c, W.d_upool.reserve(upool));
         HIPCHK(c, W.d_hb.reserve(nE * kHitCap * 4));
@@ -1047,7 +1054,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
-                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
+                            W.d_slots.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(), W.d_parts.as<uint64_t>(),
+                            d_tk, d_keys, ktop, s));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
                            W.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                            d_ncand, (int64_t)J.js.n_club_ids, s));
@@ -1057,6 +1065,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
     for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;
+    for (size_t t = 0; t < jix_fused.size(); ++t) tpos[jix_fused[t]] = (int32_t)(jix_topk.size() + t);
     std::vector<size_t> full;  // dj indices copied whole
     size_t ob = res_b;  // [fail | ncand | keys] as on the device, then the full lists
     std::vector<size_t> full_off;
@@ -1221,7 +1230,7 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     JobsState::Ws* pending = nullptr;
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
         (void)hipStreamSynchronize(c->stream);
-        J.ws[0].active = J.ws[1].active = false;
+        for (auto& w : J.ws) w.active = false;
         return code;
     };
     size_t b = 0;
@@ -1280,7 +1289,7 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
     (void)hipSetDevice(c->device);
     for (size_t i = 0; i < jobs.size(); ++i) oc[i] = 0;
     if (jobs.empty() || topk == 0) return PF_OK;
-    if (J.pending.size() >= 2) {
+    if (J.pending.size() >= (size_t)kJobSlots) {
         const int r = finish_pending(c);
         if (r != PF_OK) return r;
     }
@@ -1310,7 +1319,12 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
         }
         return PF_OK;
     }
-    const int slot = (!J.pending.empty() && J.pending.back().slot == 0) ? 1 : 0;
+    int slot = 0;  // a slot no pending call holds
+    for (bool used = true; used; ++slot) {
+        used = false;
+        for (const auto& q : J.pending) used |= q.slot == slot;
+        if (!used) break;
+    }
     JobsState::Pending pd;
     pd.ticket = *ticket;
     pd.slot = slot;

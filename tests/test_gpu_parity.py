@@ -802,7 +802,7 @@ def test_pipelined_job_chunks_equal_small_calls(big):
 
 
 def test_async_calls_equal_sync(big):
-    """pf_recommend_*_async + pf_wait: up to two calls in flight on one context (a third waits for
+    """pf_recommend_*_async + pf_wait: up to three calls in flight on one context (a fourth waits for
     the oldest), results equal to the synchronous calls bit for bit; waiting on a later ticket
     completes the earlier ones; pf_set_adj and synchronous calls complete the pending ones first
     (a row edit between launches affects only later calls); a batch too large for one chunk runs
@@ -819,7 +819,7 @@ def test_async_calls_equal_sync(big):
             assert list(x[0]) == list(y[0])
             assert np.array_equal(x[1].view(np.uint32), y[1].view(np.uint32))
 
-    hs = [eng.recommend_collaborative_async(q, 10, 2000) for q in qs]  # 3rd..5th wait for the oldest
+    hs = [eng.recommend_collaborative_async(q, 10, 2000) for q in qs]  # 4th, 5th wait for the oldest
     for h, w in zip(hs, want_c):
         same(eng.wait(h), w)
     h1 = eng.recommend_clubs_collab_async(qs[0], 10, 5000)

@@ -515,14 +515,21 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     }
     const uint32_t base = x - nit, total = (uint32_t)__shfl((int)x, 63);
     constexpr uint32_t kQueue = kHitSlots * 64u / 4u;
+    // A wave whose items exceed the queue takes two rounds: the lanes whose items end within it
+    // (a prefix of the lanes) first, then the others from the queue's start; only a second round
+    // past the queue too takes the per-lane epilogue (r3: 11 % of the waves needed two rounds)
+    const uint32_t rnd = x > kQueue ? 1u : 0u;
+    const uint64_t r1m = __ballot(rnd != 0u);
+    const uint32_t total0 = r1m ? (uint32_t)__shfl((int)base, __ffsll((unsigned long long)r1m) - 1) : total;
+    const uint32_t total1 = total - total0;
 #ifdef PF_K5_TIMERS
     if (lane == 0) {
-        atomicAdd(&g_k1t[9], total > kQueue ? 1ull : 0ull);
+        atomicAdd(&g_k1t[9], total1 > kQueue ? 1ull : 0ull);
         atomicAdd(&g_k1t[10], (unsigned long long)total);
         atomicAdd(&g_k1t[11], 1ull);
     }
 #endif
-    if (total > kQueue) {  // (wave-uniform) the per-lane epilogue, hit lists intact
+    if (total1 > kQueue) {  // (wave-uniform) the per-lane epilogue, hit lists intact
         if (!active) return 0.0f;
         if (hin)  // K1u's hit words: into the lane's list, where fas_epilogue reads them
 #pragma unroll
@@ -533,42 +540,12 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     auto item = [&](uint32_t k) {  // 16-B entry k of the wave's strip (rows of 64 words)
         return reinterpret_cast<uint4*>(hl + ((4u * k) >> 6) * kPairThreads + (uint32_t)wv * 64u + ((4u * k) & 63u));
     };
-    wave_sync();  // every lane holds its hit words: the strip is free
-    const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
-    uint32_t k = base;
-    if (club_it) *item(k++) = make_uint4((uint32_t)ic, nc, 0u, kItemClubs << 16);
-    if (fr_it) *item(k++) = make_uint4((uint32_t)ifr, nf, 0u, kItemFriends << 16);
-    const uint32_t nbase = (uint32_t)(ro + ((len + 3u) >> 2));  // the record's column norms (uint4 index)
-    double dot = 0.0;
-#pragma unroll
-    for (int i = 0; i < (int)kHitCap; ++i) {
-        if ((uint32_t)i < nhl) {
-            const uint32_t w = hw[i], col = colw(w);
-            const uint32_t val = probe_p(v, kTagTok | (w & 0xFFFFFFu));
-            const bool first = i == 0 || col != colw(hw[i > 0 ? i - 1 : 0]);
-            dot = (first ? 0.0 : dot) + hit_product(v, val & kTidMask, (int32_t)(w >> 24));
-            const bool last = (uint32_t)(i + 1) == nhl || col != colw(hw[i + 1 < (int)kHitCap ? i + 1 : i]);
-            if (last) {
-                const uint32_t rank = (uint32_t)__popcll(cmask & ((1ull << col) - 1ull));
-                *item(k++) = make_uint4((uint32_t)__double2loint(dot), (uint32_t)__double2hiint(dot), nbase,
-                                        (kItemText << 16) | (rank << 8) | col);
-            }
-        }
-    }
-    wave_sync();
-    for (uint32_t j = (uint32_t)lane; j < total; j += 64u) {  // the wave's terms, one per lane
-        uint4 it = *item(j);
-        const double term = item_term(q, it, item_norm(st, it));
-        it.x = (uint32_t)__double2loint(term);
-        it.y = (uint32_t)__double2hiint(term);
-        *item(j) = it;
-    }
-    wave_sync();
-    if (tep) tep[0] = clock64();
     auto term_at = [&](uint32_t kk) {
         const uint4 it = *item(kk);
         return __hiloint2double((int)it.y, (int)it.x);
     };
+    const uint64_t cmask = (uint64_t)h0.x | ((uint64_t)h0.y << 32);
+    const uint32_t nbase = (uint32_t)(ro + ((len + 3u) >> 2));  // the record's column norms (uint4 index)
     // every active lane: the fixed terms (an overflowed lane computes its set terms itself)
     double sum = 0.0;
     int used = 0;
@@ -585,36 +562,76 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
         sum += q.sig_reg[bcnt][m];
         ++used;
     }
-    uint32_t kk = base;
-    if (q.n_clubs > 0 && nc > 0) {
-        sum += ic == 0 ? q.sig0_clubs : (overflow ? set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs) : term_at(kk++));
-        ++used;
-    }
-    if (q.n_friends > 0 && nf > 0) {
-        sum += ifr == 0 ? q.sig0_friends
-                        : (overflow ? set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends) : term_at(kk++));
-        ++used;
-    }
-    // the common columns ascending: a hit column's term (the items are in column order), else s = 0
+    const bool has_clubs = q.n_clubs > 0 && nc > 0, has_friends = q.n_friends > 0 && nf > 0;
+    used += (has_clubs ? 1 : 0) + (has_friends ? 1 : 0);
     uint64_t common = q.colmask & cmask;
     used += __popcll(common);
-    if (active && !overflow) {
-        // a uniform loop over the query's columns (scalar control, the s = 0 term a broadcast
-        // read), adding where the candidate has the column too
-        const uint32_t ke = base + nit;
-        uint32_t nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
-        uint64_t qm = __builtin_amdgcn_readfirstlane((uint32_t)q.colmask) |
-                      ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(q.colmask >> 32)) << 32);
-        while (qm) {
-            const uint32_t c = (uint32_t)__ffsll((unsigned long long)qm) - 1u;
-            qm &= qm - 1ull;
-            const double s0 = q.sig0_col[c];
-            if ((common >> c) & 1ull) {
-                if (c == nextc) {
-                    sum += term_at(kk++);
-                    nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
-                } else {
-                    sum += s0;
+    const uint32_t rbase = rnd ? base - total0 : base;  // the lane's first item in its round
+    const uint32_t nrounds = r1m ? 2u : 1u;
+#pragma unroll
+    for (uint32_t r = 0; r < 2u; ++r) {
+        if (r >= nrounds) break;
+        const bool mine = rnd == r;
+        wave_sync();  // every lane holds its hit words / the previous round is consumed: the strip is free
+        if (mine && nit) {
+            uint32_t k = rbase;
+            if (club_it) *item(k++) = make_uint4((uint32_t)ic, nc, 0u, kItemClubs << 16);
+            if (fr_it) *item(k++) = make_uint4((uint32_t)ifr, nf, 0u, kItemFriends << 16);
+            double dot = 0.0;
+#pragma unroll
+            for (int i = 0; i < (int)kHitCap; ++i) {
+                if ((uint32_t)i < nhl) {
+                    const uint32_t w = hw[i], col = colw(w);
+                    const uint32_t val = probe_p(v, kTagTok | (w & 0xFFFFFFu));
+                    const bool first = i == 0 || col != colw(hw[i > 0 ? i - 1 : 0]);
+                    dot = (first ? 0.0 : dot) + hit_product(v, val & kTidMask, (int32_t)(w >> 24));
+                    const bool last = (uint32_t)(i + 1) == nhl || col != colw(hw[i + 1 < (int)kHitCap ? i + 1 : i]);
+                    if (last) {
+                        const uint32_t rank = (uint32_t)__popcll(cmask & ((1ull << col) - 1ull));
+                        *item(k++) = make_uint4((uint32_t)__double2loint(dot), (uint32_t)__double2hiint(dot), nbase,
+                                                (kItemText << 16) | (rank << 8) | col);
+                    }
+                }
+            }
+        }
+        wave_sync();
+        const uint32_t tr = r ? total1 : total0;
+        for (uint32_t j = (uint32_t)lane; j < tr; j += 64u) {  // the round's terms, one per lane
+            uint4 it = *item(j);
+            const double term = item_term(q, it, item_norm(st, it));
+            it.x = (uint32_t)__double2loint(term);
+            it.y = (uint32_t)__double2hiint(term);
+            *item(j) = it;
+        }
+        wave_sync();
+        if (tep && r == 0) tep[0] = clock64();
+        if (!mine) continue;
+        // the lane's round: clubs, friends, then the common columns ascending (a hit column's term,
+        // the items being in column order, else s = 0), recommender_similarity.cpp:80-113
+        uint32_t kk = rbase;
+        if (has_clubs)
+            sum += ic == 0 ? q.sig0_clubs : (overflow ? set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs) : term_at(kk++));
+        if (has_friends)
+            sum += ifr == 0 ? q.sig0_friends
+                            : (overflow ? set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends) : term_at(kk++));
+        if (active && !overflow) {
+            // a uniform loop over the query's columns (scalar control, the s = 0 term a broadcast
+            // read), adding where the candidate has the column too
+            const uint32_t ke = rbase + nit;
+            uint32_t nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
+            uint64_t qm = __builtin_amdgcn_readfirstlane((uint32_t)q.colmask) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(q.colmask >> 32)) << 32);
+            while (qm) {
+                const uint32_t c = (uint32_t)__ffsll((unsigned long long)qm) - 1u;
+                qm &= qm - 1ull;
+                const double s0 = q.sig0_col[c];
+                if ((common >> c) & 1ull) {
+                    if (c == nextc) {
+                        sum += term_at(kk++);
+                        nextc = kk < ke ? (item(kk)->w & 0xFFu) : 0xFFu;
+                    } else {
+                        sum += s0;
+                    }
                 }
             }
         }

@@ -855,7 +855,6 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     std::vector<ImgJob> ij(resident ? 0 : img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
     uint32_t max_lds = 0;
-    bool gtab = false;
     size_t ipool = 0;
     int64_t scr = 0;
     for (size_t k = 0; k < img_idx.size(); ++k) {
@@ -887,10 +886,32 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         }
         const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
         r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;
-        gtab = gtab || r.lds_bytes == 0;
         const uint32_t need = (uint32_t)sizeof(QConst) + r.lds_bytes + kHitSlots * (packed ? 4u : 8u) * kPairThreads +
                               4u * kPairThreads + 2048u;
         max_lds = std::max(max_lds, need);
+    }
+    // The pair blocks in three launches by their image: LDS-staged images whose block fits two
+    // workgroups per CU, larger LDS-staged ones, global-memory tables.  One launch sized for the
+    // batch's largest image ran every block of 6 % of the cfg-3 steps at one workgroup per CU
+    // (484 vs 338 us, r3ad), and one global-table image switched every block to global probes.
+    uint32_t lds_c[3] = {0u, 0u, 0u};
+    int nb_c[3] = {0, 0, 0};
+    {
+        constexpr uint32_t kTwoPerCu = 80u * 1024u;  // 160 KB of LDS per CU
+        std::vector<uint8_t> icls(refs.size());
+        for (size_t k = 0; k < refs.size(); ++k) {
+            const uint32_t need = (uint32_t)sizeof(QConst) + refs[k].lds_bytes +
+                                  kHitSlots * (packed ? 4u : 8u) * kPairThreads + 4u * kPairThreads + 2048u;
+            icls[k] = refs[k].lds_bytes == 0 ? 2 : (need <= kTwoPerCu ? 0 : 1);
+            lds_c[icls[k]] = std::max(lds_c[icls[k]], need);
+        }
+        std::vector<PairBlock> part[3];
+        for (const PairBlock& pb : blocks) part[icls[pb.qimg]].push_back(pb);
+        blocks.clear();
+        for (int k = 0; k < 3; ++k) {
+            nb_c[k] = (int)part[k].size();
+            blocks.insert(blocks.end(), part[k].begin(), part[k].end());
+        }
     }
     hl.lap(kHpImages);
     // ---- staging: [DevJob | pool32 | pool64 | ImgJob | QImageRef | PairBlock | jix x3], then the
@@ -1001,7 +1022,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
                             d_ncand, J.aux));
-    HIPCHK(c, launch_order_pairs(d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), hc.n, d_ord, J.aux));
+    for (int k = 0, o = 0; k < 3; o += nb_c[k++])  // each launch's dispatch order (relative to its blocks)
+        HIPCHK(c, launch_order_pairs(d_blk + o, nb_c[k], W.d_slots.as<int32_t>(), hc.n, d_ord + o, J.aux));
     if (!ujobs.empty())
         HIPCHK(c, launch_order_pairs(d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), hc.n, d_word, J.aux));
     HIPCHK(c, hipEventRecord(J.ev_join, J.aux));
@@ -1029,8 +1051,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         HIPCHK(c, launch_union_walk(c->ds, W.d_upool.as<uint8_t>(), d_uj, max_wlds, d_wb, (int)wblocks.size(), d_word,
                                     W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(), s));
     }
-    HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, max_lds, gtab, d_blk, (int)blocks.size(), d_ord,
-                           W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
+    for (int k = 0, o = 0; k < 3; o += nb_c[k++])
+        HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, lds_c[k], k == 2, d_blk + o, nb_c[k], d_ord + o,
+                               W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
     HIPCHK(c, launch_pairs_prewalked(c->ds, ipl, d_refs, max_lds, d_pb, (int)pblocks.size(),
                                      W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(),
                                      W.d_fl.as<float>(), s));

@@ -702,16 +702,30 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
 // store (contiguous 16-B steps, so the lane's loads consume whole cache lines), its own hit list
 // then holds the whole record's hits in order; the column norms follow the record in the row
 // store, so no tile lookup sits in front of them.
-template <bool PACKED>
-__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, int p, bool active, uint64_t* twalk = nullptr) {
-    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-    uint64_t ro = 0;
+// A pair candidate's headers and row offset, loaded before the block stages its image (the loads
+// are in flight across the staging round trip and its barrier)
+struct PairHdr {
+    uint4 h0, h1, h2;
+    uint64_t ro;
+};
+__device__ __forceinline__ PairHdr load_pair_hdr(const DevStore& st, int p, bool active) {
+    PairHdr H;
+    H.h0 = H.h1 = H.h2 = make_uint4(0, 0, 0, 0);
+    H.ro = 0;
     if (active) {
-        h0 = st.hdr0[p];
-        h1 = st.hdr1[p];
-        h2 = st.hdr2[p];
-        ro = st.row_off[p];
+        H.h0 = st.hdr0[p];
+        H.h1 = st.hdr1[p];
+        H.h2 = st.hdr2[p];
+        H.ro = st.row_off[p];
     }
+    return H;
+}
+
+template <bool PACKED>
+__device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, const PairHdr& H, bool active,
+                                          uint64_t* twalk = nullptr) {
+    const uint4 h0 = H.h0, h1 = H.h1, h2 = H.h2;
+    const uint64_t ro = H.ro;
     const uint32_t nc = h2.y, nset = h2.y + h2.z;
     const uint32_t len = active ? record_words(h2, PACKED) : 0u;
     const RowRec rec{reinterpret_cast<const uint32_t*>(st.rows + ro),
@@ -738,19 +752,12 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, in
 // counts and hit words come from hc[P] / hb[P * kHitCap ..] (64 B, four 16-B loads in flight),
 // and only the epilogue runs here.  An overflowed list (> kHitCap hits) takes the epilogue's
 // record re-walk against the staged image, as after a walk of its own.
-__device__ __forceinline__ float fas_slot_pre(const DevStore& st, const QView& v, int p, bool active, uint64_t P,
-                                              const uint32_t* __restrict__ hb, const uint2* __restrict__ hc,
+__device__ __forceinline__ float fas_slot_pre(const DevStore& st, const QView& v, const PairHdr& H, bool active,
+                                              uint64_t P, const uint32_t* __restrict__ hb, const uint2* __restrict__ hc,
                                               uint64_t* twalk = nullptr) {
-    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-    uint64_t ro = 0;
-    uint2 wr = make_uint2(0u, 0u);
-    if (active) {
-        h0 = st.hdr0[p];
-        h1 = st.hdr1[p];
-        h2 = st.hdr2[p];
-        ro = st.row_off[p];
-        wr = hc[P];
-    }
+    const uint4 h0 = H.h0, h1 = H.h1, h2 = H.h2;
+    const uint64_t ro = H.ro;
+    const uint2 wr = active ? hc[P] : make_uint2(0u, 0u);
     const uint32_t nh = wr.y > kHitCap ? kHitCap + 1 : wr.y;
     uint32_t hw[kHitCap];
     {
@@ -1575,15 +1582,15 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
     int p = i < b.count ? slots[b.begin + i] : -1;
     const bool active = p >= 0;
     if (!__syncthreads_or(active)) return;
+    const PairHdr H = load_pair_hdr(st, p, active);
     char* scratch;
     const QView v = stage_query<GTAB>(smem, pool, refs[b.qimg], &scratch);
 #ifdef PF_K5_TIMERS
     const uint64_t t1 = clock64();
 #endif
-    if (!active) p = 0;
     float f;
-    if constexpr (PRE) f = fas_slot_pre(st, v, p, active, (uint64_t)b.out + (uint64_t)i, hb, hc, twp);
-    else f = fas_slot<PACKED>(st, v, p, active, twp);
+    if constexpr (PRE) f = fas_slot_pre(st, v, H, active, (uint64_t)b.out + (uint64_t)i, hb, hc, twp);
+    else f = fas_slot<PACKED>(st, v, H, active, twp);
     if (active) out[b.out + i] = f;
 #ifdef PF_K5_TIMERS
     const uint64_t t3 = clock64();

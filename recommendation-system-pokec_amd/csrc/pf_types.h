@@ -16,7 +16,10 @@ constexpr int kNormSlots = kNumFixed + kMaxCols;
 constexpr int kValTab = 128;        // completion/age sigmoid tables cover values 1..128
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
-constexpr uint32_t kHitCap = 16;    // token hits kept per candidate in LDS (overflow -> slow re-walk)
+#ifndef PF_HIT_CAP
+#define PF_HIT_CAP 16
+#endif
+constexpr uint32_t kHitCap = PF_HIT_CAP;  // token hits kept per candidate in LDS (overflow -> slow re-walk)
 #ifndef PF_QUEUE_EXTRA
 #define PF_QUEUE_EXTRA 0
 #endif

@@ -17,7 +17,7 @@ constexpr int kValTab = 128;        // completion/age sigmoid tables cover value
 constexpr int kMaxTopK = 64;        // in-kernel top-k bound (one key per lane)
 constexpr int kScanThreads = 256;   // 4 waves per scan block
 #ifndef PF_HIT_CAP
-#define PF_HIT_CAP 16
+#define PF_HIT_CAP 20
 #endif
 constexpr uint32_t kHitCap = PF_HIT_CAP;  // token hits kept per candidate in LDS (overflow -> slow re-walk)
 #ifndef PF_QUEUE_EXTRA

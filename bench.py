@@ -268,8 +268,10 @@ def pmc_pass(args, select):
                 continue
             mean = sum(v) / len(v)
             factor, fsrc = factors[k]
+            # _raw: the picked per-dispatch values, for callers that group dispatches into stages
+            # (pair_stage_traffic); never printed
             out[k] = ({"bytes_per_launch": mean * 1024 * factor, "fetch_size_kib_mean": mean, "launches": len(v),
-                       "factor": factor, "factor_source": fsrc}, None)
+                       "factor": factor, "factor_source": fsrc, "_raw": list(v)}, None)
         return out
     except Exception as e:
         return {k: (None, str(e)[:300]) for k in select}
@@ -358,6 +360,7 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True,
         dist.barrier()
     # timed region: the pair kernel timed by HIP events (the launch roofline); the pair and byte
     # counts come from an untimed replay of the same steps (the counting kernel stays out of it)
+    disp0 = sum(e.jobs_stats()["pair_dispatches"] for e in engs)  # K1' dispatches before the timed steps
     for e in engs:
         e.jobs_stats_reset(time_pairs=True, count=False)
 
@@ -389,11 +392,12 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True,
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timing = {"pair_ms": 0.0, "pair_launches": 0}
+    timing = {"pair_ms": 0.0, "pair_launches": 0, "disp1": 0}
     for e in engs:
         tm_ = e.jobs_stats()
         timing["pair_ms"] += tm_["pair_ms"]
         timing["pair_launches"] += tm_["pair_launches"]
+        timing["disp1"] += tm_["pair_dispatches"]
         if e is not eng:
             e.jobs_stats_reset(time_pairs=False, count=False)
     eng.jobs_stats_reset(time_pairs=False, count=True)
@@ -402,6 +406,7 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True,
     st = eng.jobs_stats()
     eng.jobs_stats_reset(time_pairs=False, count=False)
     st["pair_ms"], st["pair_launches"] = timing["pair_ms"], timing["pair_launches"]
+    st["disp0"], st["disp1"] = disp0, timing["disp1"]
     st["elapsed"], st["results"], st["async"] = elapsed, nres, use_async
     if dist:
         t = torch.tensor([st["pairs"], st["candidates"]], dtype=torch.float64, device="cuda")
@@ -410,6 +415,29 @@ def measure_cfg3(engs, mine, warm, steps, dist=None, torch=None, use_async=True,
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         st["pairs"], st["candidates"], st["elapsed"] = float(t[0]), float(t[1]), float(tm.item())
     return st
+
+
+def pair_stage_traffic(pmc, st):
+    """HBM bytes per pair STAGE of the timed region from the PMC child's per-dispatch FETCH_SIZE rows
+    of fas_pairs_kernel (every dispatch, in order): a pair stage launches up to four K1' dispatches
+    (one per image LDS class, plus the pre-walked pairs), so the rows are grouped by the engines'
+    own dispatch counters (pf_jobs_stats.pair_dispatches before / after the timed region; the child
+    runs the same deterministic command, so its dispatch sequence is the same).  Returns (bytes per
+    stage or None, traffic_source)."""
+    if not pmc or not pmc[0]:
+        return None, (pmc[1] if pmc else "not run")
+    info = {k: v for k, v in pmc[0].items() if k != "_raw"}
+    raw, d0, d1, stages = pmc[0].get("_raw", []), st.get("disp0"), st.get("disp1"), st.get("pair_launches")
+    if d0 is None or d1 is None or not stages or d1 > len(raw) or d1 <= d0:
+        return None, {**info, "error": f"dispatch counts {d0}..{d1} do not fit the {len(raw)} PMC rows"}
+    kib = sum(raw[d0:d1])
+    per_stage = kib * 1024 * info["factor"] / stages
+    info.update({"bytes_per_launch": per_stage, "unit_of_launch": "pair stage (all its K1' dispatches)",
+                 "dispatches": d1 - d0, "stages": stages, "dispatch_range": [d0, d1],
+                 "fetch_size_kib_per_stage": kib / stages})
+    info.pop("fetch_size_kib_mean", None)
+    info.pop("launches", None)
+    return per_stage, info
 
 
 def cfg3_fields(st, steps, pmc):
@@ -424,7 +452,7 @@ def cfg3_fields(st, steps, pmc):
 
     achieved = rate(phys)
     alg_pl = st["pair_alg_bytes"] / launches if launches else None
-    traffic = pmc[0]["bytes_per_launch"] if pmc and pmc[0] else None
+    traffic, tsrc = pair_stage_traffic(pmc, st)
     return {
         "value": st["pairs"] / elapsed, "unit": "pair-FAS/s", "ms_per_step": elapsed * 1e3 / steps,
         "candidates_per_s": st["candidates"] / elapsed, "queries_per_s": CFG3_QUERIES * steps / elapsed,
@@ -438,7 +466,7 @@ def cfg3_fields(st, steps, pmc):
                                     "words (K1' walks the record), per pair block the staged query image",
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
-                     "traffic_source": (pmc[0] if pmc and pmc[0] else (pmc[1] if pmc else "not run")),
+                     "traffic_source": tsrc,
                      "alg_effective_gbs": rate(alg_pl),
                      "alg_effective_frac": None if rate(alg_pl) is None else rate(alg_pl) / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_pl,
@@ -633,6 +661,7 @@ def run_cfg5(args, world, rank, local):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    disp0 = sum_stats(lambda e: e.jobs_stats())["pair_dispatches"]  # K1' dispatches before the timed steps
     for e in engs:
         e.jobs_stats_reset(time_pairs=True, count=False)
     ts = time.perf_counter()
@@ -671,7 +700,9 @@ def run_cfg5(args, world, rank, local):
         return None if (b is None or not avg_ms) else b / (avg_ms * 1e-3) / 1e9
 
     achieved = rate(phys)
-    traffic = pmc["bytes_per_launch"] if pmc else None
+    # HBM bytes per pair stage: the timed stages' K1' dispatches grouped by the dispatch counters
+    traffic, tsrc = pair_stage_traffic((pmc, pmc_err), {"disp0": disp0, "disp1": timing["pair_dispatches"],
+                                                        "pair_launches": launches})
     value = n_eval * steps / elapsed
     rec = {
         "metric": METRIC, "value": value, "unit": "hold-out users/s", "n_gpus": world, "steps": steps,
@@ -696,7 +727,7 @@ def run_cfg5(args, world, rank, local):
                                     "words (K1' walks the record), per 256-pair block the staged query image",
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
-                     "traffic_source": pmc if pmc else pmc_err,
+                     "traffic_source": tsrc,
                      "alg_effective_gbs": rate(alg_pl),
                      "alg_bytes_per_launch": alg_pl,
                      "pair_kernel_share_of_step": (timing["pair_ms"] / (elapsed * 1e3)) if elapsed > 0 else None},
@@ -800,12 +831,10 @@ def main():
             sel = {}
             if args.workload in ("cfg2", "cfg4"):
                 sel[want_kernel] = lambda v, k=args.steps: v[len(v) - k:] if len(v) >= k else []
-            if args.workload == "cfg3":
-                sel["fas_pairs_kernel"] = lambda v: v  # warmup and timed steps alike
-            elif sub3:
-                # pair launches: the top-k self-check (1), cfg 3's warmup (W3), its timed steps, the
-                # counting replay; the timed ones
-                sel["fas_pairs_kernel"] = lambda v, w=W3, k=args.cfg3_steps: v[1 + w:1 + w + k]
+            if args.workload == "cfg3" or sub3:
+                # every K1' dispatch; the timed stages' ones are picked later by the engines'
+                # dispatch counters (pair_stage_traffic)
+                sel["fas_pairs_kernel"] = lambda v: v
             pmcs = pmc_pass(args, sel)
             for k, (_, e) in pmcs.items():
                 if e:
@@ -965,7 +994,7 @@ def main():
                                      "pf_scan_bytes: the shard's record stream + 48-B headers"),
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_launch_ms else rate(traffic) / HBM_PEAK_GBS,
-                     "traffic_source": pmc if pmc else pmc_err,
+                     "traffic_source": ({k: v for k, v in pmc.items() if k != "_raw"} if pmc else pmc_err),
                      "alg_effective_gbs": alg_eff,
                      "alg_effective_frac": None if alg_eff is None else alg_eff / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_bytes,

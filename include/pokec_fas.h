@@ -276,12 +276,15 @@ int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* ou
  * and union-table bytes (one per 512-pair / walk block), and the pair-scoring stage's device
  * time (HIP events around K1u + K1' in each launch) and launch count.  enable: bit 0 = time the pair kernel (HIP events around each
  * launch), bit 1 = count pairs and bytes (one extra small kernel per launch); 0 stops
- * both.  Fields of a part that is off read 0. */
+ * both.  Fields of a part that is off read 0.  pair_dispatches: the pair-kernel (K1')
+ * dispatches since pf_open, never reset (a pair stage launches up to four, by image LDS
+ * class), so a profiler's per-dispatch rows can be grouped into the stages they belong to. */
 typedef struct pf_jobs_stats {
     int64_t jobs, candidates, pairs;
     int64_t pair_alg_bytes, pair_record_bytes, pair_image_bytes;
     double  pair_ms;
     int64_t pair_launches;
+    int64_t pair_dispatches;
 } pf_jobs_stats;
 int pf_jobs_stats_reset(pf_ctx* ctx, int32_t enable);
 int pf_jobs_stats_read(pf_ctx* ctx, pf_jobs_stats* out);

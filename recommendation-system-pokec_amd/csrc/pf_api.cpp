@@ -537,7 +537,7 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     }
     const bool prof = pf::host_prof().on;
     auto t0 = std::chrono::steady_clock::now();
-    auto stage = [&](const char* what) {  // PF_HOST_PROF=1: pf_open stage clocks on stderr
+    auto stage = [&](const char* what) {  // PF_DEBUG host_prof=1: pf_open stage clocks on stderr
         const auto t1 = std::chrono::steady_clock::now();
         if (prof) fprintf(stderr, "[pf_open] %s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
         t0 = t1;
@@ -592,13 +592,21 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     c->ds.row_pad = c->d_rowstore.as<uint4>() + hs.row_off[c->hc.n];  // build_store's trailing padding line
     c->stream_bytes = (int64_t)hs.stream.size() * 16;
     c->norm_bytes = (int64_t)hs.norms.size() * 8;
-    if (c->hp.ok)
+    if (c->hp.ok) {
         c->post_bytes = (int64_t)c->hp.hdr.size() * 16 + (int64_t)c->hp.post.size() * 4 +
                         (int64_t)c->hp.pnorm.size() * 8 + (int64_t)c->hp.cells.size() * 4;
+        c->ps.n_post = (uint32_t)c->hp.post.size();
+        c->ps.n_tok_entries = (uint32_t)c->hp.pnorm.size();
+        c->ps.n_cells = (uint32_t)c->hp.cells.size();
+    }
     // the host copies of the device stores (~5 GB at 1.63M users) are returned to the system on a
     // detached thread: unmapping them takes ~0.6 s that pf_open need not wait for
-    std::thread([a = std::move(hs.stream), b = std::move(hs.norms), r = std::move(hs.rows),
-                 p = std::move(c->hp.post), q = std::move(c->hp.pnorm)]() mutable {}).detach();
+    try {
+        std::thread([a = std::move(hs.stream), b = std::move(hs.norms), r = std::move(hs.rows),
+                     p = std::move(c->hp.post), q = std::move(c->hp.pnorm)]() mutable {}).detach();
+    } catch (...) {  // no thread to be had: free them here (no exception crosses the C ABI)
+        hs.stream.clear(); hs.norms.clear(); hs.rows.clear(); c->hp.post.clear(); c->hp.pnorm.clear();
+    }
     std::vector<uint64_t>().swap(hs.row_off);
     c->ds.stream = c->d_stream.as<uint4>();
     c->ds.tile_off = c->d_tile_off.as<uint64_t>();

@@ -48,7 +48,7 @@ struct Job {
     std::vector<std::pair<int32_t, float>> out;  // ranked (id, score), <= topk
 };
 
-// Host-side stage clocks of the batched drivers (PF_HOST_PROF=1: summed over the process and
+// Host-side stage clocks of the batched drivers (PF_DEBUG host_prof=1: summed over the process and
 // printed to stderr at exit; profiling only).
 enum HostStage {
     kHpPlan = 0, kHpPrep, kHpImages, kHpPack, kHpGpu, kHpUnpack, kHpStage2, kHpCollab, kHpFinish, kHpStages

@@ -112,8 +112,8 @@ struct JobsState {
     // stream (both latency-bound, independent), joined before the pair kernel
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool union_on = true;                        // collaborative friend groups walk each record once (K6u / K1u;
-                                                 // PF_DEBUG union=0: every pair walks its own record)
+    bool union_on = false;                       // collaborative friend groups walk each record once (K6u / K1u;
+                                                 // opt-in, PF_DEBUG union=1: measured slower)
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
     std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;
@@ -166,6 +166,7 @@ struct JobsState {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> stat_ev;
     size_t stat_used = 0;
     int64_t st_jobs = 0, st_cands = 0, st_img_bytes = 0, st_launches = 0;
+    int64_t n_dispatch = 0;                      // K1' dispatches since open (pf_jobs_stats.pair_dispatches)
 };
 
 }  // namespace pf

@@ -1051,9 +1051,12 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         HIPCHK(c, launch_union_walk(c->ds, W.d_upool.as<uint8_t>(), d_uj, max_wlds, d_wb, (int)wblocks.size(), d_word,
                                     W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(), s));
     }
-    for (int k = 0, o = 0; k < 3; o += nb_c[k++])
+    for (int k = 0, o = 0; k < 3; o += nb_c[k++]) {
         HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, lds_c[k], k == 2, d_blk + o, nb_c[k], d_ord + o,
                                W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
+        J.n_dispatch += nb_c[k] > 0;
+    }
+    J.n_dispatch += !pblocks.empty();
     HIPCHK(c, launch_pairs_prewalked(c->ds, ipl, d_refs, max_lds, d_pb, (int)pblocks.size(),
                                      W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(),
                                      W.d_fl.as<float>(), s));
@@ -1418,6 +1421,7 @@ int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) {
     o->pair_image_bytes = J.st_img_bytes;
     o->pair_ms = ms;
     o->pair_launches = J.st_launches;
+    o->pair_dispatches = J.n_dispatch;
     return PF_OK;
 }
 

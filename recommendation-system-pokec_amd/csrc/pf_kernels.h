@@ -65,13 +65,5 @@ hipError_t launch_union_walk(const DevStore& st, const uint8_t* upool, const Uni
 hipError_t launch_pairs_prewalked(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
                                   const PairBlock* blocks, int nblocks, const int32_t* slots, const uint32_t* hb,
                                   const uint2* hc, float* out, hipStream_t s);
-// one collaborative query of a K4 batch: M rows at moff ([rows][nc]), w / row at woff ([F]),
-// scores to out + coff ([nc])
-struct CollabSum {
-    int64_t moff, coff;
-    int32_t woff, F, nc, pad;
-};
-hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, const CollabSum* jobs, int njobs,
-                             int max_nc, float* out, hipStream_t s);
 
 }  // namespace pf

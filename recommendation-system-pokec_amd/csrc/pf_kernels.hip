@@ -4,7 +4,6 @@
 //                          blockIdx.y, fused per-wave / per-block top-k (K2a)
 //   topk_merge_kernel K2b  per-query merge of per-block (or per-GPU) key lists
 //   fas_pairs_kernel  K1'  FAS for explicit (query, candidate) pairs (A10/A12/A14/A15)
-//   collab_sum_kernel K4   score(c) = sum_f (double)w_f * FAS(f,c) in friend-list order (A14)
 //
 // One lane owns one candidate (64 candidates = one tile per wave).  Records are stored
 // tile-interleaved, so each 16-B step of a wave is one coalesced 1 KiB load.  The walk
@@ -894,8 +893,9 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
         if (lane < k) st_agent(qparts + (size_t)blockIdx.x * k + lane, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // program order: stores, wait, ticket (no hardware fence)
         unsigned t = 0;
-        if (lane == 0) t = atomicAdd(&sy->done, 1u);
+        if (lane == 0) t = __hip_atomic_fetch_add(&sy->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0) {
             *s_flag = t == gridDim.x - 1;
             *s_cnt = 0;
@@ -1084,43 +1084,88 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
 
 // ---------------------------------------------------------------- K5: postings scan
 // All-candidates FAS (A13) through the postings store (pf_types.h): a workgroup scores one
-// block of 1024 consecutive candidates at a time (thread i owns candidates i + 256 kk)
-// from the lists the query names, never the candidates' records:
+// block of kBlockCands (512) consecutive candidates at a time (thread i owns candidates i and
+// i + 256) from the lists the query names, never the candidates' records:
 //   1. ranges: every list's sub-range for this block (one cell lookup per list);
 //   2. sets: club / friend list entries add their multiplicity to per-candidate LDS
 //      counters (integer, order-free) and the exclusion list marks adj[q] + {q};
 //   3. fixed terms (public .. friends) per owned candidate from its 32-B header;
-//   4. text, one active query column at a time in ascending order: the column's token
-//      lists (<= 8 tokens per pass) write each hit's tf byte at [candidate][token] and its
-//      (candidate, column) norm; each wave lists its own hit candidates (ballot + popcount,
-//      no atomics), and their dot (ascending tid: token order, only the hit bytes visited)
-//      and cosine -> sigmoid term are computed densely by the wave, one candidate per lane,
-//      so the FP64 divisions and exp never run on idle lanes; the owners then add
-//      the column's term, or the s = 0 term of a common column without hits, in the
-//      reference's order (recommender_similarity.cpp:38-113).
-// LDS: QConst | tf bytes u64[1024] | norm f64[1024] | term f64[1024] | counters u32[1024]
-// (later the hit lists, u16[4][256]) | exclusion bits u32[32] | misc u32[4] | QCol[48] |
-// PTok[n_tok] | ranges uint2[n_lists] | prefix u32[n_tok + 1].  The tail merge reuses the
-// tf-byte array.
-constexpr uint32_t kPostFixedLds = kBlockCands * (8 + 8 + 8 + 4) + kBlockCands / 8 + 16 + 16 * kPostMaxCols +
-                                   8 * (kNumFixed + kPostMaxCols + 1);
+//   4. text, in ROUNDS of <= 64 query tokens (whole columns where they fit, the columns in
+//      ascending order) whose list entries in the block fit the round's kRoundCap hit slots:
+//      a. walk: every entry of the round's lists, flattened over the workgroup (all loads in
+//         flight at once), sets bit (token - round start) of its candidate's 64-bit hit mask;
+//      b. slots: each wave gives its candidates' hits a contiguous range of hit slots, a
+//         candidate's hits in token order (= column, then tid ascending);
+//      c. place: every entry writes its tf and token into its slot (the slot index is the
+//         popcount of the mask below its bit), and the first hit of a column its
+//         (candidate, column) norm;
+//      d. terms, wave-dense: one lane per (candidate, column) item sums the products of its
+//         hits in ascending tid order (recommender.cpp:74-85) and computes the cosine ->
+//         sigmoid term (recommender_similarity.cpp:93-113), so the FP64 divisions and exp
+//         run on as many lanes as there are items, not once per column for the whole wave;
+//      e. the owners add, in the reference's order, each common column's term, or its s = 0
+//         term when the candidate has no hit in it.
+//      A column longer than a round (> 64 tokens, or more entries than kRoundCap) is split
+//      over rounds; its owners carry the dot in registers and compute its term themselves.
+//   5. FAS (recommender_similarity.cpp:114-123), idx-keyed wave top-k, fused cross-block merge.
+// A block costs 2 + 4 x rounds barriers and one memory round trip per round (the walk); the
+// round-1 design paid two barriers and a round trip per 8-token pass (21.6 passes per block).
 
-// A query token in LDS: its weight and idf, and the products for tf = 1 and 2 (the common
-// cases), each computed as the reference does, wq * (tf * idf) (recommender.cpp:74-85).
+// A query token in LDS: its weight and idf (the product wq * (tf * idf), recommender.cpp:74-85)
 struct PTok {
-    double p1, p2, wq, idf;
+    double wq, idf;
 };
+
+// LDS carve of the fixed part (after QConst)
+constexpr uint32_t kLdsMask = 0;                                          // u64 [kBlockCands] hit masks
+constexpr uint32_t kLdsSlot = kLdsMask + 8 * kBlockCands;                 // f64 [kRoundCap] norm -> term
+constexpr uint32_t kLdsHit = kLdsSlot + 8 * kRoundCap;                    // u16 [kRoundCap] hits
+constexpr uint32_t kLdsHbase = kLdsHit + 2 * kRoundCap;                   // u16 [kBlockCands] first slot
+constexpr uint32_t kLdsCnt = kLdsHbase + 2 * kBlockCands;                 // u32 [kBlockCands] set counters
+constexpr uint32_t kLdsExb = kLdsCnt + 4 * kBlockCands;                   // u32 [kBlockCands / 32] excluded
+constexpr uint32_t kLdsMisc = kLdsExb + 4 * (kBlockCands / 32);           // u32 [16]
+constexpr uint32_t kLdsCols = kLdsMisc + 64;                              // QCol [kPostMaxCols]
+constexpr uint32_t kLdsFtab = kLdsCols + 16 * kPostMaxCols;               // f64 [7 + 48 + 1] F by used
+constexpr uint32_t kLdsSeg = kLdsFtab + 8 * (kNumFixed + kPostMaxCols + 1);  // u32 [kRoundToks] token segments
+constexpr uint32_t kPostFixedLds = (kLdsSeg + 4 * kRoundToks + 15) & ~15u;
+static_assert(kBlockCands == 2 * kPostThreads, "two candidates per thread");
+static_assert(kRoundCap < 65536 && kBlockCands <= kRoundCap, "u16 slots; a one-token round fits");
+static_assert(kPostWaves * kMaxTopK * 8 + 16 + 4 * kMaxTopK <= 8 * kRoundCap, "scan_tail scratch in the slots");
+
+// hit slot: tf | token - round start << 8 | first hit of its column segment | first hit of its candidate
+constexpr uint32_t kHitFirst = 1u << 14;
+constexpr uint32_t kHitCand = 1u << 15;
+// token segment (per token of a round): segment start | end << 8 (round-relative) | column << 16 |
+// split (the column spans several rounds) << 24
+constexpr uint32_t kSegSplit = 1u << 24;
+
+#ifdef PF_K5_CHECK
+// checked build (tools/build_variant.sh k5chk XFLAGS=-DPF_K5_CHECK): every global index of K5 is
+// range-checked; a bad one is reported and replaced by 0 instead of faulting
+__device__ __forceinline__ uint32_t k5_chk(uint32_t i, uint32_t n, int what) {
+    if (i >= n) {
+        printf("K5 CHECK %d: index %u >= %u (block %d thread %d)\n", what, i, n, (int)blockIdx.x, (int)threadIdx.x);
+        return 0u;
+    }
+    return i;
+}
+#define K5CHK(i, n, w) k5_chk((i), (n), (w))
+#else
+#define K5CHK(i, n, w) (i)
+#endif
+
+__device__ __forceinline__ uint64_t low_bits(uint32_t n) { return n >= 64u ? ~0ull : ((1ull << n) - 1ull); }
 
 // entries of list L for candidates [c0, c1] (cells c0 >> shift .. c1 >> shift)
 __device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0, uint32_t c1) {
-    return make_uint2(L.off + ps.cells[L.cell_off + (c0 >> L.shift)], L.off + ps.cells[L.cell_off + (c1 >> L.shift) + 1]);
+    return make_uint2(L.off + ps.cells[K5CHK(L.cell_off + (c0 >> L.shift), ps.n_cells, 1)],
+                      L.off + ps.cells[K5CHK(L.cell_off + (c1 >> L.shift) + 1, ps.n_cells, 2)]);
 }
 
 // Flattened walk over the entries of lists rng[0 .. nl): thread i takes flat entries
-// i + 256u (u < 2) of every 512-entry group, loads them (and, for token lists, their norms)
-// together, then calls f(list, entry, norm) for each.
-template <bool NORMS, class F>
-__device__ __forceinline__ void walk_lists(const PostStore& ps, const uint2* rng, int nl, F f) {
+// i + 256u (u < 2) of every 512-entry group, loads them together, then calls f(list, entry)
+template <class F>
+__device__ __forceinline__ void walk_sets(const PostStore& ps, const uint2* rng, int nl, F f) {
     constexpr int U = 2;
     uint32_t total = 0;
     for (int j = 0; j < nl; ++j) total += rng[j].y - rng[j].x;
@@ -1141,15 +1186,11 @@ __device__ __forceinline__ void walk_lists(const PostStore& ps, const uint2* rng
             pre += len;
         }
         uint32_t ent[U];
-        double nv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            ent[u] = js[u] >= 0 ? ps.post[xs[u]] : 0u;
-            nv[u] = (NORMS && js[u] >= 0) ? ps.pnorm[xs[u]] : 0.0;
-        }
+        for (int u = 0; u < U; ++u) ent[u] = js[u] >= 0 ? ps.post[K5CHK(xs[u], ps.n_post, 3)] : 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (js[u] >= 0) f(js[u], ent[u], nv[u]);
+            if (js[u] >= 0) f(js[u], ent[u]);
     }
 }
 
@@ -1171,58 +1212,53 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
     if (lane == 0) gpre[nl] = carry;
 }
 
-// The entries of token lists js .. js + nj - 1 (nj <= 8) flattened over the workgroup, with
-// the block's token prefix gpre: a thread finds the list of a flat entry in 3 bisection
-// steps.  One group of 512 flat entries: a thread's two (list - js or -1, entry, norm),
-// loaded together.
-constexpr int kGroupU = 2;  // flat entries per thread in a group (r2i: 3 -> 210 us, 4 -> 217.6 vs 206)
-struct Group {
-    int jj[kGroupU];
-    uint32_t ent[kGroupU];
-    double nv[kGroupU];
-};
-
-__device__ __forceinline__ void load_group(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
-                                           uint32_t f0, Group& g) {
-    static_assert(kChunkToks <= 8, "3 bisection steps cover 8 lists");
-    const int je = js + nj;
-    const uint32_t base = gpre[js], total = gpre[je] - base;
-    uint32_t xs[kGroupU];
+// the list of flat round entry g (gpre[ja] <= g < gpre[jb], jb - ja <= 64): the last list
+// starting at or before g, branch-free (a probe past the round reads gpre[jb] > g)
+__device__ __forceinline__ int round_list(const uint32_t* gpre, int ja, int jb, uint32_t g) {
+    int j = ja;
 #pragma unroll
-    for (int u = 0; u < kGroupU; ++u) {
-        const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
-        // last list starting at or before fl, branch-free: a probe past the pass reads
-        // gpre[je] - base = total > fl (the result only matters for fl < total)
-        int j = js;
-        j += gpre[min(j + 4, je)] - base <= fl ? 4 : 0;
-        j += gpre[min(j + 2, je)] - base <= fl ? 2 : 0;
-        j += gpre[min(j + 1, je)] - base <= fl ? 1 : 0;
-        g.jj[u] = fl < total ? j - js : -1;
-        xs[u] = fl < total ? rng[j].x + (fl - (gpre[j] - base)) : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kGroupU; ++u) {
-        g.ent[u] = g.jj[u] >= 0 ? ps.post[xs[u]] : 0u;
-        g.nv[u] = g.jj[u] >= 0 ? ps.pnorm[xs[u]] : 0.0;
-    }
+    for (int s = 32; s > 0; s >>= 1) j += gpre[min(j + s, jb)] <= g ? s : 0;
+    return j;
 }
 
-// f(list - js, entry, norm) for every entry of group g, then for the groups of the pass
-// after the first (long lists only), loaded here
-template <class F>
-__device__ __forceinline__ void walk_pass(const PostStore& ps, const uint2* rng, const uint32_t* gpre, int js, int nj,
-                                          const Group& g, F f) {
-#pragma unroll
-    for (int u = 0; u < kGroupU; ++u)
-        if (g.jj[u] >= 0) f(g.jj[u], g.ent[u], g.nv[u]);
-    const uint32_t total = gpre[js + nj] - gpre[js];
-    for (uint32_t f0 = kGroupU * kPostThreads; f0 < total; f0 += kGroupU * kPostThreads) {
-        Group r;
-        load_group(ps, rng, gpre, js, nj, f0, r);
-#pragma unroll
-        for (int u = 0; u < kGroupU; ++u)
-            if (r.jj[u] >= 0) f(r.jj[u], r.ent[u], r.nv[u]);
+// product of one shared token, recommender.cpp:74-85: wA * wB, wB = tf * idf
+__device__ __forceinline__ double tok_product(const PTok* pt, int j, uint32_t tf) {
+    const PTok v = pt[j];
+    return v.wq * ((double)tf * v.idf);
+}
+
+// The next round from (column ci, token jcur): tokens [ja, jb), columns [ca, ce) touched (ce - 1
+// is left unfinished when ci_next == ce - 1).  Greedy: whole columns while the round holds <= 64
+// tokens and <= kRoundCap entries; a column that does not fit an empty round is split (at least
+// one token, whose entries in the block are <= kBlockCands hits).
+struct Round {
+    int ja, jb, ca, ce;
+};
+__device__ __forceinline__ Round next_round(const QCol* scol, const uint32_t* gpre, int n_act, int& ci, int& jcur) {
+    Round r;
+    r.ja = jcur;
+    r.jb = jcur;
+    r.ca = ci;
+    const uint32_t g0 = gpre[r.ja];
+    while (ci < n_act) {
+        const int j1 = scol[ci].j1;
+        if (j1 - r.ja <= kRoundToks && gpre[j1] - g0 <= (uint32_t)kRoundCap) {
+            r.jb = j1;
+            ++ci;
+            continue;
+        }
+        if (r.jb == r.ja) {
+            int jb = r.ja + 1;
+            const int lim = min(j1, r.ja + kRoundToks);
+            while (jb < lim && gpre[jb + 1] - g0 <= (uint32_t)kRoundCap) ++jb;
+            r.jb = jb;
+            if (jb == j1) ++ci;
+        }
+        break;
     }
+    jcur = r.jb;
+    r.ce = (ci < n_act && scol[ci].j0 < r.jb) ? ci + 1 : ci;
+    return r;
 }
 
 #ifdef PF_K5_TIMERS
@@ -1247,35 +1283,38 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     const uint32_t* excl = reinterpret_cast<const uint32_t*>(img + H.excl_off);
     const int tid = (int)threadIdx.x, lane = tid & 63;
     char* base = smem + sizeof(QConst);
-    uint64_t* tfv = reinterpret_cast<uint64_t*>(base);
-    uint8_t* tfb = reinterpret_cast<uint8_t*>(base);
-    double* nrm = reinterpret_cast<double*>(base + kBlockCands * 8);
-    double* term = reinterpret_cast<double*>(base + kBlockCands * 16);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kBlockCands * 24);
-    uint16_t* list = reinterpret_cast<uint16_t*>(cnt);
-    uint32_t* exb = reinterpret_cast<uint32_t*>(base + kBlockCands * 28);
-    uint32_t* misc = exb + kBlockCands / 32;  // [0]: the next block (dynamic hand-out)
-    QCol* scol = reinterpret_cast<QCol*>(misc + 4);  // the active columns (read at every pass)
-    double* ftab = reinterpret_cast<double*>(scol + kPostMaxCols);  // F = used / (7 + T) by used
-    PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
-    uint2* rng = reinterpret_cast<uint2*>(base + kPostFixedLds + sizeof(PTok) * H.n_tok);
-    uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + H.n_tok + H.n_club + H.n_friend);
+    uint64_t* mask = reinterpret_cast<uint64_t*>(base + kLdsMask);
+    double* slot = reinterpret_cast<double*>(base + kLdsSlot);
+    uint16_t* hit = reinterpret_cast<uint16_t*>(base + kLdsHit);
+    uint16_t* hbase = reinterpret_cast<uint16_t*>(base + kLdsHbase);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kLdsCnt);
+    uint32_t* exb = reinterpret_cast<uint32_t*>(base + kLdsExb);
+    uint32_t* misc = reinterpret_cast<uint32_t*>(base + kLdsMisc);  // [0] next block, [1] hit slots taken
+    QCol* scol = reinterpret_cast<QCol*>(base + kLdsCols);
+    double* ftab = reinterpret_cast<double*>(base + kLdsFtab);  // F = used / (7 + T) by used
+    uint32_t* seg = reinterpret_cast<uint32_t*>(base + kLdsSeg);
     const int nsets = H.n_club + H.n_friend;
     const int nl = H.n_tok + nsets;
+    PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
+    PList* pl = reinterpret_cast<PList*>(pt + H.n_tok);
+    uint2* rng = reinterpret_cast<uint2*>(pl + nl);
+    uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + nl);
+    uint8_t* colof = reinterpret_cast<uint8_t*>(gpre + H.n_tok + 1);  // token -> active column index
     stage(smem, img, sizeof(QConst));
-    for (int j = tid; j < H.n_act; j += kPostThreads) scol[j] = cols[j];
+    for (int j = tid; j < H.n_act; j += kPostThreads) {
+        const QCol c = cols[j];
+        scol[j] = c;
+        for (int x = c.j0; x < c.j1; ++x) colof[x] = (uint8_t)j;
+    }
     for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kPostThreads)
         ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(img)->n_cols);
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
-        PTok v;
-        v.wq = toks[j].wq;
-        v.idf = toks[j].idf;
-        v.p1 = v.wq * (1.0 * v.idf);
-        v.p2 = v.wq * (2.0 * v.idf);
-        pt[j] = v;
+        const QTok t = toks[j];
+        pt[j] = PTok{t.wq, t.idf};
+        pl[j] = t.l;
     }
-#pragma unroll
-    for (int kk = 0; kk < kCandsPerThread; ++kk) tfv[kk * kPostThreads + tid] = 0ull;
+    for (int j = tid; j < nsets; j += kPostThreads) pl[H.n_tok + j] = sets[j];
+    __syncthreads();  // the staged lists are read by other threads (ranges: thread j takes list j)
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
 #ifdef PF_K5_TIMERS
@@ -1292,8 +1331,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
         // 1. ranges of every list in this block; headers of the owned candidates
-        for (int j = tid; j < nl; j += kPostThreads)
-            rng[j] = list_range(ps, j < H.n_tok ? toks[j].l : sets[j - H.n_tok], c0, c1);
+        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
         uint4 ha[kCandsPerThread], hb[kCandsPerThread];
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
@@ -1302,6 +1340,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
             hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
             cnt[kk * kPostThreads + tid] = 0u;
+            mask[kk * kPostThreads + tid] = 0ull;
         }
         if (tid < kBlockCands / 32) exb[tid] = 0u;
         K5T(0);
@@ -1327,7 +1366,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             }
         }
         // 2. clubs / friends
-        walk_lists<false>(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e, double) {
+        walk_sets(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e) {
             const uint32_t p = (e >> 8) - c0;
             if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
@@ -1369,102 +1408,182 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
         }
         K5T(3);
-        __syncthreads();  // the counters' LDS now holds the compacted lists
-        K5T(1);
-        // 4. text columns, ascending.  A pass is one column's tokens js .. js + nj - 1
-        // (nj <= kChunkToks); the first group of the next pass's entries is loaded while
-        // this pass is scored (software pipeline: the loads are the walk's latency).
-        const int n_act = H.n_act;
-        Group ahead;
-        {
-            int c = 0;  // the first column with tokens (columns without any have no passes)
-            while (c < n_act && scol[c].j1 == scol[c].j0) ++c;
-            load_group(ps, rng, gpre, c < n_act ? scol[c].j0 : 0, c < n_act ? min(kChunkToks, scol[c].j1 - scol[c].j0) : 0,
-                       0, ahead);
-        }
-        for (int ci = 0; ci < n_act; ++ci) {
-            const QCol col = scol[ci];
-            const int t = col.t;
-            uint32_t colhit = 0;  // bit kk: owned candidate kk has a hit in column t
-            // a column of more than kChunkToks tokens carries its dot in term[] across passes
-            const bool multi = col.j1 - col.j0 > kChunkToks;
-            if (multi) {
+        // 4. text columns in rounds (ascending tokens = ascending columns, then tids)
+        double cdot[kCandsPerThread], cnrm[kCandsPerThread];  // a split column's dot / norm so far
+        uint32_t chit = 0;                                     // bit kk: the split column has a hit
 #pragma unroll
-                for (int kk = 0; kk < kCandsPerThread; ++kk) term[kk * kPostThreads + tid] = 0.0;
-            }
-            for (int js = col.j0; js < col.j1; js += kChunkToks) {
-                const int nj = min(kChunkToks, col.j1 - js);
-                const bool last = js + kChunkToks >= col.j1;
-                walk_pass(ps, rng, gpre, js, nj, ahead, [&](int j, uint32_t e, double nv) {
-                    const uint32_t p = (e >> 8) - c0;
-                    if (p < B) {
-                        tfb[p * 8 + j] = (uint8_t)(e & 0xFFu);
-                        nrm[p] = nv;
+        for (int kk = 0; kk < kCandsPerThread; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
+        int ci = 0, jcur = 0;
+        while (ci < H.n_act) {
+            const Round R = next_round(scol, gpre, H.n_act, ci, jcur);
+            const int ja = R.ja, jb = R.jb;
+            const uint32_t g0 = gpre[ja], F = gpre[jb] - g0;  // the round's flat entries
+            if (F > 0) {
+                // token segments of the round (read after the walk's barrier)
+                if (tid < jb - ja) {
+                    const int j = ja + tid;
+                    const QCol c = scol[colof[j]];
+                    const int lo = max(c.j0, ja) - ja, hi = min(c.j1, jb) - ja;
+                    seg[tid] = (uint32_t)lo | (uint32_t)hi << 8 | (uint32_t)c.t << 16 |
+                               ((c.j0 < ja || c.j1 > jb) ? kSegSplit : 0u);
+                }
+                if (tid == 0) misc[1] = 0u;
+                // a. walk: the round's entries flattened over the workgroup, all loads in flight
+                constexpr int U = kRoundCap / kPostThreads;
+                uint32_t kp[U];  // p | token << 10 | tf << 16, or ~0
+                double kn[U];
+                {
+                    uint32_t xs[U];
+                    int js[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t f = (uint32_t)(tid + kPostThreads * u);
+                        js[u] = f < F ? round_list(gpre, ja, jb, g0 + f) : -1;
+                        xs[u] = js[u] >= 0 ? rng[js[u]].x + (g0 + f - gpre[js[u]]) : 0u;  // 0: a valid address
                     }
-                });
-                K5T(12);
-                {  // one load site (copies of in-flight registers at a join would wait for them)
-                    int njs = 0, nnj = 0;  // the next pass (none: 0 tokens)
-                    if (!last) {
-                        njs = js + kChunkToks;
-                        nnj = min(kChunkToks, col.j1 - njs);
-                    } else {
-                        int c = ci + 1;
-                        while (c < n_act && scol[c].j1 == scol[c].j0) ++c;
-                        if (c < n_act) {
-                            njs = scol[c].j0;
-                            nnj = min(kChunkToks, scol[c].j1 - njs);
+                    uint32_t ent[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {  // unconditional: every load of the round in flight
+                        ent[u] = ps.post[K5CHK(xs[u], ps.n_tok_entries, 4)];
+                        kn[u] = ps.pnorm[K5CHK(xs[u], ps.n_tok_entries, 5)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t p = (ent[u] >> 8) - c0;
+                        kp[u] = ~0u;
+                        if (js[u] >= 0 && p < B) {
+                            const uint32_t jr = (uint32_t)(js[u] - ja);
+                            kp[u] = p | jr << 10 | (ent[u] & 0xFFu) << 16;
+                            atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << jr);
                         }
                     }
-                    load_group(ps, rng, gpre, njs, nnj, 0, ahead);
+                }
+                for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {  // one-token rounds past the cap
+                    const int j = round_list(gpre, ja, jb, g0 + f);
+                    const uint32_t p = (ps.post[K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 6)] >> 8) - c0;
+                    if (p < B) atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << (j - ja));
                 }
                 K5T(4);
                 __syncthreads();
                 K5T(5);
-                // each wave lists its own hit candidates (ballot + popcount) and scores them
-                // itself: no atomics, and no barrier between listing and scoring
-                uint16_t* wl = list + (tid >> 6) * (kBlockCands / kPostWaves);
-                uint32_t nw = 0;
+                // b. hit slots: the wave's candidates' hits in one contiguous range
+                uint32_t nk[kCandsPerThread], tot = 0;
 #pragma unroll
                 for (int kk = 0; kk < kCandsPerThread; ++kk) {
-                    const int p = kk * kPostThreads + tid;
-                    if (tfv[p] != 0ull) colhit |= 1u << kk;
-                    const bool h = (colhit >> kk) & 1u;
-                    const uint64_t m = __ballot(h);
-                    if (h) wl[nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)p;
-                    nw += (uint32_t)__popcll(m);
+                    nk[kk] = (uint32_t)__popcll(mask[kk * kPostThreads + tid]);
+                    tot += nk[kk];
                 }
-                wave_sync();
-                K5T(6);
-                for (uint32_t i = lane; i < nw; i += 64) {
-                    const int p = wl[i];
-                    uint64_t v = tfv[p];
-                    tfv[p] = 0ull;
-                    double dot = multi ? term[p] : 0.0;
-                    while (v) {  // the hit tokens in ascending order
-                        const int j = (__ffsll((unsigned long long)v) - 1) >> 3;
-                        const uint32_t tf = (uint32_t)(v >> (8 * j)) & 0xFFu;
-                        v &= ~(0xFFull << (8 * j));
-                        const double* pw = &pt[js + j].p1;  // p1, p2, wq, idf
-                        double x;
-                        if (tf <= 2u) x = pw[tf - 1u];
-                        else x = pw[2] * ((double)tf * pw[3]);
-                        dot += x;
+                uint32_t incl = tot;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+                    if (lane >= o) incl += y;
+                }
+                const uint32_t wn = (uint32_t)__shfl((int)incl, 63);
+                uint32_t wb = 0;
+                if (lane == 0) wb = atomicAdd(&misc[1], wn);
+                wb = (uint32_t)__shfl((int)wb, 0);
+                {
+                    uint32_t h0 = wb + incl - tot;
+#pragma unroll
+                    for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                        hbase[kk * kPostThreads + tid] = (uint16_t)h0;
+                        h0 += nk[kk];
                     }
-                    term[p] = !last ? dot : (dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm[p]));
                 }
-                wave_sync();
+                K5T(6);
+                __syncthreads();
+                K5T(1);
+                // c. place every hit at its slot, the column's first hit with its norm
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (kp[u] == ~0u) continue;
+                    const uint32_t p = kp[u] & 1023u, jr = (kp[u] >> 10) & 63u, tf = kp[u] >> 16;
+                    const uint64_t below = mask[p] & low_bits(jr);
+                    const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 8);
+                    const uint32_t lo = seg[jr] & 0xFFu;
+                    const bool first = (below >> lo) == 0ull;
+                    hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
+                    if (first) slot[r] = kn[u];
+                }
+                for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {
+                    const int j = round_list(gpre, ja, jb, g0 + f);
+                    const uint32_t x = K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 7);
+                    const uint32_t e = ps.post[x];
+                    const uint32_t p = (e >> 8) - c0;
+                    if (p >= B) continue;
+                    const uint32_t jr = (uint32_t)(j - ja);
+                    const uint64_t below = mask[p] & low_bits(jr);
+                    const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 9);
+                    const bool first = (below >> (seg[jr] & 0xFFu)) == 0ull;
+                    hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
+                    if (first) slot[r] = ps.pnorm[x];
+                }
                 K5T(7);
                 __syncthreads();
                 K5T(8);
+                // d. terms, one (candidate, column) item per lane over the wave's slots
+                for (uint32_t r = wb + (uint32_t)lane; r < wb + wn; r += 64) {
+                    const uint32_t h = hit[r];
+                    if (!(h & kHitFirst)) continue;
+                    const uint32_t jr = (h >> 8) & 63u, sg = seg[jr];
+                    if (sg & kSegSplit) continue;  // the owner carries a split column
+                    const uint32_t hi = (sg >> 8) & 0xFFu;
+                    const int t = (int)((sg >> 16) & 0xFFu);
+                    double dot = tok_product(pt, ja + (int)jr, h & 0xFFu);
+                    for (uint32_t r2 = r + 1; r2 < wb + wn; ++r2) {  // the column's further hits, tid ascending
+                        const uint32_t h2 = hit[r2];
+                        const uint32_t j2 = (h2 >> 8) & 63u;
+                        if ((h2 & kHitCand) || j2 >= hi) break;
+                        dot += tok_product(pt, ja + (int)j2, h2 & 0xFFu);
+                    }
+                    slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, slot[r]);
+                }
+                wave_sync();
+                K5T(9);
             }
-            // the image lists every non-empty query column, so the common columns are met
-            // here in ascending order (recommender_similarity.cpp:93-113)
+            // e. the owners add the round's finished common columns in ascending order
 #pragma unroll
-            for (int kk = 0; kk < kCandsPerThread; ++kk)
-                if ((pend[kk] >> t) & 1ull) sum[kk] += ((colhit >> kk) & 1u) ? term[kk * kPostThreads + tid] : q.sig0_col[t];
+            for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                const int p = kk * kPostThreads + tid;
+                const uint64_t m = F > 0 ? mask[p] : 0ull;
+                const uint32_t hb0 = F > 0 ? hbase[p] : 0u;
+                for (int c = R.ca; c < R.ce; ++c) {
+                    const QCol col = scol[c];
+                    const int t = col.t;
+                    if (!((pend[kk] >> t) & 1ull)) continue;
+                    const uint32_t lo = (uint32_t)(max(col.j0, ja) - ja), hi = (uint32_t)(min(col.j1, jb) - ja);
+                    const uint64_t h = m & (low_bits(hi) & ~low_bits(lo));
+                    const uint32_t r0 = hb0 + (uint32_t)__popcll(m & low_bits(lo));
+                    if (col.j0 >= ja && col.j1 <= jb) {
+                        sum[kk] += h ? slot[r0] : q.sig0_col[t];
+                        continue;
+                    }
+                    // split column (rare): the dot over its segments in ascending order
+                    if (h) {
+                        uint64_t v = h;
+                        uint32_t r = r0;
+                        while (v) {
+                            const int jr = __ffsll((unsigned long long)v) - 1;
+                            v &= v - 1;
+                            cdot[kk] += tok_product(pt, ja + jr, hit[r++] & 0xFFu);
+                        }
+                        cnrm[kk] = slot[r0];
+                        chit |= 1u << kk;
+                    }
+                    if (col.j1 <= jb) {
+                        const bool hh = (chit >> kk) & 1u;
+                        sum[kk] += (hh && cdot[kk] != 0.0) ? text_term(q, t, cdot[kk], cnrm[kk]) : q.sig0_col[t];
+                        cdot[kk] = 0.0;
+                        chit &= ~(1u << kk);
+                    }
+                }
+                if (F > 0) mask[p] = 0ull;
+            }
+            K5T(10);
+            if (F > 0) __syncthreads();  // the next round rewrites the masks, slots and segments
         }
-        K5T(9);
+        K5T(11);
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
         uint64_t keys[kCandsPerThread];
 #pragma unroll
@@ -1475,37 +1594,33 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 const int uk = (int)((used >> (8 * kk)) & 0xFFu);
                 if (uk > 0) {
                     const double S = sum[kk] / (double)uk;
-                    const double F = ftab[uk];  // (double)uk / (double)(kNumFixed + q.n_cols)
-                    f = (S <= 0.0 && F <= 0.0) ? 0.0f : (float)((2.0 * S * F) / (S + F));
+                    const double Fv = ftab[uk];  // (double)uk / (double)(kNumFixed + q.n_cols)
+                    f = (S <= 0.0 && Fv <= 0.0) ? 0.0f : (float)((2.0 * S * Fv) / (S + Fv));
                 }
                 // keyed by idx (idx order = uid order); uids are filled in before the merge
                 key = score_key(f, (int32_t)(c0 + kk * kPostThreads + tid));
             }
             keys[kk] = key;
         }
-        // each lane's 4 keys ascending, then pushed best-first: after the first push the
-        // wave's threshold rejects most of the rest, so at most one 64-key sort per block
-        static_assert(kCandsPerThread == 4, "4-key sorting network");
-        auto cas = [&](int a, int b) {
-            const uint64_t x = keys[a], y = keys[b];
-            keys[a] = x < y ? x : y;
-            keys[b] = x < y ? y : x;
-        };
-        cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+        // the lane's 2 keys ascending, then pushed best-first: after the first push the
+        // wave's threshold rejects most of the rest
+        static_assert(kCandsPerThread == 2, "2-key sort");
+        if (keys[1] < keys[0]) { const uint64_t x = keys[0]; keys[0] = keys[1]; keys[1] = x; }
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
-        K5T(10);
+        K5T(12);
         if (mode & 1u) {
             // misc[0] was last read before this block's first barrier
             if (tid == 0) misc[0] = (uint32_t)blk_begin + gridDim.x + atomicAdd(next_blk, 1u);
             __syncthreads();
             blk = (int)misc[0];
         } else {
+            __syncthreads();  // the next block rewrites the exclusion bits the owners read above
             blk += (int)gridDim.x;
         }
     }
 #ifdef PF_K5_TIMERS
-    tacc[11] = clock64() - tstart;
+    tacc[13] = clock64() - tstart;
     if (lane == 0) {
         for (int i = 0; i < 14; ++i) atomicAdd(&g_k5t[i], (unsigned long long)tacc[i]);
         atomicAdd(&g_k5t[15], 1ull);
@@ -1516,8 +1631,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         const uint32_t idx = (uint32_t)best ^ 0x80000000u;
         best = (best & 0xFFFFFFFF00000000ull) | (ps.hdr[2 * (size_t)idx + 1].w ^ 0x80000000u);
     }
-    // tail scratch in the (idle) tf-byte array: merge keys, then flag / threshold / block ids
-    scan_tail(best, k, tfv, reinterpret_cast<int*>(tfv + kPostWaves * kMaxTopK), sync, parts, out, out_rows);
+    // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
+    uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
+    scan_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows);
 }
 
 // ---------------------------------------------------------------- K2: merge
@@ -1735,25 +1851,6 @@ __global__ __launch_bounds__(kPairThreads) void union_walk_kernel(DevStore st, c
     }
 }
 
-// ---------------------------------------------------------------- K4: collaborative sum
-// For each collaborative query J (blockIdx.y): score(c) = sum over friend-list positions j (in
-// order) of (double)w[j] * (double)M[row[j]][c] (recommender_graph.cpp:167-180); row[j] < 0 ->
-// friend skipped.  One launch serves a batch of queries.
-__global__ __launch_bounds__(256) void collab_sum_kernel(const float* __restrict__ M, const float* __restrict__ w,
-                                                         const int32_t* __restrict__ row,
-                                                         const CollabSum* __restrict__ jobs, float* __restrict__ out) {
-    const CollabSum J = jobs[blockIdx.y];
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= J.nc) return;
-    double s = 0.0;
-    for (int j = 0; j < J.F; ++j) {
-        const int r = row[J.woff + j];
-        if (r < 0) continue;
-        s += (double)w[J.woff + j] * (double)M[J.moff + (size_t)r * J.nc + c];
-    }
-    out[J.coff + c] = (float)s;
-}
-
 // ---------------------------------------------------------------- launchers
 hipError_t launch_scan(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t lds, bool gtab,
                        int nq, int tile_begin, int tile_end, int k, int blocks, uint64_t* parts, ScanSync* sync,
@@ -1785,9 +1882,10 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
     return last_nb;
 }
 
-// K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | ranges[n_lists] | prefix[n_tok + 1]
+// K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | PList[n_lists] | ranges[n_lists] |
+// prefix[n_tok + 1] | token -> column u8[n_tok]
 uint32_t post_var_lds(int n_tok, int n_lists) {
-    return (uint32_t)(sizeof(PTok) * n_tok + 8 * n_lists + 4 * (n_tok + 1) + 15) & ~15u;
+    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 4 * (n_tok + 1) + n_tok + 15) & ~15u;
 }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 
@@ -1805,11 +1903,12 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
         unsigned long long t[16];
         hipStreamSynchronize(s);
         hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k5t), sizeof(t));
-        static const char* nm[14] = {"ranges+hdr", "barriers", "excl+sets", "fixed", "next-load", "walk-bar",
-                                     "compact", "dense", "pass-bar", "owner-add", "fas+topk", "total", "walk", "-"};
+        static const char* nm[14] = {"ranges+hdr", "barriers", "excl+sets", "fixed", "walk", "walk-bar",
+                                     "slots", "place", "place-bar", "terms", "owner-add", "rounds-end", "fas+topk",
+                                     "total"};
         if (++calls % 10 == 0) {
             fprintf(stderr, "k5t per wave (clock64):");
-            for (int i = 0; i < 13; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[15]);
+            for (int i = 0; i < 14; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[15]);
             fprintf(stderr, "\n");
         }
         const unsigned long long z[16] = {0};
@@ -1904,11 +2003,5 @@ hipError_t launch_pairs_prewalked(const DevStore& st, const uint8_t* pool, const
     return hipGetLastError();
 }
 
-hipError_t launch_collab_sum(const float* M, const float* w, const int32_t* row, const CollabSum* jobs, int njobs,
-                             int max_nc, float* out, hipStream_t s) {
-    if (njobs <= 0 || max_nc <= 0) return hipSuccess;
-    hipLaunchKernelGGL(collab_sum_kernel, dim3((max_nc + 255) / 256, njobs), dim3(256), 0, s, M, w, row, jobs, out);
-    return hipGetLastError();
-}
 
 }  // namespace pf

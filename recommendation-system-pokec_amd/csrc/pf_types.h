@@ -191,11 +191,14 @@ struct DevStore {
 // candidates holding it, so a query reads only the lists it names instead of every record.
 // Candidates are in idx order (ascending uid, the reference's tie-break order); a workgroup
 // scores one block of kBlockCands consecutive candidates at a time.
-constexpr int kBlockCands = 1024;          // LDS capacity of a workgroup block (4 candidates per thread)
+constexpr int kBlockCands = 512;           // candidates of a workgroup block (2 per thread)
 constexpr int kPostWaves = 4;              // waves per K5 workgroup
 constexpr int kPostThreads = kPostWaves * kWave;
 constexpr int kCandsPerThread = kBlockCands / kPostThreads;
-constexpr int kChunkToks = 8;              // query tokens of one column handled per pass (one tf byte each)
+// K5 rounds: a block's query tokens are taken in rounds of <= kRoundToks tokens (one 64-bit hit
+// mask per candidate) whose list entries in the block number <= kRoundCap (the round's hit slots)
+constexpr int kRoundToks = 64;
+constexpr int kRoundCap = 2048;
 constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
 constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
 constexpr int kPostMinShift = 9;           // cells of >= 512 candidates: a block spans at most 3
@@ -236,7 +239,10 @@ struct PostStore {
     const uint32_t* cells;
     int32_t n;                // candidates
     int32_t n_blocks;         // ceil(n / bsize)
-    int32_t bsize;            // candidates per block (<= kBlockCands), chosen so the blocks fill whole waves of resident workgroups
+    int32_t bsize;            // candidates per block (<= kBlockCands)
+    uint32_t n_post;          // entries of post (token entries first: pnorm has n_tok_entries)
+    uint32_t n_tok_entries;
+    uint32_t n_cells;
 };
 
 

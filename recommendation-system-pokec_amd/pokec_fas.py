@@ -48,7 +48,8 @@ class PfLayoutStats(ctypes.Structure):
 class PfJobsStats(ctypes.Structure):
     _fields_ = [("jobs", ctypes.c_int64), ("candidates", ctypes.c_int64), ("pairs", ctypes.c_int64),
                 ("pair_alg_bytes", ctypes.c_int64), ("pair_record_bytes", ctypes.c_int64),
-                ("pair_image_bytes", ctypes.c_int64), ("pair_ms", ctypes.c_double), ("pair_launches", ctypes.c_int64)]
+                ("pair_image_bytes", ctypes.c_int64), ("pair_ms", ctypes.c_double), ("pair_launches", ctypes.c_int64),
+                ("pair_dispatches", ctypes.c_int64)]
 
 
 class PfDatasetInfo(ctypes.Structure):
@@ -152,14 +153,19 @@ class FasEngine:
         L = lib()
         self._L = L
         self.h = ctypes.c_void_p()
+        # in-flight asynchronous calls by ticket: the C side writes their outputs into these arrays
+        # whenever the queue drains (pf_wait, or any synchronous call), so the engine, not the
+        # caller's handle, keeps them alive until a wait covers them or the engine closes
+        self._inflight = {}
         rc = L.pf_open(desc_ptr, device, ctypes.byref(self.h))
         if rc != PF_OK:
             raise FasError(f"pf_open failed ({rc}): {L.pf_last_error(None).decode()}")
 
     def close(self):
         if getattr(self, "h", None):
-            self._L.pf_close(self.h)
+            self._L.pf_close(self.h)  # drops never-waited calls without writing their outputs
             self.h = None
+        getattr(self, "_inflight", {}).clear()
 
     def __del__(self):
         try:
@@ -215,7 +221,9 @@ class FasEngine:
         t = ctypes.c_uint64()
         self._check(getattr(self._L, fn)(self.h, q.ctypes.data, len(q), k, limit, ou.ctypes.data, os_.ctypes.data,
                                          oc.ctypes.data, ctypes.byref(t)), fn)
-        return FasEngine.Pending(q, k, ou, os_, oc, t.value)
+        p = FasEngine.Pending(q, k, ou, os_, oc, t.value)
+        self._inflight[p.ticket] = p
+        return p
 
     def recommend_interest_async(self, users, topk, candidate_limit=10000):
         return self._topk_async("pf_recommend_interest_async", users, topk, candidate_limit)
@@ -229,6 +237,8 @@ class FasEngine:
     def wait(self, p):
         """Results of an asynchronous call (and of every earlier one), as the synchronous form's."""
         self._check(self._L.pf_wait(self.h, p.ticket), "pf_wait")
+        for t in [t for t in self._inflight if t <= p.ticket]:  # pf_wait finished every call up to p
+            del self._inflight[t]
         k = p.k
         return [(p.ou[i * k:i * k + p.oc[i]].copy(), p.os[i * k:i * k + p.oc[i]].copy()) for i in range(len(p.q))]
 

@@ -1,0 +1,45 @@
+# One parameterised GPU-box script for the round's runs (replaces the per-run tools/gpu_r3*.sh).
+#   bash tools/gpu_round.sh TAG STEP [STEP ...]
+# Steps (each under its own time limit, chained: the first failure ends the script):
+#   tests        full GPU suite                         -> gpurun_out/TAG/gputest.log
+#   tests:EXPR   GPU tests matching -k EXPR             -> gpurun_out/TAG/gputest_k.log
+#   bench        default bench line (cfg 2, CPU baseline + PMC pass) -> bench.json
+#   prof         rocprofv3 kernel trace + stats of a 20-step cfg-2 run -> prof_default/
+#   cfgN         bench.py --workload cfgN               -> cfgN.json
+#   quick        cfg 2, 100 steps, no CPU baseline / PMC -> quick.json
+#   quick4       cfg 4, 3 steps, no CPU baseline / PMC   -> quick4.json
+#   k5t          profiling build (make K5T=1 into exp/k5t) per-phase K5 clocks -> k5t.err
+#   pmc:NAME:C1,C2..  one rocprofv3 --pmc pass over a 20-step cfg-2 run -> pmc_NAME/
+set -o pipefail
+TAG=$1
+shift
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp
+O=gpurun_out/$TAG
+Q="--no-cpu-baseline --no-pmc"
+for S in "$@"; do
+    echo "== $S $(date +%T)"
+    case $S in
+    tests)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || exit 1 ;;
+    tests:*)
+        timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${S#tests:}" > $O/gputest_k.log 2>&1 || exit 1 ;;
+    bench)
+        timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 2 ;;
+    prof)
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/prof.json 2> $O/prof.err || exit 3 ;;
+    cfg[2345])
+        timeout -k 10 900 python3 bench.py --workload $S > $O/$S.json 2> $O/$S.err || exit 4 ;;
+    quick)
+        timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 $Q > $O/quick.json 2> $O/quick.err || exit 5 ;;
+    quick4)
+        timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
+    k5t)
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/k5t/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/k5t.json 2> $O/k5t.err || exit 7 ;;
+    pmc:*)
+        R=${S#pmc:}; N=${R%%:*}; C=${R#*:}
+        timeout -s KILL 120 rocprofv3 --pmc ${C//,/ } -d $O/pmc_$N -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmc_$N.json 2> $O/pmc_$N.err || exit 8 ;;
+    *)
+        echo "unknown step $S"; exit 9 ;;
+    esac
+done
+echo "== done $(date +%T)"

@@ -831,13 +831,16 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     }
     __syncthreads();
     const QConst* q = reinterpret_cast<const QConst*>(smem);
+    // the image's sizes are workgroup-uniform: read into SGPRs (as LDS loads they would sit in a
+    // VGPR each for the whole kernel, and the walk loops are register-bound)
+    auto uni = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     QView v;
     v.q = q;
-    v.lg = q->lg;
-    v.lge = q->lg_excl;
-    v.hmul = q->hmul;
-    v.excl_off = q->excl_off;
-    const uint32_t kb = 8u * (q->excl_off + (1u << q->lg_excl)), vb = (uint32_t)q->n_vals * 16u;
+    v.lg = (int)uni((uint32_t)q->lg);
+    v.lge = (int)uni((uint32_t)q->lg_excl);
+    v.hmul = uni(q->hmul);
+    v.excl_off = uni(q->excl_off);
+    const uint32_t kb = 8u * (v.excl_off + (1u << v.lge)), vb = uni((uint32_t)q->n_vals) * 16u;
     char* p = smem + sizeof(QConst);
     if constexpr (!GTAB) {
         v.tab = reinterpret_cast<const uint2*>(p);
@@ -848,7 +851,7 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
         v.vals = reinterpret_cast<const QVal*>(pool + (size_t)r.const_off * 16u + r.vals_off);
     }
     v.hits = p;
-    p += (size_t)q->n_hits_max * blockDim.x;  // n_hits_max = bytes per lane of the hit list
+    p += (size_t)uni(q->n_hits_max) * blockDim.x;  // n_hits_max = bytes per lane of the hit list
     v.nh = reinterpret_cast<uint32_t*>(p);     // per-thread hit counts (split records)
     p += 4u * blockDim.x;
     *scratch = p;
@@ -1034,12 +1037,10 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         const int cand = lane >> lgk, ci = lane & ((1 << lgk) - 1);
         const bool active = cand < min(kTileSlots >> lgk, st.n_slots - slot0);
         const int p = slot0 + cand;
+        // h0 / h1 are loaded after the walk (the epilogue's first reads): holding them across the
+        // walk's double buffer spilled registers
         uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, h2 = h0;
-        if (active) {
-            h0 = st.hdr0[p];
-            h1 = st.hdr1[p];
-            h2 = st.hdr2[p];
-        }
+        if (active) h2 = st.hdr2[p];
         const uint32_t nc = h2.y, nset = h2.y + h2.z;
         const uint32_t len = record_words(h2, PACKED);
         const uint32_t q = chunk_words(len, lgk, PACKED);
@@ -1050,26 +1051,22 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         W.cnt = 0; W.nh = 0; W.pend = 0;
         if (!PACKED && clen > 0 && j0 > 0) W.pend = word_at(st, l, q, j0 - 1);  // a token pair may straddle chunks
         walk_chunk<PACKED, false>(W, st.stream + st.tile_off[tile] + lane, j0, clen, nc, nset, v, blockDim.x);
+        // one epilogue site (a second inlined copy for split records cost K1 64 B of scratch per
+        // lane): a split record sums its chunk counters over its lanes, publishes the hit counts,
+        // and its first lane finishes it; a whole record (lgk = 0) is the one-chunk case
+        if (active) {
+            h0 = st.hdr0[p];
+            h1 = st.hdr1[p];
+        }
         float f = 0.0f;
-        if (lgk == 0) {
-            if (active) {
-                const uint32_t nh = W.nh;
-                const TileRec rec{&st, l, q};
-                f = fas_epilogue<PACKED>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
-            }
-        } else {
-            // a split record: sum the chunk counters over its lanes, publish the hit counts,
-            // and let the record's first lane finish it
-            uint32_t cnt = W.cnt;
-            for (int m = 1; m < (1 << lgk); m <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, m);
-            v.nh[threadIdx.x] = W.nh;
-            __builtin_amdgcn_wave_barrier();
-            if (active && ci == 0) {
-                const uint32_t* nhp = v.nh + threadIdx.x;
-                const TileRec rec{&st, l, q};
-                f = fas_epilogue<PACKED>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u << lgk,
-                                         [&](uint32_t g) { return nhp[g]; });
-            }
+        uint32_t cnt = W.cnt;
+        for (int m = 1; m < (1 << lgk); m <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, m);
+        v.nh[threadIdx.x] = W.nh;
+        __builtin_amdgcn_wave_barrier();
+        if (active && ci == 0) {
+            const uint32_t* nhp = v.nh + threadIdx.x;
+            const TileRec rec{&st, l, q};
+            f = fas_epilogue<PACKED>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u << lgk, [&](uint32_t g) { return nhp[g]; });
         }
         uint64_t key = ~0ull;
         if (active && ci == 0) {

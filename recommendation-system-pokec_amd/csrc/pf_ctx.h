@@ -112,8 +112,6 @@ struct JobsState {
     // stream (both latency-bound, independent), joined before the pair kernel
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool union_on = false;                       // collaborative friend groups walk each record once (K6u / K1u;
-                                                 // opt-in, PF_DEBUG union=1: measured slower)
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
     std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;
@@ -129,7 +127,6 @@ struct JobsState {
     // 0.344 -> 0.385 ms beside the next call's images and gathers; cfg 3 1.93e9 -> 1.71e9).
     struct Ws {
         DBuf d_plan, d_ht, d_seq, d_slots, d_ids, d_fl, d_img, d_scr;  // d_plan: the plan, then the results
-        DBuf d_upool, d_hb, d_hc;  // K6u union tables; K1u walk results (hit words, counts) per pair index
         DBuf d_acc;                // clubs accumulators (zero between uses)
         DBuf d_parts;              // K4''s per-block top-k lists (the fused collaborative top-k)
         int64_t acc_jobs = 0;      // clubs jobs the accumulators hold

@@ -11,8 +11,6 @@
 //   load_threads=N        loader threads (default: min(16, hardware threads))
 //   resident_images=0     the job pipeline builds its query images per call (K6) instead of
 //                         referencing the ones built for every user at open
-//   union=1               collaborative friend groups walk each candidate record once (K6u / K1u;
-//                         measured slower than the pair walks)
 //   host_prof=1           host stage clocks on stderr (pf_open, the loaders, the job pipeline)
 //
 // e.g. PF_DEBUG=scan=stream,stage_limit=0

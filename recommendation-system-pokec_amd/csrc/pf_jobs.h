@@ -27,10 +27,6 @@ constexpr uint32_t kImgLdsSmall = 16 * 1024;
 hipError_t launch_qimages(const DevStore& st, const DevJobsStore& g, const ImgJob* ij, int n_small, int n_big, int n_glob,
                           uint8_t* pool, uint32_t* scratch, int32_t* fail, hipStream_t s);
 uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed);
-// K6u: the union key tables of n friend groups (pf_kernels.h UnionJob; writes their hmul)
-hipError_t launch_unions(const DevStore& st, const DevJobsStore& g, UnionJob* uj, int n, uint32_t max_lds, uint8_t* upool,
-                         int32_t* fail, hipStream_t s);
-uint32_t union_lds(int dlg, int words);
 // K4' (+ the fused top-k of jobs with topk <= kMaxTopK: parts = gridDim.x * k keys per job,
 // tickets = one zeroed counter per job, out = the chunk's key rows, k = their width)
 hipError_t launch_collab(const DevJob* jobs, const int32_t* jix, int njobs, int max_cap, const int32_t* pool,
@@ -42,9 +38,9 @@ hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* j
 // the pair blocks' dispatch order, longest first record first (pf_jobs.hip order_pairs_kernel)
 hipError_t launch_order_pairs(const PairBlock* blocks, int nblocks, const int32_t* slots, int32_t n_slots,
                               int32_t* order, hipStream_t s);
-// mode 0: pair blocks that walk; 1: pre-walked pair blocks (hc: K1u's counts); 2: K1u walk blocks
+// pair counts and bytes of the pair blocks (pf_jobs_stats)
 hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
-                             unsigned long long* acc, int mode, const uint2* hc, const UnionJob* uj, hipStream_t s);
+                             unsigned long long* acc, hipStream_t s);
 hipError_t launch_job_topk(const DevJob* jobs, const int32_t* jix, int njobs, const float* score, const int32_t* ids,
                            const int32_t* slots, const int32_t* ncand, uint64_t* out, int k, hipStream_t s);
 

@@ -638,102 +638,6 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
     if (tid == 0) atomicOr(fail, 1);
 }
 
-// ---------------------------------------------------------------- K6u: union key tables
-// One workgroup per friend group of a collaborative job (pf_kernels.h UnionJob): every word of the
-// friends' records as the pair walk probes it (club / friend words themselves, tokens as kTagTok |
-// col << 18 | tid) goes into an LDS de-duplication set that ORs in the friend's bit; the distinct
-// (key, mask) items are then placed in a 2-choice cuckoo table (K6's parallel insertion with
-// atomic exchange, a new multiplier after a failed attempt) that aliases the set, and copied out.
-// Empty slots are {~0, 0}: a miss reads mask 0, and no record word is ~0 past its record's end.
-__global__ __launch_bounds__(kJobThreads) void union_kernel(DevStore st, DevJobsStore g, UnionJob* __restrict__ uj,
-                                                            uint8_t* __restrict__ upool, int32_t* __restrict__ fail) {
-    __shared__ int s_fail, s_n;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x;
-    const int n = uj[blockIdx.x].n, lg = uj[blockIdx.x].lg, dlg = uj[blockIdx.x].dlg;
-    const uint32_t dsz = 1u << dlg, dmask = dsz - 1u, tsz = 1u << lg;
-    uint32_t* dk = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* dm = dk + dsz;
-    uint64_t* items = reinterpret_cast<uint64_t*>(dm + dsz);
-    for (uint32_t i = tid; i < dsz; i += kJobThreads) {
-        dk[i] = kPadWord;
-        dm[i] = 0u;
-    }
-    if (tid == 0) {
-        s_fail = 0;
-        s_n = 0;
-    }
-    __syncthreads();
-    for (int f = 0; f < n; ++f) {
-        const int p = g.slot_of[uj[blockIdx.x].idx[f]];
-        const uint4 h2 = st.hdr2[p];
-        const uint32_t nset = h2.y + h2.z, len = record_words(h2, true);
-        const uint32_t* rw = reinterpret_cast<const uint32_t*>(st.rows + st.row_off[p]);
-        for (uint32_t j = tid; j < len; j += kJobThreads) {
-            const uint32_t w = rw[j];
-            const uint32_t key = j < nset ? w : (kTagTok | (w & 0xFFFFFFu));
-            uint32_t h = (key * kHashMul) >> (32 - dlg);
-            for (;;) {
-                const uint32_t old = atomicCAS(&dk[h], kPadWord, key);
-                if (old == kPadWord || old == key) {
-                    atomicOr(&dm[h], 1u << f);
-                    break;
-                }
-                h = (h + 1u) & dmask;
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < dsz; i += kJobThreads)
-        if (dk[i] != kPadWord) items[atomicAdd(&s_n, 1)] = make_entry(dk[i], dm[i]);
-    __syncthreads();
-    const uint32_t nuniq = (uint32_t)s_n;
-    uint64_t* tab = reinterpret_cast<uint64_t*>(smem);  // the set is consumed (tsz <= dsz / 2 entries of 8 B)
-    for (uint32_t s = 0; s < 16; ++s) {
-        const uint32_t hmul = kHashMul + 2u * s * 0x6A09E667u;
-        for (uint32_t i = tid; i < tsz; i += kJobThreads) tab[i] = kEmptyEntryPacked;
-        __syncthreads();
-        for (uint32_t i = tid; i < nuniq; i += kJobThreads) {
-            uint64_t cur = items[i];
-            uint32_t x = cuckoo_x((uint32_t)cur, hmul);
-            uint32_t at = cuckoo_h1(x, lg);
-            bool placed = false;
-            for (int kick = 0; kick < 500; ++kick) {
-                const uint64_t old = (uint64_t)atomicExch(reinterpret_cast<unsigned long long*>(&tab[at]),
-                                                          (unsigned long long)cur);
-                if (old == kEmptyEntryPacked) { placed = true; break; }
-                cur = old;
-                x = cuckoo_x((uint32_t)cur, hmul);
-                const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
-                at = at == a ? b : a;
-            }
-            if (!placed) atomicOr(&s_fail, 1);
-        }
-        __syncthreads();
-        const int failed = s_fail;
-        __syncthreads();
-        if (!failed) {
-            if (tid == 0) uj[blockIdx.x].hmul = hmul;
-            uint64_t* out = reinterpret_cast<uint64_t*>(upool + uj[blockIdx.x].tab_off);
-            for (uint32_t i = tid; i < tsz; i += kJobThreads) out[i] = tab[i];
-            return;
-        }
-        if (tid == 0) s_fail = 0;
-        __syncthreads();
-    }
-    if (tid == 0) atomicOr(fail, 1);
-}
-
-// LDS bytes of a union build: the de-duplication set (8 B per slot, the table aliases it) + items
-uint32_t union_lds(int dlg, int words) { return (8u << dlg) + 8u * (uint32_t)words; }
-
-hipError_t launch_unions(const DevStore& st, const DevJobsStore& g, UnionJob* uj, int n, uint32_t max_lds, uint8_t* upool,
-                         int32_t* fail, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(union_kernel, dim3(n), dim3(kJobThreads), max_lds, s, st, g, uj, upool, fail);
-    return hipGetLastError();
-}
-
 // LDS bytes of an image's build (table + item list + set), pf_jobs_plan.cpp splits the launch by it
 uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed) {
     const uint64_t b = 8ull * (((uint64_t)(packed ? 1 : 3) << lg) + (1ull << lge)) + 8ull * nitems + 4ull * (1ull << dlg);
@@ -1063,17 +967,11 @@ __global__ __launch_bounds__(kJobThreads) void topk_kernel(const DevJob* __restr
 // ---------------------------------------------------------------- pair statistics
 // (pf_jobs_stats) per scored pair: 1, SURVEY 8(d) D3's b_c of the candidate, and the bytes the
 // pair-scoring stage reads / writes for it by access pattern:
-//   mode 0 (K1' walks the pair):  48-B headers + 8-B row offset + its record words;
-//   mode 1 (K1' pre-walked pair): 48-B headers + 8-B row offset + its K1u counts (8 B) and hit
-//                                 words (4 B each; an overflowed list: its record words instead);
-//   mode 2 (a K1u walk block, no pairs of its own): per candidate its 16-B header + row offset +
-//                                 record words once, and per friend of the group the counts and hit
-//                                 words it writes.
+// 48-B headers + 8-B row offset + its record words (K1' walks the pair's record).
 template <bool PACKED>
 __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const PairBlock* __restrict__ blocks,
                                                          const int32_t* __restrict__ slots,
-                                                         unsigned long long* __restrict__ acc, int mode,
-                                                         const uint2* __restrict__ hc, const UnionJob* __restrict__ uj) {
+                                                         unsigned long long* __restrict__ acc) {
     __shared__ unsigned long long red[3][4];
     const PairBlock b = blocks[blockIdx.x];
     const int i = threadIdx.x;
@@ -1083,23 +981,9 @@ __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const Pair
         if (p >= 0) {
             const uint4 h2 = st.hdr2[p];
             const unsigned long long rec = 4ull * record_words(h2, PACKED);
-            if (mode == 2) {
-                const UnionJob U = uj[b.qimg];
-                v[2] += 24ull + rec;
-                for (int g = 0; g < U.n; ++g) {
-                    const uint32_t nh = hc[(uint64_t)b.out + (uint64_t)g * (uint32_t)U.ostride + (uint64_t)x].y;
-                    v[2] += 8ull + 4ull * (nh < kHitCap ? nh : kHitCap);
-                }
-                continue;
-            }
             v[0] += 1ull;
             v[1] += 32ull + 4ull * (h2.y + h2.z) + 8ull * h2.w;
-            if (mode == 1) {
-                const uint32_t nh = hc[(uint64_t)b.out + (uint64_t)x].y;
-                v[2] += 56ull + 8ull + (nh > kHitCap ? rec : 4ull * nh);
-            } else {
-                v[2] += 56ull + rec;
-            }
+            v[2] += 56ull + rec;
         }
     }
 #pragma unroll
@@ -1121,12 +1005,12 @@ __global__ __launch_bounds__(256) void pair_stats_kernel(DevStore st, const Pair
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nblocks, const int32_t* slots,
-                             unsigned long long* acc, int mode, const uint2* hc, const UnionJob* uj, hipStream_t s) {
+                             unsigned long long* acc, hipStream_t s) {
     if (nblocks <= 0) return hipSuccess;
     if (st.packed)
-        hipLaunchKernelGGL(pair_stats_kernel<true>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc, mode, hc, uj);
+        hipLaunchKernelGGL(pair_stats_kernel<true>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc);
     else
-        hipLaunchKernelGGL(pair_stats_kernel<false>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc, mode, hc, uj);
+        hipLaunchKernelGGL(pair_stats_kernel<false>, dim3(nblocks), dim3(256), 0, s, st, blocks, slots, acc);
     return hipGetLastError();
 }
 

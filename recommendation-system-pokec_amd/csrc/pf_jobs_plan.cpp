@@ -387,7 +387,6 @@ int jobs_open(pf_ctx* c) {
     J.view_over = nullptr;
     J.view_over_n = 0;
     J.nodes_dirty = false;
-    J.union_on = packed && debug_long("union", 0) != 0;
     sc.lap("handles");
     const int rc = build_resident_images(c);
     if (rc != PF_OK) return rc;
@@ -674,14 +673,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     };
     std::vector<int32_t> jix_collab, jix_clubs, jix_topk, jix_fused;
     int max_cap_collab = 0, ktop = 1;
-    // collaborative friend groups (K6u / K1u): their pairs' walks happen once per group in K1u,
-    // and K1' runs only their epilogues (pblocks)
     const int lge = lg_for(0);
     auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
-    std::vector<UnionJob> ujobs;
-    std::vector<PairBlock> wblocks, pblocks;
-    size_t upool = 0;
-    uint32_t max_ulds = 0, max_wlds = 0;
     {
         size_t nb = 0, words = 0;  // the blocks and pool words this chunk appends (one allocation)
         for (size_t i = b; i < e; ++i) {
@@ -754,57 +747,11 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                 const int64_t span = kPairSpan;
                 std::vector<int32_t> fimg(d.nfd);
                 for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
-                // friend groups: consecutive friends whose images are LDS-staged, up to kUnionMax of
-                // them and kUnionKeys record words (a group of one walks as a plain pair)
-                std::vector<std::pair<int, int>> grp;
-                std::vector<uint8_t> in_grp(d.nfd, 0);
-                if (J.union_on && p.cap > 0) {
-                    auto words = [&](int r) { return (int64_t)J.img_nset[p.fd[r]] + ntok_of(p.fd[r]); };
-                    auto ok = [&](int r) {
-                        const int32_t idx = p.fd[r];
-                        const int lgi = J.img_lg[idx];
-                        if (lgi == 0 || words(r) > kUnionKeys) return false;
-                        const size_t kv = 8 * (((size_t)1 << lgi) + ((size_t)1 << lge)) + (size_t)ntok_of(idx) * sizeof(QVal);
-                        return kv <= kStageLimitJobs;
-                    };
-                    for (int r = 0; r < d.nfd;) {
-                        int r1 = r;
-                        int64_t w = 0;
-                        while (r1 < d.nfd && r1 - r < kUnionMax && ok(r1) && w + words(r1) <= kUnionKeys) w += words(r1++);
-                        if (r1 - r >= 2) {
-                            grp.emplace_back(r, r1);
-                            for (int q = r; q < r1; ++q) in_grp[q] = 1;
-                            UnionJob U{};
-                            U.n = r1 - r;
-                            U.words = (int32_t)w;
-                            U.lg = pow2_lg(w * 5 / 2 + 1);  // load <= 0.4
-                            U.dlg = std::max(U.lg, pow2_lg(2 * w));
-                            U.tab_off = (uint32_t)upool;
-                            U.ostride = (int32_t)p.cap;
-                            for (int q = r; q < r1; ++q) U.idx[q - r] = p.fd[q];
-                            upool += (size_t)8 << U.lg;
-                            max_ulds = std::max(max_ulds, union_lds(U.dlg, U.words));
-                            max_wlds = std::max(max_wlds, 8u << U.lg);
-                            ujobs.push_back(U);
-                        }
-                        r = r1 > r ? r1 : r + 1;
-                    }
-                }
-                const int32_t u0 = (int32_t)ujobs.size() - (int32_t)grp.size();
                 for (int64_t x = 0; x < p.cap; x += span) {
                     const int32_t cnt = (int32_t)std::min<int64_t>(span, p.cap - x);
                     for (int r = 0; r < d.nfd; ++r)
-                        if (!in_grp[r])
-                            blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
-                                                       (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
-                    for (size_t gi = 0; gi < grp.size(); ++gi) {
-                        const int r0 = grp[gi].first;
-                        wblocks.push_back(PairBlock{u0 + (int32_t)gi, (int32_t)(d.cand_off + x), cnt,
-                                                    (int32_t)(d.m_off + (int64_t)r0 * p.cap + x)});
-                        for (int r = r0; r < grp[gi].second; ++r)
-                            pblocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
-                                                        (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
-                    }
+                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
+                                                   (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
                 }
                 jix_collab.push_back(jn);
                 max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);
@@ -850,11 +797,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (size_t k = 0; k < img_idx.size(); ++k) order[pos[k]] = img_idx[k];
         img_idx.swap(order);
         for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
-        for (PairBlock& pb : pblocks) pb.qimg = pos[pb.qimg];
     }
     std::vector<ImgJob> ij(resident ? 0 : img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
-    uint32_t max_lds = 0;
     size_t ipool = 0;
     int64_t scr = 0;
     for (size_t k = 0; k < img_idx.size(); ++k) {
@@ -886,9 +831,6 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         }
         const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
         r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;
-        const uint32_t need = (uint32_t)sizeof(QConst) + r.lds_bytes + kHitSlots * (packed ? 4u : 8u) * kPairThreads +
-                              4u * kPairThreads + 2048u;
-        max_lds = std::max(max_lds, need);
     }
     // The pair blocks in three launches by their image: LDS-staged images whose block fits two
     // workgroups per CU, larger LDS-staged ones, global-memory tables.  One launch sized for the
@@ -925,10 +867,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_ij = a16z(o_p64 + pool64.size() * 8);
     const size_t o_refs = a16z(o_ij + ij.size() * sizeof(ImgJob));
     const size_t o_blk = a16z(o_refs + refs.size() * sizeof(QImageRef));
-    const size_t o_uj = a16z(o_blk + blocks.size() * sizeof(PairBlock));
-    const size_t o_wb = a16z(o_uj + ujobs.size() * sizeof(UnionJob));
-    const size_t o_pb = a16z(o_wb + wblocks.size() * sizeof(PairBlock));
-    const size_t o_jc = a16z(o_pb + pblocks.size() * sizeof(PairBlock));
+    const size_t o_jc = a16z(o_blk + blocks.size() * sizeof(PairBlock));
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
     const size_t o_tk = a16z(o_jt + jix_topk.size() * 4);  // K4' top-k tickets (zero), one per collaborative job
@@ -945,17 +884,13 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_ij, ij.data(), ij.size() * sizeof(ImgJob));
     put(o_refs, refs.data(), refs.size() * sizeof(QImageRef));
     put(o_blk, blocks.data(), blocks.size() * sizeof(PairBlock));
-    put(o_uj, ujobs.data(), ujobs.size() * sizeof(UnionJob));
-    put(o_wb, wblocks.data(), wblocks.size() * sizeof(PairBlock));
-    put(o_pb, pblocks.data(), pblocks.size() * sizeof(PairBlock));
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
     if (!jix_collab.empty()) std::memset(h + o_tk, 0, jix_collab.size() * 4);
     std::memset(h + o_res, 0, 16);
-    const size_t o_ord = a16z(o_res + res_b);  // the pair / walk blocks' dispatch orders (device-written)
-    const size_t o_word = a16z(o_ord + std::max<size_t>(blocks.size(), 1) * 4);
-    HIPCHK(c, W.d_plan.reserve(o_word + std::max<size_t>(wblocks.size(), 1) * 4));
+    const size_t o_ord = a16z(o_res + res_b);  // the pair blocks' dispatch order (device-written)
+    HIPCHK(c, W.d_plan.reserve(o_ord + std::max<size_t>(blocks.size(), 1) * 4));
     if (J.aux == nullptr) {
         HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming));
@@ -973,10 +908,6 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const ImgJob* d_ij = reinterpret_cast<const ImgJob*>(d + o_ij);
     const QImageRef* d_refs = reinterpret_cast<const QImageRef*>(d + o_refs);
     const PairBlock* d_blk = reinterpret_cast<const PairBlock*>(d + o_blk);
-    UnionJob* d_uj = reinterpret_cast<UnionJob*>(d + o_uj);
-    const PairBlock* d_wb = reinterpret_cast<const PairBlock*>(d + o_wb);
-    const PairBlock* d_pb = reinterpret_cast<const PairBlock*>(d + o_pb);
-    int32_t* d_word = reinterpret_cast<int32_t*>(d + o_word);
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
@@ -1001,11 +932,6 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int collab_gx = (max_cap_collab + 63) / 64;  // K4' blocks per job (pf_jobs.hip kCollabCands)
     if (!jix_collab.empty())
         HIPCHK(c, W.d_parts.reserve(jix_collab.size() * (size_t)std::max(collab_gx, 1) * (size_t)ktop * 8));
-    if (!ujobs.empty()) {  // K1u's results per pair index (E: every output slot of the chunk)
-        HIPCHK(c, W.d_upool.reserve(upool));
-        HIPCHK(c, W.d_hb.reserve(nE * kHitCap * 4));
-        HIPCHK(c, W.d_hc.reserve(nE * 8));
-    }
     hl.lap(kHpPlan);  // workspaces
     if (!jix_clubs.empty()) {
         const int64_t want = (int64_t)jix_clubs.size();
@@ -1018,22 +944,18 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     // ---- the stages, in stream order; the gathers and dispatch orders run on the aux stream and
     // join before the pair kernel, beside the images
-    HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, unions, fail word) is up
+    HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, fail word) is up
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
                             d_ncand, J.aux));
     for (int k = 0, o = 0; k < 3; o += nb_c[k++])  // each launch's dispatch order (relative to its blocks)
         HIPCHK(c, launch_order_pairs(d_blk + o, nb_c[k], W.d_slots.as<int32_t>(), hc.n, d_ord + o, J.aux));
-    if (!ujobs.empty())
-        HIPCHK(c, launch_order_pairs(d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), hc.n, d_word, J.aux));
     HIPCHK(c, hipEventRecord(J.ev_join, J.aux));
     if (!resident)
         HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds,
                                  W.d_img.as<uint8_t>(), W.d_scr.as<uint32_t>(), d_fail, s));
-    if (!ujobs.empty())
-        HIPCHK(c, launch_unions(c->ds, J.js, d_uj, (int)ujobs.size(), max_ulds, W.d_upool.as<uint8_t>(), d_fail, s));
     HIPCHK(c, hipStreamWaitEvent(s, J.ev_join, 0));
-    const bool any_pairs = !blocks.empty() || !pblocks.empty();
+    const bool any_pairs = !blocks.empty();
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && any_pairs) {
         if (J.stat_used == J.stat_ev.size()) {
@@ -1047,36 +969,23 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         ++J.stat_used;
         HIPCHK(c, hipEventRecord(pe0, s));
     }
-    if (!ujobs.empty()) {  // the pair-scoring stage (timed): K1u walks, K1' pairs, K1' pre-walked pairs
-        HIPCHK(c, launch_union_walk(c->ds, W.d_upool.as<uint8_t>(), d_uj, max_wlds, d_wb, (int)wblocks.size(), d_word,
-                                    W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(), s));
-    }
-    for (int k = 0, o = 0; k < 3; o += nb_c[k++]) {
+    for (int k = 0, o = 0; k < 3; o += nb_c[k++]) {  // the pair-scoring stage (timed)
         HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, lds_c[k], k == 2, d_blk + o, nb_c[k], d_ord + o,
                                W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
         J.n_dispatch += nb_c[k] > 0;
     }
-    J.n_dispatch += !pblocks.empty();
-    HIPCHK(c, launch_pairs_prewalked(c->ds, ipl, d_refs, max_lds, d_pb, (int)pblocks.size(),
-                                     W.d_slots.as<int32_t>(), W.d_hb.as<uint32_t>(), W.d_hc.as<uint2>(),
-                                     W.d_fl.as<float>(), s));
     if (pe1) {
         HIPCHK(c, hipEventRecord(pe1, s));
         ++J.st_launches;
     }
     if (J.stats_count && any_pairs) {
         unsigned long long* acc = J.d_stats.as<unsigned long long>();
-        const uint2* hcv = W.d_hc.as<uint2>();
-        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), acc, 0, hcv, d_uj, s));
-        HIPCHK(c, launch_pair_stats(c->ds, d_pb, (int)pblocks.size(), W.d_slots.as<int32_t>(), acc, 1, hcv, d_uj, s));
-        HIPCHK(c, launch_pair_stats(c->ds, d_wb, (int)wblocks.size(), W.d_slots.as<int32_t>(), acc, 2, hcv, d_uj, s));
-        for (const PairBlock& wb : wblocks) J.st_img_bytes += (int64_t)8 << ujobs[wb.qimg].lg;  // the staged union table
-        for (const auto* bl : {&blocks, &pblocks})
-            for (const PairBlock& pb : *bl) {  // the staged image per pair block (QConst + tables)
-                const QImageRef& r = refs[pb.qimg];
-                const int32_t idx = img_idx[pb.qimg];
-                J.st_img_bytes += (int64_t)r.vals_off + ntok_of(idx) * (int64_t)sizeof(QVal);
-            }
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), acc, s));
+        for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
+            const QImageRef& r = refs[pb.qimg];
+            const int32_t idx = img_idx[pb.qimg];
+            J.st_img_bytes += (int64_t)r.vals_off + ntok_of(idx) * (int64_t)sizeof(QVal);
+        }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),

@@ -15,21 +15,6 @@ struct PairBlock {
     int32_t qimg, begin, count, out;
 };
 
-// One group of a collaborative job's friends whose pairs with a candidate span share one record
-// walk (recommender_graph.cpp:167-180; K6u union_kernel builds the table, K1u union_walk_kernel
-// walks): the union key table maps each key of the friends' records (club / friend words, tagged
-// token keys) to the mask of friends g < n holding it.  Friend g's pair (g, candidate i of a walk
-// block) has the pair index (= its K1' output slot) block.out + g * ostride + i.
-constexpr int kUnionMax = 8;                 // friends per group (mask bits)
-constexpr int kUnionKeys = 1536;             // record words of a group (table load <= 0.375)
-struct UnionJob {
-    int32_t n, lg, dlg;                      // friends; table / de-duplication set log2
-    uint32_t hmul;                           // cuckoo multiplier (written by K6u)
-    uint32_t tab_off;                        // byte offset of the table (2^lg {key, mask}) in the union pool
-    int32_t ostride, words, pad;             // pair-index stride between friends; record words
-    int32_t idx[kUnionMax];                  // the friends' profile idx
-};
-static_assert(sizeof(UnionJob) == 64, "UnionJob is four 16-B loads");
 
 // lds: dynamic LDS bytes per block = max over the batch of
 //   sizeof(QConst) + staged keys/vals + n_hits_max * threads + 2048
@@ -55,15 +40,5 @@ hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int
 hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
                         bool gtab, const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
                         float* out, hipStream_t s);
-// K1u: walk blocks (PairBlock layout, qimg = the union job) write every group pair's walk results:
-// hc[P] = {clubs | friends << 16 counts, token hits (kHitCap + 1 = overflowed)}, hb[P * kHitCap ..]
-// the hit record words in record order
-hipError_t launch_union_walk(const DevStore& st, const uint8_t* upool, const UnionJob* ujobs, uint32_t max_lds,
-                             const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
-                             uint32_t* hb, uint2* hc, hipStream_t s);
-// K1' over pre-walked pairs (their walk results from K1u instead of a record walk)
-hipError_t launch_pairs_prewalked(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
-                                  const PairBlock* blocks, int nblocks, const int32_t* slots, const uint32_t* hb,
-                                  const uint2* hc, float* out, hipStream_t s);
 
 }  // namespace pf

@@ -483,18 +483,16 @@ __device__ __forceinline__ double item_term(const QConst& q, const uint4& it, do
 
 __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& st, const RowRec& rec, uint64_t ro,
                                                uint32_t len, const uint4& h0, const uint4& h1, const uint4& h2,
-                                               uint32_t cnt, uint32_t nh, bool active, uint64_t* tep,
-                                               const uint32_t* hin = nullptr) {
+                                               uint32_t cnt, uint32_t nh, bool active, uint64_t* tep) {
     const QConst& q = *v.q;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
     const bool overflow = nh > kHitCap;
     uint32_t* hl = reinterpret_cast<uint32_t*>(v.hits);
     const uint32_t nhl = (active && !overflow) ? nh : 0u;
-    // the hit words: the lane's LDS hit list (its own walk), or hin (registers: K1u's walk)
+    // the hit words of the lane's LDS hit list (its own walk)
     uint32_t hw[kHitCap];
 #pragma unroll
-    for (int i = 0; i < (int)kHitCap; ++i)
-        hw[i] = (uint32_t)i < nhl ? (hin ? hin[i] : hl[i * kPairThreads + threadIdx.x]) : 0u;
+    for (int i = 0; i < (int)kHitCap; ++i) hw[i] = (uint32_t)i < nhl ? hl[i * kPairThreads + threadIdx.x] : 0u;
     auto colw = [](uint32_t w) { return (w >> kTidBits) & 63u; };
     uint32_t ncol = 0;
 #pragma unroll
@@ -530,10 +528,6 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
 #endif
     if (total1 > kQueue) {  // (wave-uniform) the per-lane epilogue, hit lists intact
         if (!active) return 0.0f;
-        if (hin)  // K1u's hit words: into the lane's list, where fas_epilogue reads them
-#pragma unroll
-            for (int i = 0; i < (int)kHitCap; ++i)
-                if ((uint32_t)i < nhl) hl[i * kPairThreads + threadIdx.x] = hw[i];
         return fas_epilogue<true, true>(v, rec, h0, h1, h2, cnt, threadIdx.x, 1u, [nh](uint32_t) { return nh; }, tep);
     }
     auto item = [&](uint32_t k) {  // 16-B entry k of the wave's strip (rows of 64 words)
@@ -745,39 +739,6 @@ __device__ __forceinline__ float fas_slot(const DevStore& st, const QView& v, co
         const uint32_t nh = W.nh;
         return fas_epilogue<false>(v, rec, h0, h1, h2, W.cnt, threadIdx.x, 1u, [&](uint32_t) { return nh; });
     }
-}
-
-// FAS of pair P = (staged image, slot p) whose record walk K1u already did (packed): its set
-// counts and hit words come from hc[P] / hb[P * kHitCap ..] (64 B, four 16-B loads in flight),
-// and only the epilogue runs here.  An overflowed list (> kHitCap hits) takes the epilogue's
-// record re-walk against the staged image, as after a walk of its own.
-__device__ __forceinline__ float fas_slot_pre(const DevStore& st, const QView& v, const PairHdr& H, bool active,
-                                              uint64_t P, const uint32_t* __restrict__ hb, const uint2* __restrict__ hc,
-                                              uint64_t* twalk = nullptr) {
-    const uint4 h0 = H.h0, h1 = H.h1, h2 = H.h2;
-    const uint64_t ro = H.ro;
-    const uint2 wr = active ? hc[P] : make_uint2(0u, 0u);
-    const uint32_t nh = wr.y > kHitCap ? kHitCap + 1 : wr.y;
-    uint32_t hw[kHitCap];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(hb + P * kHitCap);
-        uint4 r[kHitCap / 4];
-#pragma unroll
-        for (int k = 0; k < (int)kHitCap / 4; ++k)
-            r[k] = (active && nh <= kHitCap && (uint32_t)(4 * k) < nh) ? src[k] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < (int)kHitCap / 4; ++k) {
-            hw[4 * k] = r[k].x;
-            hw[4 * k + 1] = r[k].y;
-            hw[4 * k + 2] = r[k].z;
-            hw[4 * k + 3] = r[k].w;
-        }
-    }
-    if (twalk) twalk[0] = clock64();
-    const uint32_t len = active ? record_words(h2, true) : 0u;
-    const RowRec rec{reinterpret_cast<const uint32_t*>(st.rows + ro),
-                     reinterpret_cast<const double*>(st.rows + ro + ((len + 3) >> 2))};
-    return pair_epilogue(v, st, rec, ro, len, h0, h1, h2, wr.x, nh, active, twalk ? twalk + 1 : nullptr, hw);
 }
 
 // ---------------------------------------------------------------- LDS staging
@@ -1124,7 +1085,8 @@ constexpr uint32_t kLdsMisc = kLdsExb + 4 * (kBlockCands / 32);           // u32
 constexpr uint32_t kLdsCols = kLdsMisc + 64;                              // QCol [kPostMaxCols]
 constexpr uint32_t kLdsFtab = kLdsCols + 16 * kPostMaxCols;               // f64 [7 + 48 + 1] F by used
 constexpr uint32_t kLdsSeg = kLdsFtab + 8 * (kNumFixed + kPostMaxCols + 1);  // u32 [kRoundToks] token segments
-constexpr uint32_t kPostFixedLds = (kLdsSeg + 4 * kRoundToks + 15) & ~15u;
+constexpr uint32_t kLdsCidx = kLdsSeg + 4 * kRoundToks;                   // u8 [kPostMaxCols] column -> active index
+constexpr uint32_t kPostFixedLds = (kLdsCidx + kPostMaxCols + 15) & ~15u;
 static_assert(kBlockCands == 2 * kPostThreads, "two candidates per thread");
 static_assert(kRoundCap < 65536 && kBlockCands <= kRoundCap, "u16 slots; a one-token round fits");
 static_assert(kPostWaves * kMaxTopK * 8 + 16 + 4 * kMaxTopK <= 8 * kRoundCap, "scan_tail scratch in the slots");
@@ -1297,10 +1259,12 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint2* rng = reinterpret_cast<uint2*>(pl + nl);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + nl);
     uint8_t* colof = reinterpret_cast<uint8_t*>(gpre + H.n_tok + 1);  // token -> active column index
+    uint8_t* cidx = reinterpret_cast<uint8_t*>(base + kLdsCidx);        // column -> active column index
     stage(smem, img, sizeof(QConst));
     for (int j = tid; j < H.n_act; j += kPostThreads) {
         const QCol c = cols[j];
         scol[j] = c;
+        cidx[c.t] = (uint8_t)j;
         for (int x = c.j0; x < c.j1; ++x) colof[x] = (uint8_t)j;
     }
     for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kPostThreads)
@@ -1539,16 +1503,18 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 wave_sync();
                 K5T(9);
             }
-            // e. the owners add the round's finished common columns in ascending order
+            // e. the owners add the round's common columns in ascending order (the candidate's
+            // columns among the round's: ~3 per round instead of every round column)
+            uint64_t rtm = 0;  // the round's columns, by column number
+            for (int c = R.ca; c < R.ce; ++c) rtm |= 1ull << scol[c].t;
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) {
                 const int p = kk * kPostThreads + tid;
                 const uint64_t m = F > 0 ? mask[p] : 0ull;
                 const uint32_t hb0 = F > 0 ? hbase[p] : 0u;
-                for (int c = R.ca; c < R.ce; ++c) {
-                    const QCol col = scol[c];
-                    const int t = col.t;
-                    if (!((pend[kk] >> t) & 1ull)) continue;
+                for (uint64_t pr = pend[kk] & rtm; pr; pr &= pr - 1) {
+                    const int t = __ffsll((unsigned long long)pr) - 1;
+                    const QCol col = scol[cidx[t]];
                     const uint32_t lo = (uint32_t)(max(col.j0, ja) - ja), hi = (uint32_t)(min(col.j1, jb) - ja);
                     const uint64_t h = m & (low_bits(hi) & ~low_bits(lo));
                     const uint32_t r0 = hb0 + (uint32_t)__popcll(m & low_bits(lo));
@@ -1670,16 +1636,12 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
 }
 
 // ---------------------------------------------------------------- K1': pairs
-// PRE (packed, LDS-staged images): the blocks' pairs were walked by K1u; their walk results are
-// read from hb / hc (pair index = the output slot) instead of walking the records here.
-template <bool PACKED, bool GTAB, bool PRE = false>
+template <bool PACKED, bool GTAB>
 __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                         const QImageRef* __restrict__ refs,
                                                         const PairBlock* __restrict__ blocks,
                                                         const int32_t* __restrict__ order,
-                                                        const int32_t* __restrict__ slots, float* __restrict__ out,
-                                                        const uint32_t* __restrict__ hb = nullptr,
-                                                        const uint2* __restrict__ hc = nullptr) {
+                                                        const int32_t* __restrict__ slots, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef PF_K5_TIMERS
     const uint64_t t0 = clock64();
@@ -1701,9 +1663,7 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
 #ifdef PF_K5_TIMERS
     const uint64_t t1 = clock64();
 #endif
-    float f;
-    if constexpr (PRE) f = fas_slot_pre(st, v, H, active, (uint64_t)b.out + (uint64_t)i, hb, hc, twp);
-    else f = fas_slot<PACKED>(st, v, H, active, twp);
+    const float f = fas_slot<PACKED>(st, v, H, active, twp);
     if (active) out[b.out + i] = f;
 #ifdef PF_K5_TIMERS
     const uint64_t t3 = clock64();
@@ -1730,122 +1690,6 @@ __global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st,
         atomicAdd(&g_k1t[7], 1ull);
     }
 #endif
-}
-
-// ---------------------------------------------------------------- K1u: union walk
-// A collaborative job's friends g < n of one group score the same candidate span
-// (recommender_graph.cpp:167-180).  K6u merged their records' keys into one table, key -> mask of
-// the friends holding it, so a lane walks its candidate's record ONCE for the whole group (the pair
-// walk walked it once per friend) and writes, for every friend g, what walk_row produces for the
-// pair (g, candidate): the clubs / friends intersection counts (each candidate word counted once
-// per friend holding it, duplicates on the candidate's side as the reference counts them,
-// recommender.cpp:119-128) and the token-hit record words in record order (kHitCap kept; more
-// reads as overflowed, and K1' re-walks that pair against the friend's own image).
-__device__ __forceinline__ uint32_t union_mask(const uint2* tab, int lg, uint32_t hmul, uint32_t key) {
-    const uint32_t x = cuckoo_x(key, hmul);
-    const uint2 e1 = tab[cuckoo_h1(x, lg)];
-    const uint2 e2 = tab[__builtin_amdgcn_ubfe(x, 32u - 2u * (uint32_t)lg, (uint32_t)lg)];
-    return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
-}
-
-struct UnionWalk {
-    uint32_t cnt[kUnionMax];  // per friend: clubs intersections (low 16 bits) + friends << 16
-    uint64_t nh;              // per friend: token hits, 8 bits each (saturating at kHitCap + 1)
-};
-
-// words j0 .. j0 + 3 of the lane's record; SETS: the step may hold club / friend words
-template <bool SETS>
-__device__ __forceinline__ void union_step(UnionWalk& W, const uint4& cw, uint32_t j0, uint32_t nc, uint32_t nset,
-                                           const uint2* tab, int lg, uint32_t hmul, uint32_t* __restrict__ hb,
-                                           uint64_t pbase, uint32_t ostride) {
-    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
-    uint32_t m[4];
-    bool tok[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        tok[i] = !SETS || j0 + i >= nset;
-        m[i] = union_mask(tab, lg, hmul, tok[i] ? (kTagTok | (w[i] & 0xFFFFFFu)) : w[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (SETS && !tok[i] && m[i]) {
-            const uint32_t inc = j0 + i < nc ? 1u : 0x10000u;
-#pragma unroll
-            for (int g = 0; g < kUnionMax; ++g) W.cnt[g] += ((m[i] >> g) & 1u) ? inc : 0u;
-        }
-        uint32_t mm = tok[i] ? m[i] : 0u;
-        while (mm) {  // the friends holding this token: its word goes to each one's hit list
-            const uint32_t g = (uint32_t)__builtin_ctz(mm);
-            mm &= mm - 1u;
-            const uint32_t c = (uint32_t)(W.nh >> (8u * g)) & 0xFFu;
-            if (c < kHitCap) hb[(pbase + (uint64_t)g * ostride) * kHitCap + c] = w[i];
-            if (c <= kHitCap) W.nh += 1ull << (8u * g);
-        }
-    }
-}
-
-__global__ __launch_bounds__(kPairThreads) void union_walk_kernel(DevStore st, const uint8_t* __restrict__ upool,
-                                                                const UnionJob* __restrict__ ujobs,
-                                                                const PairBlock* __restrict__ blocks,
-                                                                const int32_t* __restrict__ order,
-                                                                const int32_t* __restrict__ slots,
-                                                                uint32_t* __restrict__ hb, uint2* __restrict__ hc) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const PairBlock b = blocks[order ? order[blockIdx.x] : (int)blockIdx.x];
-    const int i = (int)threadIdx.x;
-    const int p = i < b.count ? slots[b.begin + i] : -1;
-    const bool active = p >= 0;
-    if (!__syncthreads_or(active)) return;
-    const UnionJob U = ujobs[b.qimg];
-    stage4(smem, upool + U.tab_off, 8u << U.lg);
-    uint4 h2 = make_uint4(0, 0, 0, 0);
-    uint64_t ro = 0;
-    if (active) {
-        h2 = st.hdr2[p];
-        ro = st.row_off[p];
-    }
-    __syncthreads();
-    const uint2* tab = reinterpret_cast<const uint2*>(smem);
-    const int lg = U.lg;
-    const uint32_t hmul = U.hmul, ostride = (uint32_t)U.ostride;
-    const uint32_t nc = h2.y, nset = active ? h2.y + h2.z : 0u;
-    const uint32_t len = active ? record_words(h2, true) : 0u;
-    const uint64_t pbase = (uint64_t)b.out + (uint64_t)i;
-    UnionWalk W;
-#pragma unroll
-    for (int g = 0; g < kUnionMax; ++g) W.cnt[g] = 0u;
-    W.nh = 0ull;
-    // walk_row's loop: groups of 4 steps, the next group's loads in flight; a lane past its record
-    // reads the padding line (kPadWord and its token key never match)
-    const uint4* base = st.rows + ro;
-    const uint4* pad = st.row_pad;
-    const uint32_t steps = (len + 3) >> 2;
-    const uint32_t smax = wave_max_u32(steps);
-    const uint32_t sset = wave_max_u32((nset + 3) >> 2);
-    auto ld = [&](uint32_t s) { return *(s < steps ? base + s : pad); };
-    uint4 c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
-    uint32_t s = 0;
-    for (; s < sset; s += 4) {
-        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
-        union_step<true>(W, c0, 4 * s, nc, nset, tab, lg, hmul, hb, pbase, ostride);
-        union_step<true>(W, c1, 4 * s + 4, nc, nset, tab, lg, hmul, hb, pbase, ostride);
-        union_step<true>(W, c2, 4 * s + 8, nc, nset, tab, lg, hmul, hb, pbase, ostride);
-        union_step<true>(W, c3, 4 * s + 12, nc, nset, tab, lg, hmul, hb, pbase, ostride);
-        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-    }
-    for (; s < smax; s += 4) {
-        const uint4 n0 = ld(s + 4), n1 = ld(s + 5), n2 = ld(s + 6), n3 = ld(s + 7);
-        union_step<false>(W, c0, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
-        union_step<false>(W, c1, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
-        union_step<false>(W, c2, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
-        union_step<false>(W, c3, 0, 0, 0, tab, lg, hmul, hb, pbase, ostride);
-        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-    }
-    if (active) {
-#pragma unroll
-        for (int g = 0; g < kUnionMax; ++g)
-            if (g < U.n) hc[pbase + (uint64_t)g * ostride] = make_uint2(W.cnt[g], (uint32_t)(W.nh >> (8 * g)) & 0xFFu);
-    }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1964,41 +1808,5 @@ hipError_t launch_pairs(const DevStore& st, const uint8_t* pool, const QImageRef
 #endif
     return hipGetLastError();
 }
-
-hipError_t launch_union_walk(const DevStore& st, const uint8_t* upool, const UnionJob* ujobs, uint32_t max_lds,
-                             const PairBlock* blocks, int nblocks, const int32_t* order, const int32_t* slots,
-                             uint32_t* hb, uint2* hc, hipStream_t s) {
-    if (nblocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(union_walk_kernel, dim3(nblocks), dim3(kPairThreads), max_lds, s, st, upool, ujobs, blocks, order,
-                       slots, hb, hc);
-    return hipGetLastError();
-}
-
-hipError_t launch_pairs_prewalked(const DevStore& st, const uint8_t* pool, const QImageRef* refs_dev, uint32_t max_lds,
-                                  const PairBlock* blocks, int nblocks, const int32_t* slots, const uint32_t* hb,
-                                  const uint2* hc, float* out, hipStream_t s) {
-    if (nblocks <= 0) return hipSuccess;
-    if (!st.packed) return hipErrorInvalidValue;  // K1u walks packed records only
-    hipLaunchKernelGGL((fas_pairs_kernel<true, false, true>), dim3(nblocks), dim3(kPairThreads), max_lds, s, st, pool,
-                       refs_dev, blocks, (const int32_t*)nullptr, slots, out, hb, hc);
-#ifdef PF_K5_TIMERS
-    {
-        static int calls = 0;
-        unsigned long long t[12];
-        hipStreamSynchronize(s);
-        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k1t), sizeof(t));
-        if (++calls % 10 == 0 && t[7])
-            fprintf(stderr,
-                    "k1pt-pre per wave (clock64): staging=%.0f load=%.0f epilogue=%.0f (dense=%.0f assembly=%.0f "
-                    "overflow=%.0f fas=%.0f) total=%.0f waves=%llu blocks=%d\n",
-                    (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[4] / t[7],
-                    (double)t[5] / t[7], (double)t[6] / t[7], (double)t[8] / t[7], (double)t[3] / t[7], t[7], nblocks);
-        const unsigned long long z[12] = {0};
-        hipMemcpyToSymbol(HIP_SYMBOL(g_k1t), z, sizeof(z));
-    }
-#endif
-    return hipGetLastError();
-}
-
 
 }  // namespace pf

@@ -1,7 +1,7 @@
 """Child process of test_gpu_parity.test_kernel_variants: the engine reads PF_DEBUG's
-stage_limit, tile_steps, union and resident_images once per process/context, so each forced kernel variant
-(global-memory query tables, records split over lanes, collaborative pairs through K1u groups)
-runs in its own process.  Exits non-zero on any
+stage_limit, tile_steps, scan, k5_block and resident_images once per process/context, so each forced
+kernel variant (global-memory query tables, records split over lanes, postings block sizes, per-call
+query images) runs in its own process.  Exits non-zero on any
 mismatch."""
 import sys
 
@@ -29,7 +29,7 @@ def main():
     if np.count_nonzero(eng.fas_pairs(a, b).view(np.uint32) != orc.fas_pairs(a, b).view(np.uint32)):
         print("pair mismatch", file=sys.stderr)
         return 1
-    # the collaborative recommender (union=1: friend groups walk each candidate record once, K1u)
+    # the collaborative recommender (per-call images: resident_images=0)
     qc = [3, 8, 1000, 15000, 19999]
     for u, g, r in zip(qc, eng.recommend_collaborative(qc, 10, 1000), orc.collab(qc, 10, 1000)):
         if list(g[0]) != list(r[0]) or not np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)):

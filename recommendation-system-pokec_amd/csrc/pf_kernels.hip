@@ -1308,10 +1308,15 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         __syncthreads();
         K5T(1);
         if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
-        // exclusion list (sorted idx of adj[q] + {q}): whole list when short, else bisect
-        {
+        // exclusion list (sorted idx of adj[q] + {q}): whole list when short (one load per thread,
+        // no barrier of its own), else bisect and walk until past the block
+        if (H.n_excl <= kPostThreads) {
+            const uint32_t e = tid < H.n_excl ? excl[tid] : ~0u;
+            const uint32_t p = e - c0;
+            if (p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
+        } else {
             uint32_t lo = 0, hi = (uint32_t)H.n_excl;
-            if (hi > kPostThreads) {
+            {
                 while (lo < hi) {  // first entry >= c0
                     const uint32_t mid = (lo + hi) >> 1;
                     if (excl[mid] < c0) lo = mid + 1; else hi = mid;

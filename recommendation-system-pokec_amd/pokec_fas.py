@@ -517,14 +517,12 @@ def rec_tests_summary(hits, club):
     if n:
         for j in range(3):
             out[j] = float(int(np.sum(hits[:, j], dtype=np.int64))) / float(n)
-    prec = rec = 0.0
-    users = 0
-    for p, r in club:
-        if p == p:  # not NaN: the user has clubs
-            prec += float(p)
-            rec += float(r)
-            users += 1
+    club = np.asarray(club, np.float64).reshape(-1, 2)
+    has = ~np.isnan(club[:, 0])  # the users with clubs
+    users = int(np.count_nonzero(has))
     if users:
-        out[3] = prec / users
-        out[4] = rec / users
+        # np.add.accumulate adds left to right (the reference's sequential double sum in plan
+        # order; np.sum's pairwise summation would round differently)
+        out[3] = float(np.add.accumulate(club[has, 0])[-1]) / users
+        out[4] = float(np.add.accumulate(club[has, 1])[-1]) / users
     return out

@@ -8,7 +8,8 @@
 #   cfgN         bench.py --workload cfgN               -> cfgN.json
 #   quick        cfg 2, 100 steps, no CPU baseline / PMC -> quick.json
 #   quick4       cfg 4, 3 steps, no CPU baseline / PMC   -> quick4.json
-#   k5t          profiling build (make K5T=1 into exp/k5t) per-phase K5 clocks -> k5t.err
+#   cfg5c1       cfg 5 at one context with the host stage clocks (PF_DEBUG host_prof=1) -> cfg5c1.err
+#   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> exp/v/k5t) per-phase K5 clocks -> k5t.err
 #   pmc:NAME:C1,C2..  one rocprofv3 --pmc pass over a 20-step cfg-2 run -> pmc_NAME/
 set -o pipefail
 TAG=$1
@@ -33,8 +34,10 @@ for S in "$@"; do
         timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 $Q > $O/quick.json 2> $O/quick.err || exit 5 ;;
     quick4)
         timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
+    cfg5c1)
+        timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5c1.json 2> $O/cfg5c1.err || exit 4 ;;
     k5t)
-        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/k5t/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/k5t.json 2> $O/k5t.err || exit 7 ;;
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/k5t/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/k5t.json 2> $O/k5t.err || exit 7 ;;
     pmc:*)
         R=${S#pmc:}; N=${R%%:*}; C=${R#*:}
         timeout -s KILL 120 rocprofv3 --pmc ${C//,/ } -d $O/pmc_$N -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmc_$N.json 2> $O/pmc_$N.err || exit 8 ;;

@@ -949,6 +949,23 @@ def main():
     phys_per_launch = (float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in timed_steps]))
                        if timed_steps else None)
     avg_launch_ms = scan_ms / launches if launches else None
+    # N > 1: every rank's scan time and shard (pf_set_shard's static posting-weight split), so the
+    # line shows the per-shard skew behind the max-over-ranks step time
+    per_rank = None
+    if dist:
+        ls = eng.layout()
+        t = torch.tensor([[avg_launch_ms or 0.0, float(ls.shard_cands), float(ls.shard_entries),
+                           phys_per_launch or 0.0]], dtype=torch.float64, device="cuda")
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rows = [p.cpu().numpy()[0] for p in parts]
+        ms_r = [float(x[0]) for x in rows]
+        cand_r = [float(x[1]) for x in rows]
+        per_rank = {"ranks": [{"rank": r, "avg_launch_ms": ms_r[r], "shard_cands": int(cand_r[r]),
+                               "shard_entries": int(rows[r][2]), "bytes_per_launch": float(rows[r][3])}
+                              for r in range(world)],
+                    "launch_ms_max_over_mean": max(ms_r) / (sum(ms_r) / world) if sum(ms_r) > 0 else None,
+                    "shard_cands_max_over_mean": max(cand_r) / (sum(cand_r) / world) if sum(cand_r) > 0 else None}
     # SURVEY 8(d) D3 record bytes of this rank's shard x queries per launch (the metric's definition)
     shard_frac = 1.0 / world
     alg_bytes = lay.alg_bytes * shard_frac * Q
@@ -1005,6 +1022,8 @@ def main():
     }
     if n1 is not None:
         rec["n1_same_workload"] = n1
+    if per_rank is not None:
+        rec["per_rank"] = per_rank
     if rank == 0 and world == 1 and base is not None:
         rec["cpu_baseline"] = base
         rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None

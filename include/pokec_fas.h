@@ -251,6 +251,8 @@ typedef struct pf_layout_stats {
     int64_t post_bytes;       /* postings store: entries + norms + cells + headers (0 if absent) */
     int32_t scan_kernel;      /* kernel the next all-candidates scan uses: PF_SCAN_STREAM / PF_SCAN_POSTINGS */
     int32_t pad;
+    int64_t shard_cands;      /* candidates in this context's shard (pf_set_shard) for that kernel */
+    int64_t shard_entries;    /* their postings entries (tokens, clubs, friends; 0 without postings) */
 } pf_layout_stats;
 int pf_layout(const pf_ctx* ctx, pf_layout_stats* out);
 

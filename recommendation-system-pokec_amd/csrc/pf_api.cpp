@@ -977,6 +977,23 @@ int pf_layout(const pf_ctx* c, pf_layout_stats* o) {
     o->post_bytes = c->post_bytes;
     o->scan_kernel = c->use_post() ? PF_SCAN_POSTINGS : PF_SCAN_STREAM;
     o->pad = 0;
+    o->shard_cands = 0;
+    o->shard_entries = 0;
+    if (c->use_post()) {
+        const int64_t bs = c->ps.bsize, n = c->hc.n;
+        const int64_t i0 = std::min<int64_t>(n, (int64_t)c->wb_begin * bs), i1 = std::min<int64_t>(n, (int64_t)c->wb_end * bs);
+        const auto& hc = c->hc;
+        o->shard_cands = i1 - i0;
+        if (i1 > i0)
+            o->shard_entries = (hc.tok_off[(size_t)i1 * hc.T] - hc.tok_off[(size_t)i0 * hc.T]) +
+                               (hc.club_off[i1] - hc.club_off[i0]) + (hc.friend_off[i1] - hc.friend_off[i0]);
+    } else {
+        for (int32_t t = c->tile_begin; t < c->tile_end; ++t) {
+            const int64_t s0 = c->hs.tile_slot0[t];
+            const int64_t s1 = t + 1 < (int32_t)c->hs.tile_slot0.size() ? (int64_t)c->hs.tile_slot0[t + 1] : (int64_t)c->hc.n;
+            o->shard_cands += s1 - s0;
+        }
+    }
     return PF_OK;
 }
 

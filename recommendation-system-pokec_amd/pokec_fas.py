@@ -42,7 +42,8 @@ PF_LOAD_REFERENCE_CAP = 100000
 class PfLayoutStats(ctypes.Structure):
     _fields_ = [("n_slots", ctypes.c_int64), ("stream_bytes", ctypes.c_int64), ("header_bytes", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64), ("packed_tokens", ctypes.c_int32), ("n_tiles", ctypes.c_int32),
-                ("post_bytes", ctypes.c_int64), ("scan_kernel", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("post_bytes", ctypes.c_int64), ("scan_kernel", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("shard_cands", ctypes.c_int64), ("shard_entries", ctypes.c_int64)]
 
 
 class PfJobsStats(ctypes.Structure):

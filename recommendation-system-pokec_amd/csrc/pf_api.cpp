@@ -253,7 +253,13 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 // unclaimed one), for one-query launches only.  r2fb A/B: 205.3 / 205.6 us vs 206.9 / 206.9 us
 // static per cfg-2 launch; batches (one block per workgroup in L2-sharing order) stay static
 // (cfg 4 9.83e9 dynamic vs 9.88e9 static).
-uint32_t post_mode(int nq) { return nq == 1 ? 1u : 0u; }
+// K5 launch mode: bit 0 = dynamic block hand-out (one query); bit 1 = transposed grid (batches:
+// the resident workgroups are many queries on the same candidate blocks, sharing their lists in
+// L2; PF_DEBUG k5_query_major=1 keeps the query-major grid)
+uint32_t post_mode(int nq) {
+    static const bool qmajor = pf::debug_long("k5_query_major", 0) != 0;
+    return nq == 1 ? 1u : (qmajor ? 0u : 2u);
+}
 
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run

@@ -831,9 +831,10 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
 // Block-level end of a scan: merge the 4 wave lists, publish the block's k-list and, in
 // the last block of the query, merge every block's list into out[row] (no second launch).
 // sc: LDS >= (waves) * k keys; misc: LDS >= 16 + 4 * kMaxTopK bytes (both idle by now).
+// qy = the query (row of sync / parts / out_rows), bx = this workgroup's index among the query's nbx
 __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
                                           uint64_t* __restrict__ parts, uint64_t* __restrict__ out,
-                                          const int32_t* __restrict__ out_rows) {
+                                          const int32_t* __restrict__ out_rows, int qy, int bx, int nbx) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // block merge: the 4 wave lists are packed densely (k keys each) and wave 0 takes
     // them 64 at a time, so 4*k <= 64 keys cost a single push
@@ -844,8 +845,8 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
     // with write-through (sc1) stores, drains them and takes a ticket; the last block of
     // the query merges, reading the lists with sc1 loads (cdna_hip_programming.md
     // Guideline 16, R1: no L2 write-back or acquire fence needed).
-    ScanSync* sy = sync + blockIdx.y;
-    uint64_t* qparts = parts + (size_t)blockIdx.y * gridDim.x * k;
+    ScanSync* sy = sync + qy;
+    uint64_t* qparts = parts + (size_t)qy * nbx * k;
     // tail scratch in the (now idle) hit lists: flag, threshold, block count, block ids
     int* s_flag = misc;
     int* s_cnt = s_flag + 1;
@@ -855,20 +856,20 @@ __device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, in
         uint64_t acc = ~0ull;
         const int n = (int)(blockDim.x >> 6) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        if (lane < k) st_agent(qparts + (size_t)blockIdx.x * k + lane, acc);
+        if (lane < k) st_agent(qparts + (size_t)bx * k + lane, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __atomic_signal_fence(__ATOMIC_SEQ_CST);  // program order: stores, wait, ticket (no hardware fence)
         unsigned t = 0;
         if (lane == 0) t = __hip_atomic_fetch_add(&sy->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0) {
-            *s_flag = t == gridDim.x - 1;
+            *s_flag = t == (unsigned)nbx - 1u;
             *s_cnt = 0;
         }
     }
     __syncthreads();
     if (!*s_flag) return;
-    const int nb = (int)gridDim.x;
-    const int row = out_rows ? out_rows[blockIdx.y] : (int)blockIdx.y;
+    const int nb = nbx;
+    const int row = out_rows ? out_rows[qy] : qy;
     // Pass 1: the k smallest of every block's first j keys (j * nb >= 2k).  Its k-th key T
     // bounds the final k-th key from above, and a block can hold further keys <= T only
     // if its j-th key is <= T, which at most k blocks satisfy (keys are distinct).
@@ -1037,7 +1038,7 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         topk_push(list, key, k, lane);
     }
     scan_tail(list, k, reinterpret_cast<uint64_t*>(scratch), reinterpret_cast<int*>(v.hits), sync, parts, out,
-              out_rows);
+              out_rows, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------- K5: postings scan
@@ -1234,7 +1235,14 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
                                                               const int32_t* __restrict__ out_rows, uint32_t mode) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint8_t* img = pool + img_off[blockIdx.y];
+    // mode bit 1 (batches): the grid is transposed, blockIdx.x = the query and blockIdx.y = the block
+    // group, so the workgroups resident at once are many queries on the same candidate blocks and
+    // the lists they share (popular tokens, clubs) are read from HBM once and then served by L2
+    const bool tr = (mode & 2u) != 0u;
+    const int qy = tr ? (int)blockIdx.x : (int)blockIdx.y;
+    const int bx = tr ? (int)blockIdx.y : (int)blockIdx.x;
+    const int nbx = tr ? (int)gridDim.y : (int)gridDim.x;
+    const uint8_t* img = pool + img_off[qy];
     const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
     const QTok* toks = reinterpret_cast<const QTok*>(img + H.tok_off);
     const QCol* cols = reinterpret_cast<const QCol*>(img + H.col_off);
@@ -1286,8 +1294,8 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     // Blocks: the workgroup's own first block, then either every gridDim.x-th block (static)
     // or (mode bit 0) the next unclaimed block of the query from a counter in its ScanSync, so the
     // blocks past the first resident round go to the workgroups that finish first.
-    unsigned int* next_blk = &sync[blockIdx.y].next;
-    for (int blk = blk_begin + (int)blockIdx.x; blk < blk_end;) {
+    unsigned int* next_blk = &sync[qy].next;
+    for (int blk = blk_begin + bx; blk < blk_end;) {
         const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
@@ -1579,12 +1587,12 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         K5T(12);
         if (mode & 1u) {
             // misc[0] was last read before this block's first barrier
-            if (tid == 0) misc[0] = (uint32_t)blk_begin + gridDim.x + atomicAdd(next_blk, 1u);
+            if (tid == 0) misc[0] = (uint32_t)(blk_begin + nbx) + atomicAdd(next_blk, 1u);
             __syncthreads();
             blk = (int)misc[0];
         } else {
             __syncthreads();  // the next block rewrites the exclusion bits the owners read above
-            blk += (int)gridDim.x;
+            blk += nbx;
         }
     }
 #ifdef PF_K5_TIMERS
@@ -1601,7 +1609,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     }
     // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
     uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
-    scan_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows);
+    scan_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
 }
 
 // ---------------------------------------------------------------- K2: merge
@@ -1741,7 +1749,8 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
     if (nq <= 0) return hipSuccess;
     // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
     // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
-    hipExtLaunchKernelGGL(fas_post_kernel, dim3(blocks, nq), dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
+    const dim3 grid = (mode & 2u) ? dim3(nq, blocks) : dim3(blocks, nq);
+    hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
                           pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode);
 #ifdef PF_K5_TIMERS
     {

@@ -560,7 +560,7 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
     ref = eng.recommend_interest_all(list(q), k)
     eng2 = tl.engine(c.desc_ptr())
     s = torch.cuda.Stream()
-    for world, kern in ((2, 1), (3, 1), (2, 2), (3, 2), (7, 2)):
+    for world, kern in ((2, 1), (3, 1), (8, 1), (2, 2), (3, 2), (7, 2), (8, 2)):
         eng2.set_scan_kernel(kern)
         parts = torch.empty((world, len(q), k), dtype=torch.int64, device="cuda")
         for r in range(world):
@@ -604,7 +604,8 @@ def test_full_size_kernels_agree(full):
     """BASELINE cfg 2 size (1,632,803 users): the postings scan (K5), the record-stream scan
     (K1) and the pair kernel (K1') are three independent GPU paths; on the full corpus
     their top-k ids and FAS bits agree, equal the oracle's for two queries, the top-k is
-    sorted by the reference comparator, and the 2-shard merge equals the single-shard result."""
+    sorted by the reference comparator, and the 2- and 8-shard merges (both scan kernels at 8, the
+    driver's N = 8 split) equal the single-shard result."""
     import torch
     pf = tl.product()
     c, eng, oracle = full
@@ -631,19 +632,25 @@ def test_full_size_kernels_agree(full):
         assert list(p[0]) == list(r[0]), u
         assert np.array_equal(p[1].view(np.uint32), r[1].view(np.uint32)), u
     s = torch.cuda.Stream()
-    parts = torch.empty((2, len(q), k), dtype=torch.int64, device="cuda")
-    for r in range(2):
-        eng.set_shard(r, 2)
-        eng.scan_keys_async(np.array(q, np.int32), k, parts[r].data_ptr(), s.cuda_stream)
-    out = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
-    eng.merge_keys_async(parts.data_ptr(), 2, len(q), k, out.data_ptr(), s.cuda_stream)
-    s.synchronize()
-    eng.set_shard(0, 1)
-    keys = out.cpu().numpy().view(np.uint64)
-    for i in range(len(q)):
-        uids, scores = pf.decode_keys(keys[i])
-        assert list(uids) == list(post[i][0])
-        assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32))
+    for world, kern in ((2, 2), (8, 2), (8, 1)):
+        eng.set_scan_kernel(kern)
+        parts = torch.empty((world, len(q), k), dtype=torch.int64, device="cuda")
+        cands = 0
+        for r in range(world):
+            eng.set_shard(r, world)
+            cands += eng.layout().shard_cands
+            eng.scan_keys_async(np.array(q, np.int32), k, parts[r].data_ptr(), s.cuda_stream)
+        assert cands == 1632803, (world, kern, cands)  # the shards partition the corpus
+        out = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
+        eng.merge_keys_async(parts.data_ptr(), world, len(q), k, out.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        eng.set_shard(0, 1)
+        eng.set_scan_kernel(0)
+        keys = out.cpu().numpy().view(np.uint64)
+        for i in range(len(q)):
+            uids, scores = pf.decode_keys(keys[i])
+            assert list(uids) == list(post[i][0]), (world, kern, q[i])
+            assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32)), (world, kern, q[i])
 
 
 def _adjacency(ptr):

@@ -4,6 +4,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdlib>
 #include <cstdint>
 #include <deque>
@@ -249,8 +253,82 @@ struct pf_ctx {
 
 namespace pf {
 
-// f(0 .. n-1) on up to 16 threads, `grain` items per thread at least (a thread costs tens of
-// microseconds: the single-user calls of the sequential drivers stay on the caller's thread)
+// A process-wide pool of worker threads (started on first use, never joined: they sleep on a
+// condition variable) for the engine's host loops.  Several contexts may submit at once: a call
+// posts its range, the workers and the caller take items from it through an atomic cursor, and the
+// caller returns when every item is done.  (Spawning 16 std::threads per call cost ~0.5 ms per job
+// chunk: three chunks per cfg-5 step.)
+class WorkPool {
+  public:
+    static WorkPool& get() {
+        static WorkPool* p = new WorkPool();  // leaked on purpose: workers outlive static destruction
+        return *p;
+    }
+    int workers() const { return (int)ts_.size(); }
+    // fn(i) for i in [0, n), on the caller and up to `helpers` workers
+    void run(size_t n, size_t helpers, const std::function<void(size_t)>& fn) {
+        Task t;
+        t.fn = &fn;
+        t.n = n;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            t.slots = (int)helpers;
+            q_.push_back(&t);
+        }
+        cv_.notify_all();
+        work(t);
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            auto it = std::find(q_.begin(), q_.end(), &t);
+            if (it != q_.end()) q_.erase(it);  // no further worker joins this task
+        }
+        std::unique_lock<std::mutex> g(t.m);
+        t.cv.wait(g, [&] { return t.active == 0; });
+    }
+
+  private:
+    struct Task {
+        const std::function<void(size_t)>* fn = nullptr;
+        size_t n = 0;
+        std::atomic<size_t> next{0};
+        int slots = 0;   // workers that may still join (under mu_)
+        int active = 0;  // workers inside (under m)
+        std::mutex m;
+        std::condition_variable cv;
+    };
+    static void work(Task& t) {
+        for (size_t i; (i = t.next.fetch_add(1)) < t.n;) (*t.fn)(i);
+    }
+    WorkPool() {
+        const int n = (int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()) - 1u);
+        for (int w = 0; w < n; ++w) {
+            ts_.emplace_back([this]() {
+                for (;;) {
+                    Task* t = nullptr;
+                    {
+                        std::unique_lock<std::mutex> g(mu_);
+                        cv_.wait(g, [&] { return !q_.empty(); });
+                        t = q_.front();
+                        if (--t->slots <= 0) q_.pop_front();
+                        std::lock_guard<std::mutex> g2(t->m);
+                        ++t->active;  // registered before the caller can see the queue without it
+                    }
+                    work(*t);
+                    std::lock_guard<std::mutex> g2(t->m);
+                    if (--t->active == 0) t->cv.notify_all();
+                }
+            });
+            ts_.back().detach();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Task*> q_;
+    std::vector<std::thread> ts_;
+};
+
+// f(0 .. n-1) on up to 16 threads (the caller and pool workers), `grain` items per thread at least
+// (the single-user calls of the sequential drivers stay on the caller's thread)
 template <class F>
 inline void par_jobs(size_t n, F f, size_t grain = 4) {
     const size_t th = std::min<size_t>(16, std::max<size_t>(1, std::min<size_t>(n / grain, std::thread::hardware_concurrency())));
@@ -258,12 +336,8 @@ inline void par_jobs(size_t n, F f, size_t grain = 4) {
         for (size_t i = 0; i < n; ++i) f(i);
         return;
     }
-    std::vector<std::thread> ts;
-    for (size_t w = 0; w < th; ++w)
-        ts.emplace_back([&, w]() {
-            for (size_t i = w; i < n; i += th) f(i);
-        });
-    for (auto& t : ts) t.join();
+    const std::function<void(size_t)> fn = [&](size_t i) { f(i); };
+    WorkPool::get().run(n, th - 1, fn);
 }
 
 

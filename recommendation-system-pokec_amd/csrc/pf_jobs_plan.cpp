@@ -561,10 +561,16 @@ void plan_job(pf_ctx* c, const Job& Jb, JP& p, bool raw) {
     for (int32_t x : p.F) p.unmapped |= x < 0;
     for (int32_t x : p.own) p.unmapped |= x < 0;
     const int64_t L = std::max<int32_t>(Jb.limit, 1);
-    // |row(node)| under the view: the base CSR's length unless an edit or the view covers it
-    const bool plain = c->jb.edited.empty() && !Jb.view.over && !Jb.view.own_row;
+    // |row(node)| under the view: the base CSR's length unless an edit or the view covers it.
+    // Without pf_set_adj edits or versioned edits, the view differs from the base only in the
+    // query's own replaced row (recommendation_tests.cpp:111-114): every other node reads g_len
+    // instead of a lookup in the 1.6M-row adjacency hash map
+    const bool base_ok = c->jb.edited.empty() && !Jb.view.over;
     auto rowlen = [&](int32_t node) -> int64_t {
-        if (plain && node >= 0 && node < (int32_t)c->jb.g_len.size()) return c->jb.g_len[node];
+        if (base_ok && node >= 0 && node < (int32_t)c->jb.g_len.size()) {
+            if (Jb.view.own_row && node == p.own_node) return (int64_t)Jb.view.own_row->size();
+            return c->jb.g_len[node];
+        }
         const std::vector<int32_t>* r = Jb.view.row(c->jb.g_uid[node]);
         return r ? (int64_t)r->size() : -1;
     };

@@ -1299,15 +1299,25 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
-        // 1. ranges of every list in this block; headers of the owned candidates
-        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
+        // 1. headers of the owned candidates, every list's range in this block and (short list) the
+        // exclusions: all loads issued before the first wait, one memory round trip
         uint4 ha[kCandsPerThread], hb[kCandsPerThread];
+#pragma unroll
+        for (int kk = 0; kk < kCandsPerThread; ++kk) {  // clamped (always valid) index, zeroed below
+            const uint32_t c = min(c0 + kk * kPostThreads + tid, c1);
+            ha[kk] = ps.hdr[2 * (size_t)c];
+            hb[kk] = ps.hdr[2 * (size_t)c + 1];
+        }
+        const bool short_excl = H.n_excl <= kPostThreads;
+        const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;
+        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
-            const bool a = c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B;
-            ha[kk] = a ? ps.hdr[2 * (size_t)c] : make_uint4(0, 0, 0, 0);
-            hb[kk] = a ? ps.hdr[2 * (size_t)c + 1] : make_uint4(0, 0, 0, 0);
+            if (!(c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B)) {
+                ha[kk] = make_uint4(0, 0, 0, 0);
+                hb[kk] = make_uint4(0, 0, 0, 0);
+            }
             cnt[kk * kPostThreads + tid] = 0u;
             mask[kk * kPostThreads + tid] = 0ull;
         }
@@ -1316,21 +1326,18 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         __syncthreads();
         K5T(1);
         if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
-        // exclusion list (sorted idx of adj[q] + {q}): whole list when short (one load per thread,
-        // no barrier of its own), else bisect and walk until past the block
-        if (H.n_excl <= kPostThreads) {
-            const uint32_t e = tid < H.n_excl ? excl[tid] : ~0u;
-            const uint32_t p = e - c0;
-            if (p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
+        // exclusion list (sorted idx of adj[q] + {q}): whole list when short (loaded above, no
+        // barrier of its own), else bisect and walk until past the block
+        if (short_excl) {
+            const uint32_t p = ex0 - c0;
+            if (tid < H.n_excl && p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
         } else {
             uint32_t lo = 0, hi = (uint32_t)H.n_excl;
-            {
-                while (lo < hi) {  // first entry >= c0
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (excl[mid] < c0) lo = mid + 1; else hi = mid;
-                }
-                hi = (uint32_t)H.n_excl;
+            while (lo < hi) {  // first entry >= c0
+                const uint32_t mid = (lo + hi) >> 1;
+                if (excl[mid] < c0) lo = mid + 1; else hi = mid;
             }
+            hi = (uint32_t)H.n_excl;
             for (uint32_t b = lo; b < hi; b += kPostThreads) {
                 const uint32_t x = b + tid;
                 const uint32_t e = x < hi ? excl[x] : ~0u;

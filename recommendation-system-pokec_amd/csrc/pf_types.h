@@ -191,14 +191,18 @@ struct DevStore {
 // candidates holding it, so a query reads only the lists it names instead of every record.
 // Candidates are in idx order (ascending uid, the reference's tie-break order); a workgroup
 // scores one block of kBlockCands consecutive candidates at a time.
-constexpr int kBlockCands = 512;           // candidates of a workgroup block (2 per thread)
-constexpr int kPostWaves = 4;              // waves per K5 workgroup
+#ifndef PF_K5_WAVES
+#define PF_K5_WAVES 4
+#endif
+constexpr int kPostWaves = PF_K5_WAVES;    // waves per K5 workgroup
 constexpr int kPostThreads = kPostWaves * kWave;
+constexpr int kBlockCands = 2 * kPostThreads;  // candidates of a workgroup block (2 per thread)
 constexpr int kCandsPerThread = kBlockCands / kPostThreads;
 // K5 rounds: a block's query tokens are taken in rounds of <= kRoundToks tokens (one 64-bit hit
-// mask per candidate) whose list entries in the block number <= kRoundCap (the round's hit slots)
+// mask per candidate) whose list entries in the block number <= kRoundCap (the round's hit slots,
+// 8 per thread)
 constexpr int kRoundToks = 64;
-constexpr int kRoundCap = 2048;
+constexpr int kRoundCap = 8 * kPostThreads;
 constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
 constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
 constexpr int kPostMinShift = 9;           // cells of >= 512 candidates: a block spans at most 3

@@ -8,6 +8,7 @@
 #   cfgN         bench.py --workload cfgN               -> cfgN.json
 #   quick        cfg 2, 100 steps, no CPU baseline / PMC -> quick.json
 #   quick4       cfg 4, 3 steps, no CPU baseline / PMC   -> quick4.json
+#   quickv:V / quick4v:V  the same with the variant library exp/v/V (tools/build_variant.sh)
 #   cfg5c1       cfg 5 at one context with the host stage clocks (PF_DEBUG host_prof=1) -> cfg5c1.err
 #   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> exp/v/k5t) per-phase K5 clocks -> k5t.err
 #   pmc:NAME:C1,C2..  one rocprofv3 --pmc pass over a 20-step cfg-2 run -> pmc_NAME/
@@ -32,6 +33,12 @@ for S in "$@"; do
         timeout -k 10 900 python3 bench.py --workload $S > $O/$S.json 2> $O/$S.err || exit 4 ;;
     quick)
         timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 $Q > $O/quick.json 2> $O/quick.err || exit 5 ;;
+    quickv:*)
+        V=${S#quickv:}
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --steps 100 --warmup 10 $Q > $O/quick_$V.json 2> $O/quick_$V.err || exit 5 ;;
+    quick4v:*)
+        V=${S#quick4v:}
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4_$V.json 2> $O/quick4_$V.err || exit 6 ;;
     quick4)
         timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
     cfg5c1)

@@ -103,15 +103,36 @@ struct Engine {
 struct EngineKey {
     const void* profiles = nullptr;
     size_t n_profiles = 0;
+    uint64_t fingerprint = 0;  // a content sample of the map (a recycled address is not reused blindly)
     int device = 0;
     std::vector<std::string> cols;
     NormMap field, column;
     std::shared_ptr<const IdfMap> idf;
     bool same(const EngineKey& o) const {
-        return profiles == o.profiles && n_profiles == o.n_profiles && device == o.device && cols == o.cols &&
+        return profiles == o.profiles && n_profiles == o.n_profiles && fingerprint == o.fingerprint &&
+               device == o.device && cols == o.cols &&
                field == o.field && column == o.column && (idf == o.idf || *idf == *o.idf);
     }
 };
+
+// FNV-1a over the first (up to) 64 profiles in the map's iteration order: ids, scalar fields and
+// list sizes. O(64) per engine lookup; tells a profiles map destroyed and re-created at the same
+// address with the same size from the one the engine was opened for.
+template <class Map>
+uint64_t profiles_fingerprint(const Map& m) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](int64_t v) {
+        for (int i = 0; i < 8; ++i) { h ^= (uint64_t)(v >> (8 * i)) & 0xFFu; h *= 1099511628211ull; }
+    };
+    int n = 0;
+    for (auto it = m.begin(); it != m.end() && n < 64; ++it, ++n) {
+        const auto& p = it->second;
+        mix(it->first); mix(p.public_flag); mix(p.completion_percentage); mix(p.gender); mix(p.age);
+        mix((int64_t)p.clubs.size()); mix((int64_t)p.friends.size()); mix((int64_t)p.token_cols.size());
+        for (const auto& c : p.token_cols) mix((int64_t)c.size());
+    }
+    return h;
+}
 
 struct Registry {
     std::mutex mu;
@@ -324,6 +345,7 @@ private:
         detail::EngineKey key;
         key.profiles = profiles;
         key.n_profiles = profiles->size();
+        key.fingerprint = detail::profiles_fingerprint(*profiles);
         key.device = device_;
         key.cols = cols;
         key.field = field_normalizers;

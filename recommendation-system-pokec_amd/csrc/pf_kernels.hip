@@ -1419,8 +1419,13 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint32_t f = (uint32_t)(tid + kPostThreads * u);
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 8)
+                        js[u] = f < F ? ja : -1;  // experiment: no list lookup (wrong entries, in range)
+                        xs[u] = js[u] >= 0 ? min(rng[js[u]].x + (g0 + f - gpre[js[u]]), ps.n_tok_entries - 1) : 0u;
+#else
                         js[u] = f < F ? round_list(gpre, ja, jb, g0 + f) : -1;
                         xs[u] = js[u] >= 0 ? rng[js[u]].x + (g0 + f - gpre[js[u]]) : 0u;  // 0: a valid address
+#endif
                     }
                     uint32_t ent[U];
 #pragma unroll
@@ -1478,6 +1483,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 // c. place every hit at its slot, the column's first hit with its norm
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 16)
+                    break;  // experiment: no placing
+#endif
                     if (kp[u] == ~0u) continue;
                     const uint32_t p = kp[u] & 1023u, jr = (kp[u] >> 10) & 63u, tf = kp[u] >> 16;
                     const uint64_t below = mask[p] & low_bits(jr);
@@ -1504,6 +1512,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 __syncthreads();
                 K5T(8);
                 // d. terms, one (candidate, column) item per lane over the wave's slots
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 2)
+                if (false)  // experiment: no terms
+#endif
                 for (uint32_t r = wb + (uint32_t)lane; r < wb + wn; r += 64) {
                     const uint32_t h = hit[r];
                     if (!(h & kHitFirst)) continue;
@@ -1518,7 +1529,11 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                         if ((h2 & kHitCand) || j2 >= hi) break;
                         dot += tok_product(pt, ja + (int)j2, h2 & 0xFFu);
                     }
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 1)
+                    slot[r] = dot;  // experiment: no cosine -> sigmoid
+#else
                     slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, slot[r]);
+#endif
                 }
                 wave_sync();
                 K5T(9);
@@ -1532,7 +1547,11 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 const int p = kk * kPostThreads + tid;
                 const uint64_t m = F > 0 ? mask[p] : 0ull;
                 const uint32_t hb0 = F > 0 ? hbase[p] : 0u;
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 4)
+                for (uint64_t pr = 0; pr; pr &= pr - 1) {  // experiment: no owner sums
+#else
                 for (uint64_t pr = pend[kk] & rtm; pr; pr &= pr - 1) {
+#endif
                     const int t = __ffsll((unsigned long long)pr) - 1;
                     const QCol col = scol[cidx[t]];
                     const uint32_t lo = (uint32_t)(max(col.j0, ja) - ja), hi = (uint32_t)(min(col.j1, jb) - ja);

@@ -8,6 +8,11 @@ the sequential drivers) and prints one JSON line with the timings.
     python tools/eval_holdout.py --data DIR [--lines N] [--holdout S] [--rectests S] [--topk K]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/eval_holdout.py ...
     python tools/eval_holdout.py --make-data DIR --users N     (writes a synthetic corpus in reference formats)
+    python tools/eval_holdout.py --cfg5-corpus 1632803 --whole --check-prefix 64 --out F.json
+        (BASELINE cfg 5 on the whole corpus: bench.py's seed-1 cfg-5 corpus, written if missing, and
+         EVERY eligible user of both drivers -- degree >= 20 for test.cpp:20-26, degree >= 4 for
+         recommendation_tests.cpp:79-90 -- with the batched drivers' first N users checked against
+         the sequential drivers run over N users)
 
 --sequential also times the one-user-at-a-time drivers (rank 0) and checks equality.
 """
@@ -40,7 +45,29 @@ def main():
     ap.add_argument("--topk", type=int, default=10)
     ap.add_argument("--batch", type=int, default=2048, help="users per device pass (large passes run as pipelined chunks)")
     ap.add_argument("--sequential", action="store_true")
+    ap.add_argument("--cfg5-corpus", type=int, default=0, help="use bench.py's cfg-5 corpus of this many users")
+    ap.add_argument("--whole", action="store_true", help="every eligible user (sample sizes = the profile count)")
+    ap.add_argument("--check-prefix", type=int, default=0,
+                    help="rank 0: the sequential drivers over this many users against the batched run's prefix")
+    ap.add_argument("--out", default=None)
     args = ap.parse_args()
+    if args.cfg5_corpus:
+        sys.path.insert(0, ROOT)
+        import bench
+        import synth
+        args.data = bench.cfg5_dir(args.cfg5_corpus)
+        marker = os.path.join(args.data, "written")
+        if int(os.environ.get("RANK", "0")) == 0 and not os.path.exists(marker):
+            c = synth.Corpus(n_users=args.cfg5_corpus, seed=1, edge_cases=0, threads=16)
+            c.write_reference_files(args.data)
+            del c
+            with open(marker, "w") as f:
+                f.write("ok\n")
+        t = time.time()
+        while not os.path.exists(marker):
+            if time.time() - t > 900:
+                raise RuntimeError("cfg5 corpus files not written")
+            time.sleep(1.0)
     if args.make_data:
         import synth
         c = synth.Corpus(n_users=args.users, seed=5, edge_cases=0, threads=16)
@@ -60,10 +87,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import pokec_fas as pf
     t0 = time.time()
-    ds = pf.Dataset(args.data, args.lines if args.lines > 0 else 2**62)
+    cache = os.path.join(args.data, f"parse_r{rank}.bin") if args.cfg5_corpus else None
+    ds = pf.Dataset(args.data, args.lines if args.lines > 0 else 2**62, cache=cache)
     eng = pf.FasEngine(ds.desc_ptr(), local)
     t_open = time.time() - t0
     info = ds.info()
+    if args.whole:
+        args.holdout = args.rectests = int(info.n_profiles)
 
     def gather(a):
         if world == 1:
@@ -106,8 +136,19 @@ def main():
         rec["sequential"] = {"holdout_s": t5 - t4, "rectests_s": t6 - t5,
                              "holdout_equal": bool(np.array_equal(seq.view(np.uint64), ratios.view(np.uint64))),
                              "rectests_equal": list(seq5) == list(rec5)}
+    if args.check_prefix and rank == 0:
+        P = args.check_prefix
+        seq = ds.holdout_friends(eng, P)
+        seq5 = ds.recommendation_tests(eng, P, args.topk)
+        rec["prefix_check"] = {
+            "users": P,
+            "holdout_equal": bool(np.array_equal(seq.view(np.uint64), ratios[:len(seq)].view(np.uint64))),
+            "rectests_equal": [float(x) for x in seq5] == [float(x) for x in pf.rec_tests_summary(hits[:P], club[:P])]}
     if rank == 0:
         print(json.dumps(rec), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(rec, f, indent=1)
     eng.close()
     if dist:
         dist.barrier()

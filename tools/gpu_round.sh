@@ -39,6 +39,18 @@ for S in "$@"; do
     quick4v:*)
         V=${S#quick4v:}
         timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4_$V.json 2> $O/quick4_$V.err || exit 6 ;;
+    quickd:*|quick4d:*)
+        # the same quick lines from another tree (e.g. a git worktree of an older commit under exp/)
+        D=${S#*:}; N=$(basename $D); W=""; [[ $S == quick4d:* ]] && W="--workload cfg4 --steps 3 --warmup 1" || W="--steps 100 --warmup 10"
+        (cd $D && timeout -k 10 300 python3 bench.py $W $Q) > $O/${S%%:*}_$N.json 2> $O/${S%%:*}_$N.err || exit 6 ;;
+    whole5)
+        # cfg 5 over EVERY eligible user of the 1.63M corpus (both drivers), prefix-checked
+        timeout -k 10 1000 python3 -u tools/eval_holdout.py --cfg5-corpus 1632803 --whole --check-prefix 64 \
+            --out $O/whole5.json > $O/whole5.log 2>&1 || exit 10 ;;
+    quick4e:*)
+        # cfg 4 quick line under a PF_DEBUG setting, e.g. quick4e:k5_query_major=1
+        E=${S#quick4e:}
+        timeout -k 10 300 env PF_DEBUG=$E python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4e_${E//[=,]/_}.json 2> $O/quick4e.err || exit 6 ;;
     quick4)
         timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
     cfg5c1)

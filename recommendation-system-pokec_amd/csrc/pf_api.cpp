@@ -254,11 +254,11 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 // static per cfg-2 launch; batches (one block per workgroup in L2-sharing order) stay static
 // (cfg 4 9.83e9 dynamic vs 9.88e9 static).
 // K5 launch mode: bit 0 = dynamic block hand-out (one query); bit 1 = transposed grid (batches:
-// the resident workgroups are many queries on the same candidate blocks, sharing their lists in
-// L2; PF_DEBUG k5_query_major=1 keeps the query-major grid)
+// the resident workgroups are many queries on the same candidate blocks; PF_DEBUG k5_transposed=1.
+// Measured slower than the query-major grid: cfg 4 216.9 vs 203.4 ms per 1024-query launch, r4c)
 uint32_t post_mode(int nq) {
-    static const bool qmajor = pf::debug_long("k5_query_major", 0) != 0;
-    return nq == 1 ? 1u : (qmajor ? 0u : 2u);
+    static const bool tr = pf::debug_long("k5_transposed", 0) != 0;
+    return nq == 1 ? 1u : (tr ? 2u : 0u);
 }
 
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once
@@ -309,19 +309,30 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
               uint64_t* d_keys, hipStream_t s, bool timed) {
     const int nq = (int)imgs.size();
     if (nq == 0) return PF_OK;
-    std::vector<uint32_t> offs;
-    int max_lists = 0, max_tok = 0;
-    size_t pool_b = 0;
-    for (const auto* im : imgs) {
-        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(im->data() + sizeof(pf::QConst));
-        max_lists = std::max(max_lists, h->n_tok + h->n_club + h->n_friend);
-        max_tok = std::max(max_tok, h->n_tok);
-        offs.push_back((uint32_t)pool_b);
-        pool_b += im->size();
+    // LDS classes: a launch's workgroups all take the LDS of its largest query, so the batch goes
+    // out in one launch per occupancy class (workgroups per CU), the queries of a class contiguous
+    // in the staged arrays; one query with thousands of friends no longer runs every query of a
+    // batch at one workgroup per CU
+    std::vector<uint32_t> vl(nq);
+    std::vector<int> pcu(nq), order(nq);
+    for (int q = 0; q < nq; ++q) {
+        const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[q]->data() + sizeof(pf::QConst));
+        vl[q] = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
+        pcu[q] = pf::post_blocks_per_cu(vl[q]);
+        order[q] = q;
     }
-    const uint32_t wave_lds = pf::post_var_lds(max_tok, max_lists);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pcu[a] > pcu[b]; });
+    std::vector<uint32_t> offs;
+    std::vector<int32_t> orows(nq);
+    size_t pool_b = 0;
+    for (int i = 0; i < nq; ++i) {
+        offs.push_back((uint32_t)pool_b);
+        pool_b += imgs[order[i]]->size();
+        orows[i] = rows[order[i]];
+    }
+    const uint32_t wave_lds = vl[order[0]];  // the one-query case
     const int nwb = c->wb_end - c->wb_begin;
-    const int per_cu = pf::post_blocks_per_cu(wave_lds);
+    const int per_cu = pcu[order[0]];
     // One query: one resident round of workgroups loops over the blocks.  A batch: one block
     // per workgroup, so the resident workgroups (dispatched x-fastest) cover one or two
     // queries at a time and share their lists and cells in L2; with a few workgroups per
@@ -336,9 +347,10 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     uint8_t* h = c->stage_acquire(total);
     if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
     std::memcpy(h, offs.data(), (size_t)nq * 4);
-    std::memcpy(h + offs_b, rows.data(), (size_t)nq * 4);
+    std::memcpy(h + offs_b, orows.data(), (size_t)nq * 4);
     std::memset(h + offs_b + rows_b, 0, sync_b);
-    for (int q = 0; q < nq; ++q) std::memcpy(h + offs_b + rows_b + sync_b + offs[q], imgs[q]->data(), imgs[q]->size());
+    for (int i = 0; i < nq; ++i)
+        std::memcpy(h + offs_b + rows_b + sync_b + offs[i], imgs[order[i]]->data(), imgs[order[i]]->size());
     HIPCHK(c, c->d_pool.ensure(total));
     HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
     HIPCHK(c, c->stage_release(s));
@@ -349,11 +361,19 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     if (rc != PF_OK) return rc;
     // timed: the events ride in the kernel's dispatch (its own start / end; r2ff: 1.8 us less
     // per launch than two marker packets around it)
-    HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base), wave_lds,
-                              nq, c->wb_begin, c->wb_end, k, blocks, c->d_part.as<uint64_t>(),
-                              reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b), d_keys,
-                              reinterpret_cast<const int32_t*>(base + offs_b), post_mode(nq),
-                              timed ? e0 : nullptr, timed ? e1 : nullptr, s));
+    // one launch per class (the first one's start and the last one's end time the call)
+    for (int q0 = 0; q0 < nq;) {
+        int q1 = q0;
+        uint32_t vmax = 0;
+        while (q1 < nq && pcu[order[q1]] == pcu[order[q0]]) vmax = std::max(vmax, vl[order[q1++]]);
+        HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
+                                  nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
+                                  c->d_part.as<uint64_t>() + (size_t)q0 * blocks * k,
+                                  reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
+                                  reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
+                                  (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
+        q0 = q1;
+    }
     if (timed) {
         c->last_ev0 = e0;
         c->last_ev1 = e1;

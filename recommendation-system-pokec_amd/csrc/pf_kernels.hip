@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 
@@ -1080,14 +1081,28 @@ constexpr uint32_t kLdsMask = 0;                                          // u64
 constexpr uint32_t kLdsSlot = kLdsMask + 8 * kBlockCands;                 // f64 [kRoundCap] norm -> term
 constexpr uint32_t kLdsHit = kLdsSlot + 8 * kRoundCap;                    // u16 [kRoundCap] hits
 constexpr uint32_t kLdsHbase = kLdsHit + 2 * kRoundCap;                   // u16 [kBlockCands] first slot
-constexpr uint32_t kLdsCnt = kLdsHbase + 2 * kBlockCands;                 // u32 [kBlockCands] set counters
+// the set counters and exclusion bits are read by the fixed terms only, before any thread passes
+// round 0's walk barrier and writes a slot: they live in the slots
+constexpr uint32_t kLdsCnt = kLdsSlot;                                    // u32 [kBlockCands] set counters
 constexpr uint32_t kLdsExb = kLdsCnt + 4 * kBlockCands;                   // u32 [kBlockCands / 32] excluded
-constexpr uint32_t kLdsMisc = kLdsExb + 4 * (kBlockCands / 32);           // u32 [16]
+static_assert(4 * kBlockCands + 4 * (kBlockCands / 32) <= 8 * kRoundCap, "set counters alias the slots");
+constexpr uint32_t kLdsMisc = kLdsHbase + 2 * kBlockCands;                // u32 [16]
 constexpr uint32_t kLdsCols = kLdsMisc + 64;                              // QCol [kPostMaxCols]
 constexpr uint32_t kLdsFtab = kLdsCols + 16 * kPostMaxCols;               // f64 [7 + 48 + 1] F by used
 constexpr uint32_t kLdsSeg = kLdsFtab + 8 * (kNumFixed + kPostMaxCols + 1);  // u32 [kRoundToks] token segments
-constexpr uint32_t kLdsCidx = kLdsSeg + 4 * kRoundToks;                   // u8 [kPostMaxCols] column -> active index
-constexpr uint32_t kPostFixedLds = (kLdsCidx + kPostMaxCols + 15) & ~15u;
+constexpr uint32_t kLdsCidx = kLdsSeg + 4 * kRoundToks;                   // end of the fixed tables
+// round list maps, two buffers (the next round's is built during this one): flat entry f < kRoundCap
+// -> its list without a search (bits of the nonempty lists' starts, nonempty lists before each
+// 64-entry word, and per nonempty list {entry index of flat 0, token - round start})
+constexpr uint32_t kMapWords = kRoundCap / 64;
+constexpr uint32_t kLdsMapB = (kLdsCidx + 7) & ~7u;                            // u64 [2][kMapWords]
+constexpr uint32_t kLdsMapN = kLdsMapB + 2 * 8 * kMapWords;                   // uint2 [2][kRoundToks]
+constexpr uint32_t kLdsMapC = kLdsMapN + 2 * 8 * kRoundToks;                  // u8 [2][kMapWords]
+// per query column number: its token range j0 | j1 << 16; per active column index c: the column
+// numbers of active columns < c as a mask (a round's columns [ca, ce) = cpre[ce] & ~cpre[ca])
+constexpr uint32_t kLdsColj = (kLdsMapC + 2 * kMapWords + 7) & ~7u;           // u32 [kPostMaxCols]
+constexpr uint32_t kLdsCpre = kLdsColj + 4 * kPostMaxCols;                    // u64 [kPostMaxCols + 1]
+constexpr uint32_t kPostFixedLds = (kLdsCpre + 8 * (kPostMaxCols + 1) + 15) & ~15u;
 static_assert(kBlockCands == 2 * kPostThreads, "two candidates per thread");
 static_assert(kRoundCap < 65536 && kBlockCands <= kRoundCap, "u16 slots; a one-token round fits");
 static_assert(kPostWaves * kMaxTopK * 8 + 16 + 4 * kMaxTopK <= 8 * kRoundCap, "scan_tail scratch in the slots");
@@ -1181,6 +1196,37 @@ __device__ __forceinline__ int round_list(const uint32_t* gpre, int ja, int jb, 
     return j;
 }
 
+// The list map of round [ja, jb) into buffer (mb, mc, mn), by one wave (lane = its lane): bit
+// s_j of mb for each list j whose entries start at flat s_j < kRoundCap and are nonempty, mc[w] =
+// such lists starting before word w, mn[k] = the k-th one's {entry index of flat 0, j - ja}.
+__device__ __forceinline__ void build_map(uint64_t* mb, uint8_t* mc, uint2* mn, const uint32_t* gpre,
+                                          const uint2* rng, int ja, int jb, int lane) {
+    const uint32_t g0 = gpre[ja];
+    const int j = ja + lane;
+    uint32_t s = 0;
+    bool ne = false;
+    if (j < jb) {
+        s = gpre[j] - g0;
+        ne = gpre[j + 1] - g0 > s && s < (uint32_t)kRoundCap;
+    }
+    if (lane < (int)kMapWords) mb[lane] = 0ull;
+    const uint64_t bal = __ballot(ne);
+    const uint32_t k = (uint32_t)__popcll(bal & low_bits((uint32_t)lane));
+    wave_sync();
+    if (ne) {
+        atomicOr(reinterpret_cast<unsigned long long*>(&mb[s >> 6]), 1ull << (s & 63u));
+        mn[k] = make_uint2(rng[j].x - s, (uint32_t)lane);
+    }
+    wave_sync();
+    uint32_t c = lane < (int)kMapWords ? (uint32_t)__popcll(mb[lane]) : 0u, x = c;
+#pragma unroll
+    for (int o = 1; o < (int)kMapWords; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane < (int)kMapWords) mc[lane] = (uint8_t)(x - c);
+}
+
 // product of one shared token, recommender.cpp:74-85: wA * wB, wB = tf * idf
 __device__ __forceinline__ double tok_product(const PTok* pt, int j, uint32_t tf) {
     const PTok v = pt[j];
@@ -1229,7 +1275,10 @@ __device__ __forceinline__ Round next_round(const QCol* scol, const uint32_t* gp
 #define K5T(slot) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
+#ifndef PF_K5_MINB
+#define PF_K5_MINB 4  // workgroups per CU the register budget is sized for (LDS allows 4 for most queries)
+#endif
+__global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(PostStore ps, const uint8_t* __restrict__ pool,
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
@@ -1267,13 +1316,22 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
     uint2* rng = reinterpret_cast<uint2*>(pl + nl);
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + nl);
     uint8_t* colof = reinterpret_cast<uint8_t*>(gpre + H.n_tok + 1);  // token -> active column index
-    uint8_t* cidx = reinterpret_cast<uint8_t*>(base + kLdsCidx);        // column -> active column index
+    uint64_t* mapb = reinterpret_cast<uint64_t*>(base + kLdsMapB);
+    uint2* mapn = reinterpret_cast<uint2*>(base + kLdsMapN);
+    uint8_t* mapc = reinterpret_cast<uint8_t*>(base + kLdsMapC);
+    uint32_t* colj = reinterpret_cast<uint32_t*>(base + kLdsColj);
+    uint64_t* cpre = reinterpret_cast<uint64_t*>(base + kLdsCpre);
     stage(smem, img, sizeof(QConst));
     for (int j = tid; j < H.n_act; j += kPostThreads) {
         const QCol c = cols[j];
         scol[j] = c;
-        cidx[c.t] = (uint8_t)j;
+        colj[c.t] = (uint32_t)c.j0 | (uint32_t)c.j1 << 16;
         for (int x = c.j0; x < c.j1; ++x) colof[x] = (uint8_t)j;
+    }
+    if (tid == 0) {  // prefix masks of the active columns (<= 48, ascending)
+        uint64_t m = 0;
+        for (int j = 0; j < H.n_act; ++j) { cpre[j] = m; m |= 1ull << cols[j].t; }
+        cpre[H.n_act] = m;
     }
     for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kPostThreads)
         ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(img)->n_cols);
@@ -1325,7 +1383,17 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         K5T(0);
         __syncthreads();
         K5T(1);
-        if (tid < 64) wave_prefix(gpre, rng, H.n_tok, lane);  // read after the barrier below
+        if (tid < 64) {  // read after the barrier below
+            wave_prefix(gpre, rng, H.n_tok, lane);
+#ifndef PF_K5_BISECT
+            wave_sync();
+            if (H.n_act > 0) {
+                int ci0 = 0, j0 = 0;
+                const Round R0 = next_round(scol, gpre, H.n_act, ci0, j0);
+                build_map(mapb, mapc, mapn, gpre, rng, R0.ja, R0.jb, lane);
+            }
+#endif
+        }
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short (loaded above, no
         // barrier of its own), else bisect and walk until past the block
         if (short_excl) {
@@ -1394,9 +1462,10 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
         uint32_t chit = 0;                                     // bit kk: the split column has a hit
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
-        int ci = 0, jcur = 0;
+        int ci = 0, jcur = 0, rnd = 0;
         while (ci < H.n_act) {
             const Round R = next_round(scol, gpre, H.n_act, ci, jcur);
+            const int mbuf = rnd++ & 1;  // this round's list map buffer
             const int ja = R.ja, jb = R.jb;
             const uint32_t g0 = gpre[ja], F = gpre[jb] - g0;  // the round's flat entries
             if (F > 0) {
@@ -1422,6 +1491,18 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 8)
                         js[u] = f < F ? ja : -1;  // experiment: no list lookup (wrong entries, in range)
                         xs[u] = js[u] >= 0 ? min(rng[js[u]].x + (g0 + f - gpre[js[u]]), ps.n_tok_entries - 1) : 0u;
+#elif !defined(PF_K5_BISECT)
+                        // the list map: nonempty lists starting at or before f, minus one
+                        js[u] = -1;
+                        xs[u] = 0u;  // a valid address
+                        if (f < F) {
+                            const uint32_t w = f >> 6;
+                            const uint32_t kk = (uint32_t)mapc[mbuf * kMapWords + w] +
+                                                (uint32_t)__popcll(mapb[mbuf * kMapWords + w] & low_bits((f & 63u) + 1u)) - 1u;
+                            const uint2 L = mapn[mbuf * kRoundToks + kk];
+                            js[u] = ja + (int)L.y;
+                            xs[u] = L.x + f;
+                        }
 #else
                         js[u] = f < F ? round_list(gpre, ja, jb, g0 + f) : -1;
                         xs[u] = js[u] >= 0 ? rng[js[u]].x + (g0 + f - gpre[js[u]]) : 0u;  // 0: a valid address
@@ -1452,6 +1533,15 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 K5T(4);
                 __syncthreads();
                 K5T(5);
+#ifndef PF_K5_BISECT
+                if (tid < 64 && ci < H.n_act) {  // the next round's list map (published by the slots barrier)
+                    int ci1 = ci, j1 = jcur;
+                    const Round R1 = next_round(scol, gpre, H.n_act, ci1, j1);
+                    const int nb = mbuf ^ 1;
+                    build_map(mapb + nb * kMapWords, mapc + nb * kMapWords, mapn + nb * kRoundToks, gpre, rng, R1.ja,
+                              R1.jb, lane);
+                }
+#endif
                 // b. hit slots: the wave's candidates' hits in one contiguous range
                 uint32_t nk[kCandsPerThread], tot = 0;
 #pragma unroll
@@ -1493,7 +1583,9 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     const uint32_t lo = seg[jr] & 0xFFu;
                     const bool first = (below >> lo) == 0ull;
                     hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
-                    if (first) slot[r] = kn[u];
+                    // the column's first hit holds its norm, the others their product (one per lane here,
+                    // so the terms below only add them up)
+                    slot[r] = first ? kn[u] : tok_product(pt, ja + (int)jr, tf);
                 }
                 for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {
                     const int j = round_list(gpre, ja, jb, g0 + f);
@@ -1506,7 +1598,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                     const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 9);
                     const bool first = (below >> (seg[jr] & 0xFFu)) == 0ull;
                     hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
-                    if (first) slot[r] = ps.pnorm[x];
+                    slot[r] = first ? ps.pnorm[x] : tok_product(pt, ja + (int)jr, e & 0xFFu);
                 }
                 K5T(7);
                 __syncthreads();
@@ -1527,7 +1619,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                         const uint32_t h2 = hit[r2];
                         const uint32_t j2 = (h2 >> 8) & 63u;
                         if ((h2 & kHitCand) || j2 >= hi) break;
-                        dot += tok_product(pt, ja + (int)j2, h2 & 0xFFu);
+                        dot += slot[r2];  // the hit's product (placed above)
                     }
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 1)
                     slot[r] = dot;  // experiment: no cosine -> sigmoid
@@ -1540,8 +1632,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
             }
             // e. the owners add the round's common columns in ascending order (the candidate's
             // columns among the round's: ~3 per round instead of every round column)
-            uint64_t rtm = 0;  // the round's columns, by column number
-            for (int c = R.ca; c < R.ce; ++c) rtm |= 1ull << scol[c].t;
+            const uint64_t rtm = cpre[R.ce] & ~cpre[R.ca];  // the round's columns, by column number
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) {
                 const int p = kk * kPostThreads + tid;
@@ -1553,11 +1644,12 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 for (uint64_t pr = pend[kk] & rtm; pr; pr &= pr - 1) {
 #endif
                     const int t = __ffsll((unsigned long long)pr) - 1;
-                    const QCol col = scol[cidx[t]];
-                    const uint32_t lo = (uint32_t)(max(col.j0, ja) - ja), hi = (uint32_t)(min(col.j1, jb) - ja);
+                    const uint32_t cj = colj[t];
+                    const int cj0 = (int)(cj & 0xFFFFu), cj1 = (int)(cj >> 16);
+                    const uint32_t lo = (uint32_t)(max(cj0, ja) - ja), hi = (uint32_t)(min(cj1, jb) - ja);
                     const uint64_t h = m & (low_bits(hi) & ~low_bits(lo));
                     const uint32_t r0 = hb0 + (uint32_t)__popcll(m & low_bits(lo));
-                    if (col.j0 >= ja && col.j1 <= jb) {
+                    if (cj0 >= ja && cj1 <= jb) {
                         sum[kk] += h ? slot[r0] : q.sig0_col[t];
                         continue;
                     }
@@ -1573,7 +1665,7 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                         cnrm[kk] = slot[r0];
                         chit |= 1u << kk;
                     }
-                    if (col.j1 <= jb) {
+                    if (cj1 <= jb) {
                         const bool hh = (chit >> kk) & 1u;
                         sum[kk] += (hh && cdot[kk] != 0.0) ? text_term(q, t, cdot[kk], cnrm[kk]) : q.sig0_col[t];
                         cdot[kk] = 0.0;
@@ -1583,6 +1675,18 @@ __global__ __launch_bounds__(kPostThreads, 4) void fas_post_kernel(PostStore ps,
                 if (F > 0) mask[p] = 0ull;
             }
             K5T(10);
+#ifndef PF_K5_BISECT
+            if (F == 0 && ci < H.n_act) {  // an empty round built no list map for the next one
+                if (tid < 64) {
+                    int ci1 = ci, j1 = jcur;
+                    const Round R1 = next_round(scol, gpre, H.n_act, ci1, j1);
+                    const int nb = mbuf ^ 1;
+                    build_map(mapb + nb * kMapWords, mapc + nb * kMapWords, mapn + nb * kRoundToks, gpre, rng,
+                              R1.ja, R1.jb, lane);
+                }
+                __syncthreads();
+            }
+#endif
             if (F > 0) __syncthreads();  // the next round rewrites the masks, slots and segments
         }
         K5T(11);
@@ -1800,14 +1904,16 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
 }
 
 int post_blocks_per_cu(uint32_t var_lds) {
-    static thread_local uint32_t last_key = ~0u;
-    static thread_local int last_nb = 1;
-    if (var_lds == last_key) return last_nb;
+    // per thread, by LDS bytes (a batch asks once per query: the occupancy API once per size)
+    static thread_local std::unordered_map<uint32_t, int> memo;
+    auto it = memo.find(var_lds);
+    if (it != memo.end()) return it->second;
     int nb = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_post_kernel, kPostThreads, post_lds(var_lds));
-    last_key = var_lds;
-    last_nb = (e == hipSuccess && nb > 0) ? nb : 1;
-    return last_nb;
+    nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    if (memo.size() > 4096) memo.clear();
+    memo.emplace(var_lds, nb);
+    return nb;
 }
 
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,

@@ -200,9 +200,12 @@ constexpr int kBlockCands = 2 * kPostThreads;  // candidates of a workgroup bloc
 constexpr int kCandsPerThread = kBlockCands / kPostThreads;
 // K5 rounds: a block's query tokens are taken in rounds of <= kRoundToks tokens (one 64-bit hit
 // mask per candidate) whose list entries in the block number <= kRoundCap (the round's hit slots,
-// 8 per thread)
+// PF_K5_RCAP per thread)
+#ifndef PF_K5_RCAP
+#define PF_K5_RCAP 6
+#endif
 constexpr int kRoundToks = 64;
-constexpr int kRoundCap = 8 * kPostThreads;
+constexpr int kRoundCap = PF_K5_RCAP * kPostThreads;
 constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
 constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
 constexpr int kPostMinShift = 9;           // cells of >= 512 candidates: a block spans at most 3

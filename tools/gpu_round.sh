@@ -57,6 +57,10 @@ for S in "$@"; do
         timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5c1.json 2> $O/cfg5c1.err || exit 4 ;;
     k5t)
         timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/k5t/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/k5t.json 2> $O/k5t.err || exit 7 ;;
+    pmcv:*)
+        # pmcv:V:C1,C2..  one counter pass over 20 cfg-2 steps with the variant library exp/v/V (K5 rows only)
+        R=${S#pmcv:}; V=${R%%:*}; C=${R#*:}
+        timeout -s KILL 120 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so rocprofv3 --pmc ${C//,/ } --kernel-include-regex fas_post -d $O/pmcv_$V -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmcv_$V.json 2> $O/pmcv_$V.err || exit 8 ;;
     pmc:*)
         R=${S#pmc:}; N=${R%%:*}; C=${R#*:}
         timeout -s KILL 120 rocprofv3 --pmc ${C//,/ } -d $O/pmc_$N -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmc_$N.json 2> $O/pmc_$N.err || exit 8 ;;

@@ -53,6 +53,14 @@ for S in "$@"; do
         timeout -k 10 300 env PF_DEBUG=$E python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4e_${E//[=,]/_}.json 2> $O/quick4e.err || exit 6 ;;
     quick4)
         timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
+    cfg5c:*)
+        # cfg5c:N  cfg 5 at N engine contexts, 5 timed steps, no CPU baseline / PMC
+        N=${S#cfg5c:}
+        timeout -k 10 900 python3 bench.py --workload cfg5 --contexts $N --steps 5 --warmup 2 $Q > $O/cfg5c$N.json 2> $O/cfg5c$N.err || exit 4 ;;
+    rehearse:*)
+        # rehearse:N[:W]  bench.py's N > 1 path with N gloo ranks on this one GPU (tools/rehearse_multi.sh)
+        R=${S#rehearse:}; N=${R%%:*}; W=cfg4; [[ $R == *:* ]] && W=${R#*:}
+        bash tools/rehearse_multi.sh $TAG $N $W || exit 11 ;;
     cfg5c1)
         timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5c1.json 2> $O/cfg5c1.err || exit 4 ;;
     k5t)

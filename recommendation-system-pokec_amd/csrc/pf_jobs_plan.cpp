@@ -1166,7 +1166,8 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     // is planned and launched while chunk i runs on the device, then chunk i is unpacked.
     // Only large calls are cut: splitting a 64-user cfg-3 step into four chunks made it slower
     // (1.09 -> 1.50 ms: four times the launches, each too small to fill the GPU; r2n).
-    const size_t chunk_jobs = n < kPipeJobs ? n : std::max<size_t>(kPipeJobs / 2, (n + 2) / 3);
+    static const size_t nchunks = (size_t)std::max(1L, debug_long("chunks", 3));  // PF_DEBUG chunks=N (A/B)
+    const size_t chunk_jobs = n < kPipeJobs ? n : std::max<size_t>(kPipeJobs / 2, (n + nchunks - 1) / nchunks);
     int slot = 0;
     JobsState::Ws* pending = nullptr;
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first

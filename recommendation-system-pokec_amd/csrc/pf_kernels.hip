@@ -1086,7 +1086,8 @@ constexpr uint32_t kLdsHbase = kLdsHit + 2 * kRoundCap;                   // u16
 constexpr uint32_t kLdsCnt = kLdsSlot;                                    // u32 [kBlockCands] set counters
 constexpr uint32_t kLdsExb = kLdsCnt + 4 * kBlockCands;                   // u32 [kBlockCands / 32] excluded
 static_assert(4 * kBlockCands + 4 * (kBlockCands / 32) <= 8 * kRoundCap, "set counters alias the slots");
-constexpr uint32_t kLdsMisc = kLdsHbase + 2 * kBlockCands;                // u32 [16]
+constexpr uint32_t kLdsItem = kLdsHbase + 2 * kBlockCands;                // u16 [kRoundCap] term items
+constexpr uint32_t kLdsMisc = (kLdsItem + 2 * kRoundCap + 15) & ~15u;       // u32 [16]
 constexpr uint32_t kLdsCols = kLdsMisc + 64;                              // QCol [kPostMaxCols]
 constexpr uint32_t kLdsFtab = kLdsCols + 16 * kPostMaxCols;               // f64 [7 + 48 + 1] F by used
 constexpr uint32_t kLdsSeg = kLdsFtab + 8 * (kNumFixed + kPostMaxCols + 1);  // u32 [kRoundToks] token segments
@@ -1303,6 +1304,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     double* slot = reinterpret_cast<double*>(base + kLdsSlot);
     uint16_t* hit = reinterpret_cast<uint16_t*>(base + kLdsHit);
     uint16_t* hbase = reinterpret_cast<uint16_t*>(base + kLdsHbase);
+    uint16_t* item = reinterpret_cast<uint16_t*>(base + kLdsItem);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + kLdsCnt);
     uint32_t* exb = reinterpret_cast<uint32_t*>(base + kLdsExb);
     uint32_t* misc = reinterpret_cast<uint32_t*>(base + kLdsMisc);  // [0] next block, [1] hit slots taken
@@ -1607,11 +1609,27 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 2)
                 if (false)  // experiment: no terms
 #endif
-                for (uint32_t r = wb + (uint32_t)lane; r < wb + wn; r += 64) {
+                {
+                // the wave's items (first hits of whole columns; the owner carries a split column),
+                // compacted so the terms run on dense lanes
+                uint16_t* wit = item + wb;
+                uint32_t ni = 0;
+                for (uint32_t r0 = wb; r0 < wb + wn; r0 += 64) {
+                    const uint32_t r = r0 + (uint32_t)lane;
+                    bool is = false;
+                    if (r < wb + wn) {
+                        const uint32_t h = hit[r];
+                        is = (h & kHitFirst) && !(seg[(h >> 8) & 63u] & kSegSplit);
+                    }
+                    const uint64_t bal = __ballot(is);
+                    if (is) wit[ni + (uint32_t)__popcll(bal & low_bits((uint32_t)lane))] = (uint16_t)r;
+                    ni += (uint32_t)__popcll(bal);
+                }
+                wave_sync();
+                for (uint32_t i = (uint32_t)lane; i < ni; i += 64) {
+                    const uint32_t r = wit[i];
                     const uint32_t h = hit[r];
-                    if (!(h & kHitFirst)) continue;
                     const uint32_t jr = (h >> 8) & 63u, sg = seg[jr];
-                    if (sg & kSegSplit) continue;  // the owner carries a split column
                     const uint32_t hi = (sg >> 8) & 0xFFu;
                     const int t = (int)((sg >> 16) & 0xFFu);
                     double dot = tok_product(pt, ja + (int)jr, h & 0xFFu);
@@ -1627,6 +1645,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, slot[r]);
 #endif
                 }
+                }
                 wave_sync();
                 K5T(9);
             }
@@ -1636,8 +1655,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) {
                 const int p = kk * kPostThreads + tid;
-                const uint64_t m = F > 0 ? mask[p] : 0ull;
-                const uint32_t hb0 = F > 0 ? hbase[p] : 0u;
+                // the candidate's hits lie in its common columns only, in ascending token order: the
+                // remaining mask and a running slot index walk them column by column
+                uint64_t mr = F > 0 ? mask[p] : 0ull;
+                uint32_t rr = F > 0 ? hbase[p] : 0u;
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 4)
                 for (uint64_t pr = 0; pr; pr &= pr - 1) {  // experiment: no owner sums
 #else
@@ -1646,9 +1667,11 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const int t = __ffsll((unsigned long long)pr) - 1;
                     const uint32_t cj = colj[t];
                     const int cj0 = (int)(cj & 0xFFFFu), cj1 = (int)(cj >> 16);
-                    const uint32_t lo = (uint32_t)(max(cj0, ja) - ja), hi = (uint32_t)(min(cj1, jb) - ja);
-                    const uint64_t h = m & (low_bits(hi) & ~low_bits(lo));
-                    const uint32_t r0 = hb0 + (uint32_t)__popcll(m & low_bits(lo));
+                    const uint64_t lm = low_bits((uint32_t)(min(cj1, jb) - ja));
+                    const uint64_t h = mr & lm;
+                    mr &= ~lm;
+                    const uint32_t r0 = rr;
+                    rr += (uint32_t)__popcll(h);
                     if (cj0 >= ja && cj1 <= jb) {
                         sum[kk] += h ? slot[r0] : q.sig0_col[t];
                         continue;

@@ -61,6 +61,10 @@ for S in "$@"; do
         # rehearse:N[:W]  bench.py's N > 1 path with N gloo ranks on this one GPU (tools/rehearse_multi.sh)
         R=${S#rehearse:}; N=${R%%:*}; W=cfg4; [[ $R == *:* ]] && W=${R#*:}
         bash tools/rehearse_multi.sh $TAG $N $W || exit 11 ;;
+    cfg5e:*)
+        # cfg5e:SETTINGS  cfg 5 at one context under PF_DEBUG=SETTINGS (e.g. chunks=6)
+        E=${S#cfg5e:}
+        timeout -k 10 900 env PF_DEBUG=$E python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5e_${E//[=,]/_}.json 2> $O/cfg5e_${E//[=,]/_}.err || exit 4 ;;
     cfg5c1)
         timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5c1.json 2> $O/cfg5c1.err || exit 4 ;;
     k5t)

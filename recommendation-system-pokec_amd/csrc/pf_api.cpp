@@ -258,7 +258,8 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 // Measured slower than the query-major grid: cfg 4 216.9 vs 203.4 ms per 1024-query launch, r4c)
 uint32_t post_mode(int nq) {
     static const bool tr = pf::debug_long("k5_transposed", 0) != 0;
-    return nq == 1 ? 1u : (tr ? 2u : 0u);
+    static const bool st = pf::debug_long("k5_static", 0) != 0;  // A/B: static hand-out for one query
+    return nq == 1 ? (st ? 0u : 1u) : (tr ? 2u : 0u);
 }
 
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once

@@ -59,7 +59,7 @@ static __device__ __attribute__((noinline)) double ratio_term(const QConst& q, i
 // ---------------------------------------------------------------- query hash (cuckoo)
 struct QView {
     const QConst* q;
-    const uint2* tab;  // packed: T | T3;  wide: T0 | T1 | T2 (2^lg each) | T3 (2^lg_excl)
+    const uint32_t* tab;  // packed: T | T3;  wide: T0 | T1 | T2 (2^lg each) | T3 (2^lg_excl); SoA per table
     const QVal* vals;
     void* hits;        // LDS [kHitCap + 1][blockDim.x] per-lane token-hit list
     uint32_t* nh;      // LDS [blockDim.x] hit counts, read across the lanes of a split record
@@ -70,20 +70,22 @@ struct QView {
 // Wide tables: 2-choice probe of table `off` (entries), capacity 2^lg; val or kEmptyVal
 __device__ __forceinline__ uint32_t probe(const QView& v, uint32_t off, int lg, uint32_t key) {
     const uint32_t x = cuckoo_x(key, v.hmul);
-    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
-    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
+    const uint32_t* K = v.tab + 2u * off;
+    const uint32_t* V = K + (1u << lg);
+    const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
     // a key sits in at most one of its two slots: AND-combining keeps both reads
     // unconditional (a ?: chain lets the compiler sink the second read into a branch)
-    const uint32_t r1 = e1.x == key ? e1.y : kEmptyVal;
-    const uint32_t r2 = e2.x == key ? e2.y : kEmptyVal;
+    const uint32_t r1 = K[a] == key ? V[a] : kEmptyVal;
+    const uint32_t r2 = K[b] == key ? V[b] : kEmptyVal;
     return r1 & r2;
 }
 
 // Packed tables: the same probe with miss = 0 (empty slots are {~0, 0}); x = the key's hash
 __device__ __forceinline__ uint32_t probe_px(const QView& v, uint32_t off, int lg, uint32_t key, uint32_t x) {
-    const uint2 e1 = v.tab[off + cuckoo_h1(x, lg)];
-    const uint2 e2 = v.tab[off + cuckoo_h2(x, lg)];
-    return (e1.x == key ? e1.y : 0u) | (e2.x == key ? e2.y : 0u);
+    const uint32_t* K = v.tab + 2u * off;
+    const uint32_t* V = K + (1u << lg);
+    const uint32_t a = cuckoo_h1(x, lg), b = cuckoo_h2(x, lg);
+    return (K[a] == key ? V[a] : 0u) | (K[b] == key ? V[b] : 0u);
 }
 // the record table T
 __device__ __forceinline__ uint32_t probe_p(const QView& v, uint32_t key) {

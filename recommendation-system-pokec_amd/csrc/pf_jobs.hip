@@ -626,9 +626,23 @@ __global__ __launch_bounds__(kJobThreads) void qimage_kernel(DevStore st, DevJob
         __syncthreads();
         if (!failed) {
             if (tid == 0) q->hmul = hmul;
-            if constexpr (LDS) {
-                uint64_t* out = reinterpret_cast<uint64_t*>(pool + I.keys_off);
-                for (uint32_t i = tid; i < tab_total; i += kJobThreads) out[i] = tab[i];
+            // out SoA per table (pf_types.h soa_words); a global build goes through the scratch
+            // after its item list (the table's own bytes are the destination)
+            uint32_t* out = reinterpret_cast<uint32_t*>(pool + I.keys_off);
+            const uint64_t* src = tab;
+            if constexpr (!LDS) {
+                uint64_t* tmp = items + nset + ntok;
+                for (uint32_t i = tid; i < tab_total; i += kJobThreads) tmp[i] = tab[i];
+                __syncthreads();
+                src = tmp;
+            }
+            const uint32_t excl = ntab << lg;
+            for (uint32_t i = tid; i < tab_total; i += kJobThreads) {
+                uint32_t kw, vw;
+                soa_words(i, excl, lg, I.lge, kw, vw);
+                const uint64_t e = src[i];
+                out[kw] = (uint32_t)e;
+                out[vw] = (uint32_t)(e >> 32);
             }
             return;
         }

@@ -142,7 +142,9 @@ int build_resident_images(pf_ctx* c) {
                 if (cls[x] == k) {
                     ImgJob m = ij[x];
                     m.scr_off = scr;
-                    if (k == 2) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[m.idx] + ntok_of(m.idx));
+                    if (k == 2)  // set + u64 items + the table's u64 copy (the SoA transform)
+                        scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[m.idx] + ntok_of(m.idx)) +
+                               2 * (((int64_t)(c->hs.packed ? 1 : 3) << m.lg) + ((int64_t)1 << m.lge));
                     ord.push_back(m);
                     ++nc[k];
                 }
@@ -833,7 +835,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             ipool = a16z(m.vals_off + (size_t)ntok * sizeof(QVal));
             if (ipool >= (size_t)UINT32_MAX) return c->fail(PF_EUNSUPP, "query images of one batch exceed 4 GB");
             m.scr_off = scr;
-            if ((int)k >= n_lds) scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok);  // set + u64 items
+            if ((int)k >= n_lds)  // set + u64 items + the table's u64 copy (the SoA transform)
+                scr += ((int64_t)1 << m.dlg) + 2 * ((int64_t)J.img_nset[idx] + ntok) + 2 * (int64_t)nkeys;
         }
         const size_t kv = nkeys * 8 + (size_t)ntok * sizeof(QVal);
         r.lds_bytes = kv <= kStageLimitJobs ? (uint32_t)kv : 0u;

@@ -401,9 +401,10 @@ struct RowWalk {
 };
 
 __device__ __forceinline__ bool has_key(const QView& v, uint32_t key, uint32_t x) {
-    const uint32_t k1 = v.tab[cuckoo_h1(x, v.lg)].x;
+    // the table's keys (SoA: the packed table T is at entry offset 0, its keys in words [0, 2^lg))
+    const uint32_t k1 = v.tab[cuckoo_h1(x, v.lg)];
     // cuckoo_h2 as one bit-field extract (the compiler emits a shift and a mask)
-    const uint32_t k2 = v.tab[__builtin_amdgcn_ubfe(x, 32u - 2u * (uint32_t)v.lg, (uint32_t)v.lg)].x;
+    const uint32_t k2 = v.tab[__builtin_amdgcn_ubfe(x, 32u - 2u * (uint32_t)v.lg, (uint32_t)v.lg)];
     return (k1 == key) | (k2 == key);
 }
 
@@ -805,11 +806,11 @@ __device__ __forceinline__ QView stage_query(char* smem, const uint8_t* pool, co
     const uint32_t kb = 8u * (v.excl_off + (1u << v.lge)), vb = uni((uint32_t)q->n_vals) * 16u;
     char* p = smem + sizeof(QConst);
     if constexpr (!GTAB) {
-        v.tab = reinterpret_cast<const uint2*>(p);
+        v.tab = reinterpret_cast<const uint32_t*>(p);
         v.vals = reinterpret_cast<const QVal*>(p + kb);
         p += kb + vb;
     } else {
-        v.tab = reinterpret_cast<const uint2*>(pool + (size_t)r.const_off * 16u + r.keys_off);
+        v.tab = reinterpret_cast<const uint32_t*>(pool + (size_t)r.const_off * 16u + r.keys_off);
         v.vals = reinterpret_cast<const QVal*>(pool + (size_t)r.const_off * 16u + r.vals_off);
     }
     v.hits = p;
@@ -1417,6 +1418,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             }
         }
         // 2. clubs / friends
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 64)
+        if (false)  // experiment: no set lists
+#endif
         walk_sets(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e) {
             const uint32_t p = (e >> 8) - c0;
             if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
@@ -1425,6 +1429,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         __syncthreads();
         K5T(1);
         // 3. fixed terms, recommender_similarity.cpp:38-91
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 128)
+#define PF_K5_NOFIXED 1  // experiment: no fixed terms
+#endif
         double sum[kCandsPerThread];
         uint32_t used = 0;  // byte kk: terms used by candidate kk (<= 7 + 48)
         uint64_t pend[kCandsPerThread];
@@ -1438,6 +1445,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             pend[kk] = cm & q.colmask;
             double s = 0.0;
             int u = 0;
+#ifndef PF_K5_NOFIXED
             const uint32_t pb = (ha[kk].y >> 16) & 0xFFu, gb = ha[kk].y >> 24;
             if (q.pubcode != kCodeMissing && pb != kCodeMissing) { s += q.sig_pub[pb == q.pubcode]; ++u; }
             if (q.gencode != kCodeMissing && gb != kCodeMissing) { s += q.sig_gen[gb == q.gencode]; ++u; }
@@ -1455,6 +1463,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             const int ic = (int)(ct & 0xFFFFu), ifr = (int)(ct >> 16);
             if (q.n_clubs > 0 && nc > 0) { s += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs); ++u; }
             if (q.n_friends > 0 && nf > 0) { s += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends); ++u; }
+#endif
             sum[kk] = s;
             used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
         }
@@ -1465,6 +1474,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
         int ci = 0, jcur = 0, rnd = 0;
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 32)
+        ci = H.n_act;  // experiment: no text rounds
+#endif
         while (ci < H.n_act) {
             const Round R = next_round(scol, gpre, H.n_act, ci, jcur);
             const int mbuf = rnd++ & 1;  // this round's list map buffer
@@ -1740,6 +1752,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         K5T(12);
         if (mode & 1u) {
             // misc[0] was last read before this block's first barrier
+            // claimed here, not at the block's start: an early claim measured 190 -> 200 us (r4i;
+            // a workgroup holding its next block while the last ones are handed out)
             if (tid == 0) misc[0] = (uint32_t)(blk_begin + nbx) + atomicAdd(next_blk, 1u);
             __syncthreads();
             blk = (int)misc[0];

@@ -600,6 +600,15 @@ bool build_query(const HostCorpus& hc, bool packed, int32_t i, const std::vector
                 c.lg_excl = lge;
                 c.hmul = hmul;
                 c.excl_off = (uint32_t)eoff;
+                // SoA per table (pf_types.h soa_words), in the same bytes
+                const std::vector<uint64_t> aos(out.keys);
+                uint32_t* w = reinterpret_cast<uint32_t*>(out.keys.data());
+                for (size_t i = 0; i < aos.size(); ++i) {
+                    uint32_t kw, vw;
+                    soa_words((uint32_t)i, (uint32_t)eoff, lg, lge, kw, vw);
+                    w[kw] = (uint32_t)aos[i];
+                    w[vw] = (uint32_t)(aos[i] >> 32);
+                }
                 return true;
             }
         }

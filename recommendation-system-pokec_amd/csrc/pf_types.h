@@ -86,6 +86,17 @@ __host__ __device__ inline uint32_t cuckoo_x(uint32_t key, uint32_t hmul) { retu
 __host__ __device__ inline uint32_t cuckoo_h1(uint32_t x, int lg) { return x >> (32 - lg); }
 __host__ __device__ inline uint32_t cuckoo_h2(uint32_t x, int lg) { return (x >> (32 - 2 * lg)) & ((1u << lg) - 1u); }
 __host__ __device__ inline uint64_t make_entry(uint32_t key, uint32_t val) { return ((uint64_t)val << 32) | key; }
+// Query tables are built as 8-B {key, val} entries and stored SoA per table: the table of 2^lg
+// entries at entry offset off keeps its keys in words [2 off, 2 off + 2^lg) and its values in the
+// next 2^lg words (the same bytes), so a wave's random key probes (ds_read_b32) spread over all 32
+// banks instead of the even ones.  Word positions of entry i of the image's tables (ntab tables of
+// 2^lg, then the exclusion table of 2^lge at excl = ntab << lg):
+__host__ __device__ inline void soa_words(uint32_t i, uint32_t excl, int lg, int lge, uint32_t& kw, uint32_t& vw) {
+    const bool ex = i >= excl;
+    const uint32_t off = ex ? excl : (i >> lg) << lg, sz = ex ? (1u << lge) : (1u << lg);
+    kw = 2u * off + (i - off);
+    vw = kw + sz;
+}
 
 // Per-query constants (A side of profile_similarity).  Built on the host with
 // glibc exp so every table entry is bit-identical to the reference.

@@ -29,6 +29,9 @@ for S in "$@"; do
         timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 2 ;;
     prof)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/prof.json 2> $O/prof.err || exit 3 ;;
+    prof5)
+        # kernel trace of cfg 5 at one context (host-side gaps between the device stages)
+        timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/prof_cfg5 -o run -- python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/prof5.json 2> $O/prof5.err || exit 3 ;;
     cfg[2345])
         timeout -k 10 900 python3 bench.py --workload $S > $O/$S.json 2> $O/$S.err || exit 4 ;;
     quick)
@@ -47,6 +50,10 @@ for S in "$@"; do
         # cfg 5 over EVERY eligible user of the 1.63M corpus (both drivers), prefix-checked
         timeout -k 10 1000 python3 -u tools/eval_holdout.py --cfg5-corpus 1632803 --whole --check-prefix 64 \
             --out $O/whole5.json > $O/whole5.log 2>&1 || exit 10 ;;
+    quicke:*)
+        # cfg 2 quick line under a PF_DEBUG setting
+        E=${S#quicke:}
+        timeout -k 10 300 env PF_DEBUG=$E python3 bench.py --steps 100 --warmup 10 $Q > $O/quicke_${E//[=,]/_}.json 2> $O/quicke.err || exit 5 ;;
     quick4e:*)
         # cfg 4 quick line under a PF_DEBUG setting, e.g. quick4e:k5_query_major=1
         E=${S#quick4e:}

@@ -696,6 +696,10 @@ void pf_close(pf_ctx* c) {
         (void)hipStreamSynchronize(c->jb.aux);
         (void)hipStreamDestroy(c->jb.aux);
     }
+    if (c->jb.aux2) {
+        (void)hipStreamSynchronize(c->jb.aux2);
+        (void)hipStreamDestroy(c->jb.aux2);
+    }
     if (c->jb.ev_fork) (void)hipEventDestroy(c->jb.ev_fork);
     if (c->jb.ev_join) (void)hipEventDestroy(c->jb.ev_join);
     if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -679,7 +679,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(kPairSpan, count - x),
                                        (int32_t)(out + x)});
     };
-    std::vector<int32_t> jix_collab, jix_clubs, jix_topk, jix_fused;
+    std::vector<int32_t> jix_collab, jix_clubs, jix_topk, jix_fused, jix_ctopk;
     int max_cap_collab = 0, ktop = 1;
     const int lge = lg_for(0);
     auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
@@ -768,15 +768,22 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             }
         }
         if (p.kind != kDjRawGraph && p.kind != kDjRawCollab && jobs[i].topk <= kDevTopK) {
-            // a collaborative job with candidates gets its top-k inside K4' (collab_kernel)
-            (p.kind == kDjCollab && p.cap > 0 ? jix_fused : jix_topk).push_back(jn);
+            // a collaborative job with candidates gets its top-k inside K4' (collab_kernel); the
+            // clubs jobs' K8 runs after K7 on the second aux stream (jix_ctopk, appended below)
+            (p.kind == kDjCollab && p.cap > 0 ? jix_fused : (p.kind == kDjClubs ? jix_ctopk : jix_topk)).push_back(jn);
             ktop = std::max(ktop, jobs[i].topk);
         }
         dj.push_back(d);
         jmap.push_back((int32_t)i);
     }
     if (dj.empty()) return PF_OK;
-    if (W.done == nullptr) HIPCHK(c, hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+    const int n_topk_main = (int)jix_topk.size();  // K8 on the context's stream; the clubs jobs' after them
+    jix_topk.insert(jix_topk.end(), jix_ctopk.begin(), jix_ctopk.end());
+    if (W.done == nullptr) {
+        HIPCHK(c, hipEventCreateWithFlags(&W.done, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&W.ev_pairs, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&W.ev_main, hipEventDisableTiming));
+    }
     const hipStream_t s = c->stream;
     if (E >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
     // ---- images (pf_api.cpp plan_images layout).  Resident (J.pimg, built at open): every
@@ -902,6 +909,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.d_plan.reserve(o_ord + std::max<size_t>(blocks.size(), 1) * 4));
     if (J.aux == nullptr) {
         HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
+        HIPCHK(c, hipStreamCreateWithFlags(&J.aux2, hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming));
     }
@@ -997,15 +1005,26 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
+    // K7 (clubs, one latency-bound wave per job) and its jobs' K8 go to the second aux stream once
+    // the pairs are scored, beside K4' and the next chunk's gathers and pair kernel (r4k trace: K7
+    // ran 0.8-1.4 ms per cfg-5 chunk between two pair kernels with the device mostly idle); the
+    // chunk's result copies follow there after the context stream's K4' / K8 (W.ev_main), and
+    // W.done is recorded last on that stream.  Jobs write disjoint regions of the slot's buffers.
+    const hipStream_t s2 = J.aux2;
+    HIPCHK(c, hipEventRecord(W.ev_pairs, s));
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
                             W.d_slots.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(), W.d_parts.as<uint64_t>(),
                             d_tk, d_keys, ktop, s));
+    HIPCHK(c, launch_job_topk(d_dj, d_jt, n_topk_main, W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
+                              W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, s));
+    HIPCHK(c, hipEventRecord(W.ev_main, s));
+    HIPCHK(c, hipStreamWaitEvent(s2, W.ev_pairs, 0));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
                            W.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                           d_ncand, (int64_t)J.js.n_club_ids, s));
-    HIPCHK(c, launch_job_topk(d_dj, d_jt, (int)jix_topk.size(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                              W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop,
-                              s));
+                           d_ncand, (int64_t)J.js.n_club_ids, s2));
+    HIPCHK(c, launch_job_topk(d_dj, d_jt + n_topk_main, (int)jix_topk.size() - n_topk_main, W.d_fl.as<float>(),
+                              W.d_ids.as<int32_t>(), W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, s2));
+    HIPCHK(c, hipStreamWaitEvent(s2, W.ev_main, 0));
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
     for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;
@@ -1022,17 +1041,17 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     HIPCHK(c, W.h_out.ensure(ob));
     uint8_t* ho = W.h_out.as<uint8_t>();
     const size_t o_fail = 0, o_cnt = o_rcnt - o_res, o_keys = o_rkeys - o_res;
-    HIPCHK(c, hipMemcpyAsync(ho, d + o_res, res_b, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(ho, d + o_res, res_b, hipMemcpyDeviceToHost, s2));
     for (size_t q = 0; q < full.size(); ++q) {
         const DevJob& x = dj[full[q]];
         const size_t cnt = (size_t)std::max(x.cap, x.kind == kDjClubs ? J.js.n_club_ids : 0);
         uint8_t* dst = ho + full_off[q];
-        HIPCHK(c, hipMemcpyAsync(dst, W.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, W.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(dst, W.d_fl.as<float>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s2));
+        HIPCHK(c, hipMemcpyAsync(dst + cnt * 4, W.d_ids.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost, s2));
         HIPCHK(c, hipMemcpyAsync(dst + cnt * 8, W.d_slots.as<int32_t>() + x.out_off, cnt * 4, hipMemcpyDeviceToHost,
-                                 s));
+                                 s2));
     }
-    HIPCHK(c, hipEventRecord(W.done, s));
+    HIPCHK(c, hipEventRecord(W.done, s2));
     hl.lap(kHpStage2);  // launches issued
     W.active = true;
     W.o_cnt = o_cnt;
@@ -1126,7 +1145,10 @@ int finish_pending(pf_ctx* c) {
             p.oc[i] = n;
         }
     J.pending.pop_front();
-    if (rc != PF_OK) (void)hipStreamSynchronize(c->stream);
+    if (rc != PF_OK) {
+        (void)hipStreamSynchronize(c->stream);
+        if (J.aux2) (void)hipStreamSynchronize(J.aux2);
+    }
     return rc;
 }
 
@@ -1175,6 +1197,7 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     JobsState::Ws* pending = nullptr;
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
         (void)hipStreamSynchronize(c->stream);
+        if (J.aux2) (void)hipStreamSynchronize(J.aux2);
         for (auto& w : J.ws) w.active = false;
         return code;
     };
@@ -1281,6 +1304,7 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
     rc = launch_chunk(c, pd.jobs, P, 0, n, J.ws[slot]);
     if (rc != PF_OK) {
         (void)hipStreamSynchronize(c->stream);
+        if (J.aux2) (void)hipStreamSynchronize(J.aux2);
         J.ws[slot].active = false;
         return rc;
     }

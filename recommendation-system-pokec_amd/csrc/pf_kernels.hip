@@ -1317,7 +1317,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
     PList* pl = reinterpret_cast<PList*>(pt + H.n_tok);
     uint2* rng = reinterpret_cast<uint2*>(pl + nl);
-    uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + nl);
+    uint2* rtab = rng + nl;  // the block's rounds (ja | jb << 16, ca | ce << 16), <= n_tok of them
+    uint32_t* gpre = reinterpret_cast<uint32_t*>(rtab + H.n_tok + 1);
     uint8_t* colof = reinterpret_cast<uint8_t*>(gpre + H.n_tok + 1);  // token -> active column index
     uint64_t* mapb = reinterpret_cast<uint64_t*>(base + kLdsMapB);
     uint2* mapn = reinterpret_cast<uint2*>(base + kLdsMapN);
@@ -1356,6 +1357,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // or (mode bit 0) the next unclaimed block of the query from a counter in its ScanSync, so the
     // blocks past the first resident round go to the workgroups that finish first.
     unsigned int* next_blk = &sync[qy].next;
+    // dynamic mode (one query): whole static rounds of nbx blocks, then the tail blocks by claim
+    const int tail = (mode & 1u) ? blk_begin + max(1, (blk_end - blk_begin) / nbx) * nbx : blk_end;
     for (int blk = blk_begin + bx; blk < blk_end;) {
         const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
@@ -1388,14 +1391,19 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         K5T(1);
         if (tid < 64) {  // read after the barrier below
             wave_prefix(gpre, rng, H.n_tok, lane);
-#ifndef PF_K5_BISECT
             wave_sync();
-            if (H.n_act > 0) {
-                int ci0 = 0, j0 = 0;
-                const Round R0 = next_round(scol, gpre, H.n_act, ci0, j0);
-                build_map(mapb, mapc, mapn, gpre, rng, R0.ja, R0.jb, lane);
+            // the block's rounds, once (every thread used to walk the columns' prefix chain per round)
+            {
+                int ci0 = 0, j0 = 0, nr = 0;
+                while (ci0 < H.n_act) {
+                    const Round Rr = next_round(scol, gpre, H.n_act, ci0, j0);
+                    if (lane == 0)
+                        rtab[nr] = make_uint2((uint32_t)Rr.ja | (uint32_t)Rr.jb << 16, (uint32_t)Rr.ca | (uint32_t)Rr.ce << 16);
+                    if (nr == 0) build_map(mapb, mapc, mapn, gpre, rng, Rr.ja, Rr.jb, lane);
+                    ++nr;
+                }
+                if (lane == 0) misc[3] = (uint32_t)nr;
             }
-#endif
         }
         // exclusion list (sorted idx of adj[q] + {q}): whole list when short (loaded above, no
         // barrier of its own), else bisect and walk until past the block
@@ -1473,13 +1481,18 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         uint32_t chit = 0;                                     // bit kk: the split column has a hit
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
-        int ci = 0, jcur = 0, rnd = 0;
+        int nrounds = (int)misc[3];  // written before the barrier above
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 32)
-        ci = H.n_act;  // experiment: no text rounds
+        nrounds = 0;  // experiment: no text rounds
 #endif
-        while (ci < H.n_act) {
-            const Round R = next_round(scol, gpre, H.n_act, ci, jcur);
-            const int mbuf = rnd++ & 1;  // this round's list map buffer
+        for (int rnd = 0; rnd < nrounds; ++rnd) {
+            const uint2 rr = rtab[rnd];
+            Round R;
+            R.ja = (int)(rr.x & 0xFFFFu);
+            R.jb = (int)(rr.x >> 16);
+            R.ca = (int)(rr.y & 0xFFFFu);
+            R.ce = (int)(rr.y >> 16);
+            const int mbuf = rnd & 1;  // this round's list map buffer
             const int ja = R.ja, jb = R.jb;
             const uint32_t g0 = gpre[ja], F = gpre[jb] - g0;  // the round's flat entries
             if (F > 0) {
@@ -1505,7 +1518,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 8)
                         js[u] = f < F ? ja : -1;  // experiment: no list lookup (wrong entries, in range)
                         xs[u] = js[u] >= 0 ? min(rng[js[u]].x + (g0 + f - gpre[js[u]]), ps.n_tok_entries - 1) : 0u;
-#elif !defined(PF_K5_BISECT)
+#else
                         // the list map: nonempty lists starting at or before f, minus one
                         js[u] = -1;
                         xs[u] = 0u;  // a valid address
@@ -1517,9 +1530,6 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                             js[u] = ja + (int)L.y;
                             xs[u] = L.x + f;
                         }
-#else
-                        js[u] = f < F ? round_list(gpre, ja, jb, g0 + f) : -1;
-                        xs[u] = js[u] >= 0 ? rng[js[u]].x + (g0 + f - gpre[js[u]]) : 0u;  // 0: a valid address
 #endif
                     }
                     uint32_t ent[U];
@@ -1547,15 +1557,12 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 K5T(4);
                 __syncthreads();
                 K5T(5);
-#ifndef PF_K5_BISECT
-                if (tid < 64 && ci < H.n_act) {  // the next round's list map (published by the slots barrier)
-                    int ci1 = ci, j1 = jcur;
-                    const Round R1 = next_round(scol, gpre, H.n_act, ci1, j1);
+                if (tid < 64 && rnd + 1 < nrounds) {  // the next round's list map (published by the slots barrier)
+                    const uint2 r1 = rtab[rnd + 1];
                     const int nb = mbuf ^ 1;
-                    build_map(mapb + nb * kMapWords, mapc + nb * kMapWords, mapn + nb * kRoundToks, gpre, rng, R1.ja,
-                              R1.jb, lane);
+                    build_map(mapb + nb * kMapWords, mapc + nb * kMapWords, mapn + nb * kRoundToks, gpre, rng,
+                              (int)(r1.x & 0xFFFFu), (int)(r1.x >> 16), lane);
                 }
-#endif
                 // b. hit slots: the wave's candidates' hits in one contiguous range
                 uint32_t nk[kCandsPerThread], tot = 0;
 #pragma unroll
@@ -1710,18 +1717,15 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 if (F > 0) mask[p] = 0ull;
             }
             K5T(10);
-#ifndef PF_K5_BISECT
-            if (F == 0 && ci < H.n_act) {  // an empty round built no list map for the next one
+            if (F == 0 && rnd + 1 < nrounds) {  // an empty round built no list map for the next one
                 if (tid < 64) {
-                    int ci1 = ci, j1 = jcur;
-                    const Round R1 = next_round(scol, gpre, H.n_act, ci1, j1);
+                    const uint2 r1 = rtab[rnd + 1];
                     const int nb = mbuf ^ 1;
                     build_map(mapb + nb * kMapWords, mapc + nb * kMapWords, mapn + nb * kRoundToks, gpre, rng,
-                              R1.ja, R1.jb, lane);
+                              (int)(r1.x & 0xFFFFu), (int)(r1.x >> 16), lane);
                 }
                 __syncthreads();
             }
-#endif
             if (F > 0) __syncthreads();  // the next round rewrites the masks, slots and segments
         }
         K5T(11);
@@ -1750,11 +1754,12 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         K5T(12);
-        if (mode & 1u) {
-            // misc[0] was last read before this block's first barrier
-            // claimed here, not at the block's start: an early claim measured 190 -> 200 us (r4i;
-            // a workgroup holding its next block while the last ones are handed out)
-            if (tid == 0) misc[0] = (uint32_t)(blk_begin + nbx) + atomicAdd(next_blk, 1u);
+        if ((mode & 1u) && blk + nbx >= tail) {
+            // the tail past the static rounds from the query's counter: one claim per workgroup
+            // (every workgroup claiming every block serialised ~3,000 atomics on one address).
+            // misc[0] was last read before this block's first barrier; claimed here, not at the
+            // block's start: an early claim measured 190 -> 200 us (r4i)
+            if (tid == 0) misc[0] = (uint32_t)tail + atomicAdd(next_blk, 1u);
             __syncthreads();
             blk = (int)misc[0];
         } else {
@@ -1906,7 +1911,8 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 // K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | PList[n_lists] | ranges[n_lists] |
 // prefix[n_tok + 1] | token -> column u8[n_tok]
 uint32_t post_var_lds(int n_tok, int n_lists) {
-    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 4 * (n_tok + 1) + n_tok + 15) & ~15u;
+    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 8 * (n_tok + 1) + 4 * (n_tok + 1) + n_tok +
+                      15) & ~15u;
 }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 

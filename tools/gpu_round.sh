@@ -68,14 +68,22 @@ for S in "$@"; do
         # rehearse:N[:W]  bench.py's N > 1 path with N gloo ranks on this one GPU (tools/rehearse_multi.sh)
         R=${S#rehearse:}; N=${R%%:*}; W=cfg4; [[ $R == *:* ]] && W=${R#*:}
         bash tools/rehearse_multi.sh $TAG $N $W || exit 11 ;;
+    cfg5v:*)
+        # cfg5v:V  cfg 5 at one context with the variant library exp/v/V
+        V=${S#cfg5v:}
+        timeout -k 10 900 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5v_$V.json 2> $O/cfg5v_$V.err || exit 4 ;;
     cfg5e:*)
         # cfg5e:SETTINGS  cfg 5 at one context under PF_DEBUG=SETTINGS (e.g. chunks=6)
         E=${S#cfg5e:}
         timeout -k 10 900 env PF_DEBUG=$E python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5e_${E//[=,]/_}.json 2> $O/cfg5e_${E//[=,]/_}.err || exit 4 ;;
-    cfg5c1)
-        timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5c1.json 2> $O/cfg5c1.err || exit 4 ;;
-    k5t)
-        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/k5t/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/k5t.json 2> $O/k5t.err || exit 7 ;;
+    cfg5c1|cfg5c1:*)
+        # cfg 5 at one context with the host stage clocks; cfg5c1:K runs K timed steps (default 5)
+        K=5; [[ $S == cfg5c1:* ]] && K=${S#cfg5c1:}
+        timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps $K --warmup 2 $Q > $O/cfg5c1_$K.json 2> $O/cfg5c1_$K.err || exit 4 ;;
+    k5t|k5t:*)
+        # profiling build (K5T=1) per-phase K5 clocks; k5t:V uses exp/v/V
+        V=k5t; [[ $S == k5t:* ]] && V=${S#k5t:}
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/$V.json 2> $O/$V.err || exit 7 ;;
     pmcv:*)
         # pmcv:V:C1,C2..  one counter pass over 20 cfg-2 steps with the variant library exp/v/V (K5 rows only)
         R=${S#pmcv:}; V=${R%%:*}; C=${R#*:}

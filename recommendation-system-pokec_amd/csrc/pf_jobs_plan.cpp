@@ -1191,8 +1191,29 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     // is planned and launched while chunk i runs on the device, then chunk i is unpacked.
     // Only large calls are cut: splitting a 64-user cfg-3 step into four chunks made it slower
     // (1.09 -> 1.50 ms: four times the launches, each too small to fill the GPU; r2n).
-    static const size_t nchunks = (size_t)std::max(1L, debug_long("chunks", 3));  // PF_DEBUG chunks=N (A/B)
-    const size_t chunk_jobs = n < kPipeJobs ? n : std::max<size_t>(kPipeJobs / 2, (n + nchunks - 1) / nchunks);
+    // Chunk sizes by weight (PF_DEBUG chunk_plan=w1:w2:..., A/B): the first chunk's planning and
+    // the last chunk's unpacking are the host work no device stage hides
+    static const std::vector<int> weights = [] {
+        std::vector<int> w;
+        const char* v = debug_str("chunk_plan");
+        std::string str = v ? v : "1:1:1";
+        for (size_t p = 0; p < str.size();) {
+            size_t q = str.find(':', p);
+            if (q == std::string::npos) q = str.size();
+            w.push_back(std::max(1, std::atoi(str.substr(p, q - p).c_str())));
+            p = q + 1;
+        }
+        return w;
+    }();
+    int wsum = 0;
+    for (int w : weights) wsum += w;
+    size_t ck = 0;  // chunks cut so far
+    auto chunk_end = [&](size_t b) {
+        if (n < kPipeJobs) return n;
+        const size_t w = (size_t)weights[std::min(ck, weights.size() - 1)];
+        const size_t len = std::max<size_t>(kPipeJobs / 4, (n * w + wsum - 1) / wsum);
+        return std::min(n, b + len);
+    };
     int slot = 0;
     JobsState::Ws* pending = nullptr;
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
@@ -1201,14 +1222,15 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         for (auto& w : J.ws) w.active = false;
         return code;
     };
+    // 1-hop planning of every job first, on the worker pool (a few microseconds per job; threads
+    // only for large calls: spawning them costs more than planning a 64-user step): the first
+    // chunk's launch then waits for its layout only, not for the planning of all its jobs
+    par_jobs(n, [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 256);
+    hl.lap(kHpPrep);
     size_t b = 0;
     while (b < n) {
-        const size_t lim = std::min(n, b + chunk_jobs);
-        // 1-hop planning is a few microseconds per job: threads only for large chunks
-        // (spawning them costs more than planning a 64-user step)
-        par_jobs(lim - b, [&](size_t i) { if (P[b + i].u < 0 && P[b + i].kind < 0) plan_job(c, jobs[b + i], P[b + i], raw); },
-                 256);
-        hl.lap(kHpPrep);
+        const size_t lim = chunk_end(b);
+        ++ck;
         for (size_t i = b; i < lim; ++i)
             if (P[i].unmapped) return drain(c->fail(PF_EINTERNAL, "adjacency row names an unmapped uid"));
         size_t e = b;

@@ -1359,22 +1359,34 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     unsigned int* next_blk = &sync[qy].next;
     // dynamic mode (one query): whole static rounds of nbx blocks, then the tail blocks by claim
     const int tail = (mode & 1u) ? blk_begin + max(1, (blk_end - blk_begin) / nbx) * nbx : blk_end;
+    const uint32_t B = (uint32_t)ps.bsize;
+    const bool short_excl = H.n_excl <= kPostThreads;
+    const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;  // the query's, once
+    // the next static block's headers and first list ranges, loaded before this block's FAS (their
+    // round trip hidden behind the FAS, the top-k and the block barrier)
+    uint4 pha[kCandsPerThread], phb[kCandsPerThread];
+    uint2 prng = make_uint2(0u, 0u);
+    bool have_pf = false;
     for (int blk = blk_begin + bx; blk < blk_end;) {
-        const uint32_t B = (uint32_t)ps.bsize;
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
         // 1. headers of the owned candidates, every list's range in this block and (short list) the
         // exclusions: all loads issued before the first wait, one memory round trip
         uint4 ha[kCandsPerThread], hb[kCandsPerThread];
+        if (have_pf) {
 #pragma unroll
-        for (int kk = 0; kk < kCandsPerThread; ++kk) {  // clamped (always valid) index, zeroed below
-            const uint32_t c = min(c0 + kk * kPostThreads + tid, c1);
-            ha[kk] = ps.hdr[2 * (size_t)c];
-            hb[kk] = ps.hdr[2 * (size_t)c + 1];
+            for (int kk = 0; kk < kCandsPerThread; ++kk) { ha[kk] = pha[kk]; hb[kk] = phb[kk]; }
+            if (tid < nl) rng[tid] = prng;
+            for (int j = tid + kPostThreads; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < kCandsPerThread; ++kk) {  // clamped (always valid) index, zeroed below
+                const uint32_t c = min(c0 + kk * kPostThreads + tid, c1);
+                ha[kk] = ps.hdr[2 * (size_t)c];
+                hb[kk] = ps.hdr[2 * (size_t)c + 1];
+            }
+            for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
         }
-        const bool short_excl = H.n_excl <= kPostThreads;
-        const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;
-        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
@@ -1729,6 +1741,21 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             if (F > 0) __syncthreads();  // the next round rewrites the masks, slots and segments
         }
         K5T(11);
+        // the next block when it is static: its headers and first list ranges now
+        {
+            const int nxt = blk + nbx;
+            have_pf = nxt < tail;
+            if (have_pf) {
+                const uint32_t n0 = (uint32_t)nxt * B, n1 = min(n0 + B, (uint32_t)ps.n) - 1;
+#pragma unroll
+                for (int kk = 0; kk < kCandsPerThread; ++kk) {
+                    const uint32_t c = min(n0 + kk * kPostThreads + tid, n1);
+                    pha[kk] = ps.hdr[2 * (size_t)c];
+                    phb[kk] = ps.hdr[2 * (size_t)c + 1];
+                }
+                if (tid < nl) prng = list_range(ps, pl[tid], n0, n1);
+            }
+        }
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
         uint64_t keys[kCandsPerThread];
 #pragma unroll
@@ -1781,6 +1808,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     }
     // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
     uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
+#if defined(PF_K5_EXP) && (PF_K5_EXP & 512)
+    if (lane < k) parts[((size_t)qy * nbx + bx) * k + lane] = best;  // experiment: no cross-block merge
+    return;
+#endif
     scan_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
 }
 

@@ -14,9 +14,11 @@ generator tools/pokec_synth.cpp, resident in HBM), interest FAS top-10 over ever
 --workload cfg2|cfg4 overrides the default (cfg2 at N > 1: N queries per step, one per GPU,
 weak scaling).  value = candidates scored / s over the whole job.
 --workload cfg3 (configs[2]): collaborative FoF top-10, 64 query users per step; value = pair-FAS/s;
-three engine contexts per GPU by default, steps dealt round-robin to their host threads.
+one engine context, three asynchronous calls in flight (--contexts C: C contexts per GPU, steps
+dealt round-robin to their host threads).
 --workload cfg5 (configs[4]): the hold-out evaluation (recommendation_tests.cpp: interest + collab
-+ clubs) of 2048 users per step, users split over the ranks; value = hold-out users/s.
++ clubs) of 2048 users per step, users split over the ranks, one engine context per GPU by
+default; value = hold-out users/s.
 
 Roofline of the dominant kernel (fas_post_kernel, the postings scan, by default;
 fas_scan_kernel, the record-stream scan, with --scan-kernel stream), HIP events around every
@@ -767,9 +769,9 @@ def main():
                          "users per step, users split over the ranks")
     ap.add_argument("--contexts", type=int, default=None,
                     help="cfg3 / cfg5: engine contexts per GPU, each a full replica driven by its own host "
-                         "thread; default 1 for cfg3 (asynchronous calls overlap the host planning; round 2 needed "
-                         "three contexts for that: r2s 1 -> 1.1e9, 2 -> 1.7-1.8e9, 3 -> 2.0-2.15e9 pair-FAS/s) and "
-                         "3 for cfg5 (r2fk: 1 -> 39.7k, 2 -> 51.5k, 3 -> 61.7k users/s)")
+                         "thread; default 1 (cfg3: the asynchronous calls overlap the host planning; cfg5: one "
+                         "context 99.6k-113.4k users/s against 99.0k-121.2k with three on the round-4 boxes, "
+                         "DESIGN.md section 5)")
     ap.add_argument("--sync-calls", action="store_true",
                     help="cfg3: the synchronous recommender calls instead of the asynchronous ones")
     ap.add_argument("--async-depth", type=int, default=ASYNC_DEPTH,
@@ -801,7 +803,7 @@ def main():
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
     if args.contexts is None:
-        args.contexts = {"cfg5": 3}.get(args.workload, 1)
+        args.contexts = 1
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local)
     import synth

@@ -356,7 +356,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
     HIPCHK(c, c->stage_release(s));
     uint8_t* base = c->d_pool.as<uint8_t>();
-    HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
+    HIPCHK(c, c->d_part.ensure((size_t)nq * (blocks + 8) * k * sizeof(uint64_t)));  // + 8 group lists (post_tail)
     hipEvent_t e0, e1;
     int rc = scan_events(c, timed, e0, e1);
     if (rc != PF_OK) return rc;
@@ -369,7 +369,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         while (q1 < nq && pcu[order[q1]] == pcu[order[q0]]) vmax = std::max(vmax, vl[order[q1++]]);
         HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
                                   nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
-                                  c->d_part.as<uint64_t>() + (size_t)q0 * blocks * k,
+                                  c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
                                   reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
                                   reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
                                   (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
@@ -423,7 +423,7 @@ int scan_stream(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<in
     const int32_t* d_rows = reinterpret_cast<const int32_t*>(base + refs_b);
     pf::ScanSync* d_sync = reinterpret_cast<pf::ScanSync*>(base + refs_b + rows_b);
     const uint8_t* d_images = base + refs_b + rows_b + sync_b;
-    HIPCHK(c, c->d_part.ensure((size_t)nq * blocks * k * sizeof(uint64_t)));
+    HIPCHK(c, c->d_part.ensure((size_t)nq * (blocks + 8) * k * sizeof(uint64_t)));  // + 8 group lists (post_tail)
     hipEvent_t e0, e1;
     int rc = scan_events(c, timed, e0, e1);
     if (rc != PF_OK) return rc;

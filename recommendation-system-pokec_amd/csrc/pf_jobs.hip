@@ -666,7 +666,7 @@ uint32_t qimage_lds(int lg, int lge, int dlg, uint32_t nitems, bool packed) {
 // candidate in position order.  A hub's long friend row costs one memory round trip per 64
 // positions over four waves instead of one per few positions on a single lane.
 // A job with topk <= kMaxTopK also gets its top-k here (K8's keys, K8 skips the job): each block
-// publishes the k best keys of its 64 candidates (write-through stores, scan_tail's hand-off),
+// publishes the k best keys of its 64 candidates (write-through stores, post_tail's hand-off),
 // takes a ticket, and the job's last block merges every block's list into out[jn * k ..].
 constexpr int kCollabCands = 64, kCollabTile = 64;
 

@@ -1222,15 +1222,16 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         for (auto& w : J.ws) w.active = false;
         return code;
     };
-    // 1-hop planning of every job first, on the worker pool (a few microseconds per job; threads
-    // only for large calls: spawning them costs more than planning a 64-user step): the first
-    // chunk's launch then waits for its layout only, not for the planning of all its jobs
-    par_jobs(n, [&](size_t i) { plan_job(c, jobs[i], P[i], raw); }, 256);
-    hl.lap(kHpPrep);
     size_t b = 0;
     while (b < n) {
         const size_t lim = chunk_end(b);
         ++ck;
+        // 1-hop planning is a few microseconds per job: threads only for large chunks (spawning
+        // them costs more than planning a 64-user step).  Per chunk: planning every job of a call
+        // up front measured no faster (cfg 5 113.4k vs 110.4k users/s, r4n)
+        par_jobs(lim - b, [&](size_t i) { if (P[b + i].u < 0 && P[b + i].kind < 0) plan_job(c, jobs[b + i], P[b + i], raw); },
+                 256);
+        hl.lap(kHpPrep);
         for (size_t i = b; i < lim; ++i)
             if (P[i].unmapped) return drain(c->fail(PF_EINTERNAL, "adjacency row names an unmapped uid"));
         size_t e = b;

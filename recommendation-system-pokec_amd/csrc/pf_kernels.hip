@@ -830,131 +830,80 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Block-level end of a scan: merge the 4 wave lists, publish the block's k-list and, in
-// the last block of the query, merge every block's list into out[row] (no second launch).
-// sc: LDS >= (waves) * k keys; misc: LDS >= 16 + 4 * kMaxTopK bytes (both idle by now).
-// qy = the query (row of sync / parts / out_rows), bx = this workgroup's index among the query's nbx
-__device__ __forceinline__ void scan_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
+// The scans' (K5, K1) fused cross-block merge, in two levels.  The workgroups of group g = bx mod 8 (with the
+// round-robin dispatch, the workgroups of one XCD) publish their k-lists and take a ticket on the
+// group's counter; the group's last workgroup merges the group's lists (all four waves) into slot
+// nbx + g and takes a ticket on the query's counter; the last of those merges the <= 8 group
+// lists into out[row].  Each counter sees ~nbx / 8 tickets: with one counter for all 1,024
+// workgroups of a one-query launch the tail cost ~15 us of a 185 us launch (r4n, a no-merge build).
+// parts: per query (nbx + 8) lists of k keys.  Hand-offs (cdna_hip_programming.md Guideline 16,
+// R1): a list is published with write-through stores drained before the ticket and read with
+// L1-bypassing loads after it, so no L2 write-back or acquire fence is needed.
+__device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
                                           uint64_t* __restrict__ parts, uint64_t* __restrict__ out,
                                           const int32_t* __restrict__ out_rows, int qy, int bx, int nbx) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // block merge: the 4 wave lists are packed densely (k keys each) and wave 0 takes
-    // them 64 at a time, so 4*k <= 64 keys cost a single push
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
     __syncthreads();
     if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
-    // Fused cross-block merge (no second launch).  Each block publishes its sorted k-list
-    // with write-through (sc1) stores, drains them and takes a ticket; the last block of
-    // the query merges, reading the lists with sc1 loads (cdna_hip_programming.md
-    // Guideline 16, R1: no L2 write-back or acquire fence needed).
     ScanSync* sy = sync + qy;
-    uint64_t* qparts = parts + (size_t)qy * nbx * k;
-    // tail scratch in the (now idle) hit lists: flag, threshold, block count, block ids
-    int* s_flag = misc;
-    int* s_cnt = s_flag + 1;
-    uint64_t* s_T = reinterpret_cast<uint64_t*>(s_flag + 2);
-    int* s_blk = s_flag + 4;
-    if (wave == 0) {
+    uint64_t* qparts = parts + (size_t)qy * (nbx + 8) * k;
+    const int ng = min(8, nbx), g = bx % ng, n_g = (nbx - g + ng - 1) / ng;
+    auto merge_sc = [&]() {  // wave 0: the nw wave lists in sc
         uint64_t acc = ~0ull;
-        const int n = (int)(blockDim.x >> 6) * k;
+        const int n = nw * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
+        return acc;
+    };
+    if (wave == 0) {
+        const uint64_t acc = merge_sc();
         if (lane < k) st_agent(qparts + (size_t)bx * k + lane, acc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __atomic_signal_fence(__ATOMIC_SEQ_CST);  // program order: stores, wait, ticket (no hardware fence)
         unsigned t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(&sy->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) {
-            *s_flag = t == (unsigned)nbx - 1u;
-            *s_cnt = 0;
-        }
+        if (lane == 0) t = __hip_atomic_fetch_add(&sy->grp[g * 16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) misc[0] = t == (unsigned)n_g - 1u;
     }
     __syncthreads();
-    if (!*s_flag) return;
-    const int nb = nbx;
-    const int row = out_rows ? out_rows[qy] : qy;
-    // Pass 1: the k smallest of every block's first j keys (j * nb >= 2k).  Its k-th key T
-    // bounds the final k-th key from above, and a block can hold further keys <= T only
-    // if its j-th key is <= T, which at most k blocks satisfy (keys are distinct).
-    const int j = min(k, max(1, (2 * k + nb - 1) / nb));
-    const int n1 = nb * j;
-    list = ~0ull;
-    for (int base = wave * 512; base < n1; base += (int)blockDim.x * 8) {
-        uint64_t x[8];
+    if (!misc[0]) return;
+    // the group's lists: workgroups g, g + ng, ... (n_g * k keys over the waves, 4 loads in flight)
+    {
+        uint64_t l2 = ~0ull;
+        const int n = n_g * k;
+        for (int base = wave * 256; base < n; base += nw * 256) {
+            uint64_t x[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * 64 + lane;
-            x[u] = ~0ull;
-            if (i < n1) {
-                const int blk = i / j;
-                x[u] = ld_agent(qparts + (size_t)blk * k + (i - blk * j));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) topk_push(list, x[u], k, lane);
-    }
-    if (lane < k) sc[wave * k + lane] = list;
-    __syncthreads();
-    uint64_t acc = ~0ull;
-    if (wave == 0) {
-        const int n = (int)(blockDim.x >> 6) * k;
-        for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        if (lane == 0) *s_T = rdlane64(acc, k - 1);
-    }
-    __syncthreads();
-    const uint64_t T = *s_T;
-    if (T == ~0ull) {
-        // fewer than k keys among the first j of every block: merge every list in full
-        list = ~0ull;
-        const int total = nb * k;
-        for (int base = wave * 512; base < total; base += (int)blockDim.x * 8) {
-            uint64_t x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = base + u * 64 + lane;
-                x[u] = i < total ? ld_agent(qparts + i) : ~0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) topk_push(list, x[u], k, lane);
-        }
-        __syncthreads();
-        if (lane < k) sc[wave * k + lane] = list;
-        __syncthreads();
-        if (wave == 0) {
-            acc = ~0ull;
-            const int n = (int)(blockDim.x >> 6) * k;
-            for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-            if (lane < k) out[(size_t)row * k + lane] = acc;
-        }
-        return;
-    }
-    // Pass 2: the remaining keys of the blocks whose j-th key is <= T
-    if (j < k) {
-        for (int b = (int)threadIdx.x; b < nb; b += (int)blockDim.x) {
-            const uint64_t y = ld_agent(qparts + (size_t)b * k + (j - 1));
-            if (y <= T) {
-                const int p = atomicAdd(s_cnt, 1);
-                if (p < kMaxTopK) s_blk[p] = b;
-            }
-        }
-    }
-    __syncthreads();
-    if (wave == 0) {
-        const int nblk = min(*s_cnt, kMaxTopK), rest = k - j, n2 = nblk * rest;
-        for (int base = 0; base < n2; base += 512) {
-            uint64_t x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < 4; ++u) {
                 const int i = base + u * 64 + lane;
                 x[u] = ~0ull;
-                if (i < n2) {
-                    const int bi = i / rest;
-                    x[u] = ld_agent(qparts + (size_t)s_blk[bi] * k + j + (i - bi * rest));
+                if (i < n) {
+                    const int w = i / k;
+                    x[u] = ld_agent(qparts + (size_t)(g + w * ng) * k + (i - w * k));
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) topk_push(acc, x[u] <= T ? x[u] : ~0ull, k, lane);
+            for (int u = 0; u < 4; ++u) topk_push(l2, x[u], k, lane);
         }
-        if (lane < k) out[(size_t)row * k + lane] = acc;
+        __syncthreads();
+        if (lane < k) sc[wave * k + lane] = l2;
+        __syncthreads();
+    }
+    if (wave == 0) {
+        const uint64_t acc = merge_sc();
+        if (lane < k) st_agent(qparts + (size_t)(nbx + g) * k + lane, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        unsigned t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(&sy->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = (unsigned)__shfl((int)t, 0);
+        if (t == (unsigned)ng - 1u) {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            uint64_t fin = ~0ull;
+            const int n = ng * k;
+            for (int b = 0; b < n; b += 64) topk_push(fin, b + lane < n ? ld_agent(qparts + (size_t)nbx * k + b + lane) : ~0ull, k, lane);
+            const int row = out_rows ? out_rows[qy] : qy;
+            if (lane < k) out[(size_t)row * k + lane] = fin;
+        }
     }
 }
 
@@ -1039,7 +988,7 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         }
         topk_push(list, key, k, lane);
     }
-    scan_tail(list, k, reinterpret_cast<uint64_t*>(scratch), reinterpret_cast<int*>(v.hits), sync, parts, out,
+    post_tail(list, k, reinterpret_cast<uint64_t*>(scratch), reinterpret_cast<int*>(v.hits), sync, parts, out,
               out_rows, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x);
 }
 
@@ -1107,7 +1056,7 @@ constexpr uint32_t kLdsCpre = kLdsColj + 4 * kPostMaxCols;                    //
 constexpr uint32_t kPostFixedLds = (kLdsCpre + 8 * (kPostMaxCols + 1) + 15) & ~15u;
 static_assert(kBlockCands == 2 * kPostThreads, "two candidates per thread");
 static_assert(kRoundCap < 65536 && kBlockCands <= kRoundCap, "u16 slots; a one-token round fits");
-static_assert(kPostWaves * kMaxTopK * 8 + 16 + 4 * kMaxTopK <= 8 * kRoundCap, "scan_tail scratch in the slots");
+static_assert(kPostWaves * kMaxTopK * 8 + 16 + 4 * kMaxTopK <= 8 * kRoundCap, "post_tail scratch in the slots");
 
 // hit slot: tf | token - round start << 8 | first hit of its column segment | first hit of its candidate
 constexpr uint32_t kHitFirst = 1u << 14;
@@ -1362,31 +1311,21 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const uint32_t B = (uint32_t)ps.bsize;
     const bool short_excl = H.n_excl <= kPostThreads;
     const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;  // the query's, once
-    // the next static block's headers and first list ranges, loaded before this block's FAS (their
-    // round trip hidden behind the FAS, the top-k and the block barrier)
-    uint4 pha[kCandsPerThread], phb[kCandsPerThread];
-    uint2 prng = make_uint2(0u, 0u);
-    bool have_pf = false;
     for (int blk = blk_begin + bx; blk < blk_end;) {
         const uint32_t c0 = (uint32_t)blk * B;
         const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
-        // 1. headers of the owned candidates, every list's range in this block and (short list) the
-        // exclusions: all loads issued before the first wait, one memory round trip
+        // 1. headers of the owned candidates and every list's range in this block: all loads
+        // issued before the first wait, one memory round trip.  (Loading the next static block's
+        // headers and ranges before this block's FAS measured slower: 184.8 -> 188.0 us, r4n,
+        // the 16 registers they hold spilled)
         uint4 ha[kCandsPerThread], hb[kCandsPerThread];
-        if (have_pf) {
 #pragma unroll
-            for (int kk = 0; kk < kCandsPerThread; ++kk) { ha[kk] = pha[kk]; hb[kk] = phb[kk]; }
-            if (tid < nl) rng[tid] = prng;
-            for (int j = tid + kPostThreads; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < kCandsPerThread; ++kk) {  // clamped (always valid) index, zeroed below
-                const uint32_t c = min(c0 + kk * kPostThreads + tid, c1);
-                ha[kk] = ps.hdr[2 * (size_t)c];
-                hb[kk] = ps.hdr[2 * (size_t)c + 1];
-            }
-            for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
+        for (int kk = 0; kk < kCandsPerThread; ++kk) {  // clamped (always valid) index, zeroed below
+            const uint32_t c = min(c0 + kk * kPostThreads + tid, c1);
+            ha[kk] = ps.hdr[2 * (size_t)c];
+            hb[kk] = ps.hdr[2 * (size_t)c + 1];
         }
+        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
@@ -1741,21 +1680,6 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             if (F > 0) __syncthreads();  // the next round rewrites the masks, slots and segments
         }
         K5T(11);
-        // the next block when it is static: its headers and first list ranges now
-        {
-            const int nxt = blk + nbx;
-            have_pf = nxt < tail;
-            if (have_pf) {
-                const uint32_t n0 = (uint32_t)nxt * B, n1 = min(n0 + B, (uint32_t)ps.n) - 1;
-#pragma unroll
-                for (int kk = 0; kk < kCandsPerThread; ++kk) {
-                    const uint32_t c = min(n0 + kk * kPostThreads + tid, n1);
-                    pha[kk] = ps.hdr[2 * (size_t)c];
-                    phb[kk] = ps.hdr[2 * (size_t)c + 1];
-                }
-                if (tid < nl) prng = list_range(ps, pl[tid], n0, n1);
-            }
-        }
         // 5. FAS (recommender_similarity.cpp:114-123) and the wave top-k
         uint64_t keys[kCandsPerThread];
 #pragma unroll
@@ -1809,10 +1733,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
     uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
 #if defined(PF_K5_EXP) && (PF_K5_EXP & 512)
-    if (lane < k) parts[((size_t)qy * nbx + bx) * k + lane] = best;  // experiment: no cross-block merge
+    if (lane < k) parts[((size_t)qy * (nbx + 8) + bx) * k + lane] = best;  // experiment: no cross-block merge
     return;
 #endif
-    scan_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
+    post_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
 }
 
 // ---------------------------------------------------------------- K2: merge

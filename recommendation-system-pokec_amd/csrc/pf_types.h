@@ -152,6 +152,7 @@ struct ScanSync {
     unsigned int next;  // K5 dynamic hand-out: blocks claimed past the first gridDim.x, 64 B from done
     unsigned int pad[15];
     unsigned int xcd_next[8 * 16];  // tail tile counter per XCD, 64 B apart
+    unsigned int grp[8 * 16];       // K5's group tickets (post_tail), 64 B apart
 };
 
 // top-k key: ascending key == (score desc, uid asc), recommender_graph.cpp:97-101

@@ -1289,7 +1289,9 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
     if (rc != PF_OK) return rc;
     const size_t n = jobs.size();
     std::vector<JP> P(n);
-    par_jobs(n, [&](size_t i) { plan_job(c, jobs[i], P[i], false); }, 256);
+    // an asynchronous call's jobs (cfg 3: 64 collaborative jobs at limit 10000) on the worker pool
+    // from 16 jobs up: the caller takes jobs while the workers wake, so small calls lose nothing
+    par_jobs(n, [&](size_t i) { plan_job(c, jobs[i], P[i], false); }, 16);
     int64_t el = 0, ht = 0;
     for (const JP& p : P) {
         if (p.unmapped) return c->fail(PF_EINTERNAL, "adjacency row names an unmapped uid");

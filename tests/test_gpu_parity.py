@@ -350,9 +350,11 @@ def test_big_top64_vs_oracle(big, kernel):
                                  {"PF_DEBUG": "scan=postings"},
                                  {"PF_DEBUG": "scan=postings,k5_block=64"},
                                  {"PF_DEBUG": "scan=postings,k5_block=333"},
+                                 {"PF_DEBUG": "scan=postings,k5_static=1,k5_transposed=1"},
                                  {"PF_DEBUG": "resident_images=0"}],
                          ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings",
-                              "postings-block64", "postings-block333", "per-call-images"])
+                              "postings-block64", "postings-block333", "postings-static-transposed",
+                              "per-call-images"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
     query of the batch has tables above 1 KiB (the whole launch then probes global);

@@ -29,6 +29,13 @@ for S in "$@"; do
         timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 2 ;;
     prof)
         timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/prof.json 2> $O/prof.err || exit 3 ;;
+    cfg3h|cfg3h:*)
+        # cfg 3 with the host stage clocks; cfg3h:K runs K timed steps (default 50)
+        K=50; [[ $S == cfg3h:* ]] && K=${S#cfg3h:}
+        timeout -k 10 600 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg3 --steps $K --warmup 5 $Q > $O/cfg3h_$K.json 2> $O/cfg3h_$K.err || exit 4 ;;
+    prof3)
+        # kernel trace of cfg 3 (the asynchronous pair-kernel pipeline at one context)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_cfg3 -o run -- python3 bench.py --workload cfg3 --steps 30 --warmup 5 $Q > $O/prof3.json 2> $O/prof3.err || exit 3 ;;
     prof5)
         # kernel trace of cfg 5 at one context (host-side gaps between the device stages)
         timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/prof_cfg5 -o run -- python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/prof5.json 2> $O/prof5.err || exit 3 ;;

@@ -1459,14 +1459,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 // a. walk: the round's entries flattened over the workgroup, all loads in flight
                 constexpr int U = kRoundCap / kPostThreads;
                 uint32_t kp[U];  // p | token << 10 | tf << 16, or ~0
-#ifdef PF_K5_LAZYNORM
-                uint32_t xs[U];  // experiment: the first hits' norms loaded in the place phase
-                {
-#else
-                double kn[U];
+                double kn[U];  // (norms loaded in the place phase for first hits only: 184.6 -> 199.1 us, r4q)
                 {
                     uint32_t xs[U];
-#endif
                     int js[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -1492,9 +1487,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
                     for (int u = 0; u < U; ++u) {  // unconditional: every load of the round in flight
                         ent[u] = ps.post[K5CHK(xs[u], ps.n_tok_entries, 4)];
-#ifndef PF_K5_LAZYNORM
                         kn[u] = ps.pnorm[K5CHK(xs[u], ps.n_tok_entries, 5)];
-#endif
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -1564,11 +1557,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     // the column's first hit holds its norm, the others their product (one per lane here,
                     // so the terms below only add them up)
-#ifdef PF_K5_LAZYNORM
-                    slot[r] = first ? ps.pnorm[xs[u]] : tok_product(pt, ja + (int)jr, tf);
-#else
                     slot[r] = first ? kn[u] : tok_product(pt, ja + (int)jr, tf);
-#endif
                 }
                 for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {
                     const int j = round_list(gpre, ja, jb, g0 + f);

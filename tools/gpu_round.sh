@@ -91,6 +91,10 @@ for S in "$@"; do
         # profiling build (K5T=1) per-phase K5 clocks; k5t:V uses exp/v/V
         V=k5t; [[ $S == k5t:* ]] && V=${S#k5t:}
         timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/$V.json 2> $O/$V.err || exit 7 ;;
+    pmcpasses:*)
+        # pmcpasses:KERNEL-REGEX  tools/pmc_passes.sh's five counter passes (TAG_KERNEL) over a short cfg-2 run
+        K=${S#pmcpasses:}
+        timeout -k 10 700 bash tools/pmc_passes.sh ${TAG}_$K $K || exit 8 ;;
     pmcv:*)
         # pmcv:V:C1,C2..  one counter pass over 20 cfg-2 steps with the variant library exp/v/V (K5 rows only)
         R=${S#pmcv:}; V=${R%%:*}; C=${R#*:}

@@ -36,6 +36,8 @@ hipError_t launch_clubs(const DevJobsStore& g, const DevView& v, const DevJob* j
                         const int32_t* pool, const int64_t* pool64, const float* pout, double* acc,
                         float* score, int32_t* ids, int32_t* ncand, int64_t acc_stride, hipStream_t s);
 // the pair blocks' dispatch order, longest first record first (pf_jobs.hip order_pairs_kernel)
+hipError_t launch_expand_pairs(const PairGen* gens, int ngens, const int2* pool, int nblocks, PairBlock* blocks,
+                               hipStream_t s);
 hipError_t launch_order_pairs(const PairBlock* blocks, int nblocks, const int32_t* slots, int32_t n_slots,
                               int32_t* order, hipStream_t s);
 // pair counts and bytes of the pair blocks (pf_jobs_stats)

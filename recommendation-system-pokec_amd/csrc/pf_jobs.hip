@@ -1028,6 +1028,33 @@ hipError_t launch_pair_stats(const DevStore& st, const PairBlock* blocks, int nb
     return hipGetLastError();
 }
 
+// K9: the pair blocks of a chunk from its runs (PairGen), one thread per block; the run by a
+// bisection of the runs' first blocks (ascending)
+__global__ __launch_bounds__(256) void expand_pairs_kernel(const PairGen* __restrict__ gens, int ngens,
+                                                           const int2* __restrict__ pool, int nblocks,
+                                                           PairBlock* __restrict__ blocks) {
+    const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (b >= nblocks) return;
+    int lo = 0, hi = ngens - 1;  // the last run with first <= b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (gens[mid].first <= b) lo = mid; else hi = mid - 1;
+    }
+    const PairGen g = gens[lo];
+    const int loc = b - g.first, x = loc / g.nf, f = loc - x * g.nf;
+    const int2 e = pool[g.fl + f];
+    const int off = x * kPairThreads;  // kPairSpan (pf_jobs_plan.cpp): one pair per thread of a K1' block
+    blocks[b] = PairBlock{e.x, g.cand + off, min(kPairThreads, g.cap - off), g.out + e.y * g.stride + off};
+}
+
+hipError_t launch_expand_pairs(const PairGen* gens, int ngens, const int2* pool, int nblocks, PairBlock* blocks,
+                               hipStream_t s) {
+    if (nblocks <= 0 || ngens <= 0) return hipSuccess;
+    hipLaunchKernelGGL(expand_pairs_kernel, dim3((nblocks + 255) / 256), dim3(256), 0, s, gens, ngens, pool, nblocks,
+                       blocks);
+    return hipGetLastError();
+}
+
 hipError_t launch_order_pairs(const PairBlock* blocks, int nblocks, const int32_t* slots, int32_t n_slots,
                               int32_t* order, hipStream_t s) {
     if (nblocks <= 0) return hipSuccess;

@@ -673,26 +673,40 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         img_idx.push_back(idx);
         return k;
     };
-    std::vector<PairBlock> blocks;
+    // The pair blocks as runs (PairGen, expanded on the device by K9 expand_pairs_kernel): a run is
+    // ceil(cap / kPairSpan) candidate chunks x nf (image, row) entries of the pool, chunk-major, so
+    // the host writes ~one run per job and image class instead of ~140k 16-B blocks per cfg-5 chunk
+    // (their layout was ~2.3 ms of host time per chunk, r4m host clocks).  Runs are built per job
+    // here (images as img() indices), then split by the images' LDS class below.
+    struct RawGen {
+        int32_t nch, cap, cand, out, stride, fl, nf;
+    };
+    std::vector<RawGen> rgen;
+    std::vector<int2> gpool;  // (image, row) entries of the runs
+    auto add_gen = [&](int64_t cap, int64_t cand, int64_t out, int64_t stride, const int2* ents, int nf) {
+        if (cap <= 0 || nf <= 0) return;
+        rgen.push_back(RawGen{(int32_t)((cap + kPairSpan - 1) / kPairSpan), (int32_t)cap, (int32_t)cand, (int32_t)out,
+                              (int32_t)stride, (int32_t)gpool.size(), nf});
+        gpool.insert(gpool.end(), ents, ents + nf);
+    };
     auto add_blocks = [&](int32_t im, int64_t begin, int64_t count, int64_t out) {
-        for (int64_t x = 0; x < count; x += kPairSpan)
-            blocks.push_back(PairBlock{im, (int32_t)(begin + x), (int32_t)std::min<int64_t>(kPairSpan, count - x),
-                                       (int32_t)(out + x)});
+        const int2 e = make_int2(im, 0);
+        add_gen(count, begin, out, 0, &e, 1);
     };
     std::vector<int32_t> jix_collab, jix_clubs, jix_topk, jix_fused, jix_ctopk;
     int max_cap_collab = 0, ktop = 1;
     const int lge = lg_for(0);
     auto ntok_of = [&](int32_t idx) { return hc.tok_off[(size_t)(idx + 1) * hc.T] - hc.tok_off[(size_t)idx * hc.T]; };
     {
-        size_t nb = 0, words = 0;  // the blocks and pool words this chunk appends (one allocation)
+        size_t ng = 0, words = 0;  // the runs and pool words this chunk appends (one allocation)
         for (size_t i = b; i < e; ++i) {
             const JP& p = P[i];
             if (p.kind < 0) continue;
-            const size_t ch = (size_t)(p.cap + kPairSpan - 1) / kPairSpan;
-            nb += ch * (1 + p.fd.size()) + 1 + p.fd.size() + (size_t)p.seqlen / kPairSpan;
+            ng += 2 + p.fd.size();
             words += p.own.size() + p.F.size() + 2 * p.fd.size();
         }
-        blocks.reserve(nb);
+        rgen.reserve(ng);
+        gpool.reserve(ng + 2 * (e - b));
         pool32.reserve(words + 1);
     }
     for (size_t i = b; i < e; ++i) {
@@ -752,15 +766,10 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
                 // candidate-chunk major: the friends' blocks of one candidate chunk are
                 // consecutive, so they run together and share the chunk's records in cache;
                 // a block scores span() candidates against one staged friend image
-                const int64_t span = kPairSpan;
-                std::vector<int32_t> fimg(d.nfd);
-                for (int r = 0; r < d.nfd; ++r) fimg[r] = img(p.fd[r]);
-                for (int64_t x = 0; x < p.cap; x += span) {
-                    const int32_t cnt = (int32_t)std::min<int64_t>(span, p.cap - x);
-                    for (int r = 0; r < d.nfd; ++r)
-                        blocks.push_back(PairBlock{fimg[r], (int32_t)(d.cand_off + x), cnt,
-                                                   (int32_t)(d.m_off + (int64_t)r * p.cap + x)});
-                }
+                // (block (x, r): friend r's image, candidates cand_off + x * span, out m_off + r * cap + x * span)
+                std::vector<int2> fe(d.nfd);
+                for (int r = 0; r < d.nfd; ++r) fe[r] = make_int2(img(p.fd[r]), r);
+                add_gen(p.cap, d.cand_off, d.m_off, p.cap, fe.data(), d.nfd);
                 jix_collab.push_back(jn);
                 max_cap_collab = std::max<int>(max_cap_collab, (int)p.cap);
             } else if (p.kind == kDjInterest || p.kind == kDjAll) {
@@ -811,7 +820,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         for (size_t k = 0; k < img_idx.size(); ++k) pos[k] = cls[k] == 0 ? a++ : (cls[k] == 1 ? b2++ : g2++);
         for (size_t k = 0; k < img_idx.size(); ++k) order[pos[k]] = img_idx[k];
         img_idx.swap(order);
-        for (PairBlock& pb : blocks) pb.qimg = pos[pb.qimg];
+        for (int2& ge : gpool) ge.x = pos[ge.x];
     }
     std::vector<ImgJob> ij(resident ? 0 : img_idx.size());
     std::vector<QImageRef> refs(img_idx.size());
@@ -854,6 +863,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     // (484 vs 338 us, r3ad), and one global-table image switched every block to global probes.
     uint32_t lds_c[3] = {0u, 0u, 0u};
     int nb_c[3] = {0, 0, 0};
+    std::vector<PairGen> gens;  // by class, `first` = the run's first block
+    std::vector<int2> gp2;      // their (image, row) entries
+    int64_t nblk = 0;           // pair blocks of the chunk
     {
         constexpr uint32_t kTwoPerCu = 80u * 1024u;  // 160 KB of LDS per CU
         std::vector<uint8_t> icls(refs.size());
@@ -863,12 +875,24 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             icls[k] = refs[k].lds_bytes == 0 ? 2 : (need <= kTwoPerCu ? 0 : 1);
             lds_c[icls[k]] = std::max(lds_c[icls[k]], need);
         }
-        std::vector<PairBlock> part[3];
-        for (const PairBlock& pb : blocks) part[icls[pb.qimg]].push_back(pb);
-        blocks.clear();
+        // each run split by class (its entries of one class keep their order); the classes'
+        // blocks are consecutive, class 0 first
+        gens.reserve(rgen.size() + 8);
+        gp2.reserve(gpool.size());
         for (int k = 0; k < 3; ++k) {
-            nb_c[k] = (int)part[k].size();
-            blocks.insert(blocks.end(), part[k].begin(), part[k].end());
+            int64_t cnt = 0;
+            for (const RawGen& g : rgen) {
+                const int32_t fl = (int32_t)gp2.size();
+                for (int f = 0; f < g.nf; ++f)
+                    if (icls[gpool[g.fl + f].x] == k) gp2.push_back(gpool[g.fl + f]);
+                const int32_t nf = (int32_t)gp2.size() - fl;
+                if (nf == 0) continue;
+                gens.push_back(PairGen{nf, g.nch, g.cap, g.cand, fl, g.stride, g.out, (int32_t)(nblk + cnt)});
+                cnt += (int64_t)g.nch * nf;
+            }
+            if (nblk + cnt >= INT32_MAX) return c->fail(PF_EUNSUPP, "job batch too large for one pair launch");
+            nb_c[k] = (int)cnt;
+            nblk += cnt;
         }
     }
     hl.lap(kHpImages);
@@ -883,7 +907,8 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const size_t o_ij = a16z(o_p64 + pool64.size() * 8);
     const size_t o_refs = a16z(o_ij + ij.size() * sizeof(ImgJob));
     const size_t o_blk = a16z(o_refs + refs.size() * sizeof(QImageRef));
-    const size_t o_jc = a16z(o_blk + blocks.size() * sizeof(PairBlock));
+    const size_t o_gp = a16z(o_blk + std::max<size_t>(gens.size(), 1) * sizeof(PairGen));
+    const size_t o_jc = a16z(o_gp + std::max<size_t>(gp2.size(), 1) * sizeof(int2));
     const size_t o_jk = a16z(o_jc + jix_collab.size() * 4);
     const size_t o_jt = a16z(o_jk + jix_clubs.size() * 4);
     const size_t o_tk = a16z(o_jt + jix_topk.size() * 4);  // K4' top-k tickets (zero), one per collaborative job
@@ -899,14 +924,16 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     put(o_p64, pool64.data(), pool64.size() * 8);
     put(o_ij, ij.data(), ij.size() * sizeof(ImgJob));
     put(o_refs, refs.data(), refs.size() * sizeof(QImageRef));
-    put(o_blk, blocks.data(), blocks.size() * sizeof(PairBlock));
+    put(o_blk, gens.data(), gens.size() * sizeof(PairGen));
+    put(o_gp, gp2.data(), gp2.size() * sizeof(int2));
     put(o_jc, jix_collab.data(), jix_collab.size() * 4);
     put(o_jk, jix_clubs.data(), jix_clubs.size() * 4);
     put(o_jt, jix_topk.data(), jix_topk.size() * 4);
     if (!jix_collab.empty()) std::memset(h + o_tk, 0, jix_collab.size() * 4);
     std::memset(h + o_res, 0, 16);
     const size_t o_ord = a16z(o_res + res_b);  // the pair blocks' dispatch order (device-written)
-    HIPCHK(c, W.d_plan.reserve(o_ord + std::max<size_t>(blocks.size(), 1) * 4));
+    const size_t o_bd = a16z(o_ord + std::max<size_t>((size_t)nblk, 1) * 4);  // the pair blocks (device-written, K9)
+    HIPCHK(c, W.d_plan.reserve(o_bd + std::max<size_t>((size_t)nblk, 1) * sizeof(PairBlock)));
     if (J.aux == nullptr) {
         HIPCHK(c, hipStreamCreateWithFlags(&J.aux, hipStreamNonBlocking));
         HIPCHK(c, hipStreamCreateWithFlags(&J.aux2, hipStreamNonBlocking));
@@ -924,7 +951,9 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     const int64_t* d_p64 = reinterpret_cast<const int64_t*>(d + o_p64);
     const ImgJob* d_ij = reinterpret_cast<const ImgJob*>(d + o_ij);
     const QImageRef* d_refs = reinterpret_cast<const QImageRef*>(d + o_refs);
-    const PairBlock* d_blk = reinterpret_cast<const PairBlock*>(d + o_blk);
+    const PairGen* d_gen = reinterpret_cast<const PairGen*>(d + o_blk);
+    const int2* d_gpool = reinterpret_cast<const int2*>(d + o_gp);
+    PairBlock* d_blk = reinterpret_cast<PairBlock*>(d + o_bd);
     const int32_t* d_jc = reinterpret_cast<const int32_t*>(d + o_jc);
     const int32_t* d_jk = reinterpret_cast<const int32_t*>(d + o_jk);
     const int32_t* d_jt = reinterpret_cast<const int32_t*>(d + o_jt);
@@ -962,6 +991,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     // ---- the stages, in stream order; the gathers and dispatch orders run on the aux stream and
     // join before the pair kernel, beside the images
     HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, fail word) is up
+    HIPCHK(c, launch_expand_pairs(d_gen, (int)gens.size(), d_gpool, (int)nblk, d_blk, J.aux));  // K9: the blocks
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
                             d_ncand, J.aux));
@@ -972,7 +1002,7 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds,
                                  W.d_img.as<uint8_t>(), W.d_scr.as<uint32_t>(), d_fail, s));
     HIPCHK(c, hipStreamWaitEvent(s, J.ev_join, 0));
-    const bool any_pairs = !blocks.empty();
+    const bool any_pairs = nblk > 0;
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && any_pairs) {
         if (J.stat_used == J.stat_ev.size()) {
@@ -997,12 +1027,12 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     }
     if (J.stats_count && any_pairs) {
         unsigned long long* acc = J.d_stats.as<unsigned long long>();
-        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)blocks.size(), W.d_slots.as<int32_t>(), acc, s));
-        for (const PairBlock& pb : blocks) {  // the staged image per pair block (QConst + tables)
-            const QImageRef& r = refs[pb.qimg];
-            const int32_t idx = img_idx[pb.qimg];
-            J.st_img_bytes += (int64_t)r.vals_off + ntok_of(idx) * (int64_t)sizeof(QVal);
-        }
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)nblk, W.d_slots.as<int32_t>(), acc, s));
+        for (const PairGen& g : gens)  // the staged image per pair block (QConst + tables)
+            for (int f = 0; f < g.nf; ++f) {
+                const int32_t k = gp2[g.fl + f].x;
+                J.st_img_bytes += (int64_t)g.nch * ((int64_t)refs[k].vals_off + ntok_of(img_idx[k]) * (int64_t)sizeof(QVal));
+            }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
     // K7 (clubs, one latency-bound wave per job) and its jobs' K8 go to the second aux stream once

@@ -15,6 +15,15 @@ struct PairBlock {
     int32_t qimg, begin, count, out;
 };
 
+// A run of pair blocks, expanded on the device (pf_jobs.hip expand_pairs_kernel): block
+// first + x * nf + f (chunk x < nch, entry f < nf) scores image pool[fl + f].x against candidates
+// [cand + x * kPairThreads, + min(kPairThreads, cap - x * kPairThreads)) into out + pool[fl + f].y * stride
+// + x * kPairThreads (chunk-major: one candidate chunk's friends consecutive, sharing its records
+// in cache)
+struct PairGen {
+    int32_t nf, nch, cap, cand, fl, stride, out, first;
+};
+
 
 // lds: dynamic LDS bytes per block = max over the batch of
 //   sizeof(QConst) + staged keys/vals + n_hits_max * threads + 2048

@@ -266,7 +266,12 @@ uint32_t post_mode(int nq) {
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
 // candidates/s.
-constexpr int kBatchBlocksPerWg = 4;
+constexpr int kBatchBlocksPerWgDefault = 4;
+// PF_DEBUG k5_batch_blocks=N (A/B)
+int batch_blocks_per_wg() {
+    static const int n = (int)std::max(1L, pf::debug_long("k5_batch_blocks", kBatchBlocksPerWgDefault));
+    return n;
+}
 
 // Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
 // launch the caller passes timed = false, or that sampling skips, records nothing and clears
@@ -340,7 +345,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // query looping over the range instead, 256 queries run at once and L2 hits collapse
     // (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
     const int blocks = nq == 1 ? std::max(1, std::min(nwb, c->num_cus * per_cu))
-                               : std::max(1, (nwb + kBatchBlocksPerWg - 1) / kBatchBlocksPerWg);
+                               : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
@@ -979,7 +984,7 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     // workgroups that stage a query's image, as scan_post launches the fitting queries
     const int nwb = c->wb_end - c->wb_begin;
     const int wgs = nfit == 1 ? c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists))
-                              : (nwb + kBatchBlocksPerWg - 1) / kBatchBlocksPerWg;
+                              : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
     par_jobs((size_t)nq, [&](size_t i) {
         out[i] = kind[i] == 0 ? 0 : (kind[i] == 2 ? k1 : post_query_bytes(c, imgs[i], wgs));
     }, 1);

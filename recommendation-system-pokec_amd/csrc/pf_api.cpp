@@ -275,6 +275,12 @@ int batch_blocks_per_wg() {
     return n;
 }
 
+// Workgroups of a one-query postings scan: one resident round (PF_DEBUG k5_wgs=N overrides it, A/B)
+int one_query_wgs(int resident) {
+    static const long n = pf::debug_long("k5_wgs", 0);
+    return n > 0 ? (int)n : resident;
+}
+
 // Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
 // launch the caller passes timed = false, or that sampling skips, records nothing and clears
 // last_ev0/last_ev1, so pf_last_scan_ms never reports another launch's time.
@@ -341,12 +347,12 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     const uint32_t wave_lds = vl[order[0]];  // the one-query case
     const int nwb = c->wb_end - c->wb_begin;
     const int per_cu = pcu[order[0]];
-    // One query: one resident round of workgroups loops over the blocks.  A batch: one block
-    // per workgroup, so the resident workgroups (dispatched x-fastest) cover one or two
-    // queries at a time and share their lists and cells in L2; with a few workgroups per
-    // query looping over the range instead, 256 queries run at once and L2 hits collapse
-    // (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
-    const int blocks = nq == 1 ? std::max(1, std::min(nwb, c->num_cus * per_cu))
+    // One query: one resident round of workgroups loops over the blocks.  A batch: a few blocks
+    // per workgroup (batch_blocks_per_wg), so the resident workgroups (dispatched x-fastest)
+    // cover a few queries at a time and share their lists and cells in L2; with one resident
+    // round looping over every query's range instead, 256 queries run at once and L2 hits
+    // collapse (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
+    const int blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
                                : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
@@ -985,7 +991,7 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     }
     // workgroups that stage a query's image, as scan_post launches the fitting queries
     const int nwb = c->wb_end - c->wb_begin;
-    const int wgs = nfit == 1 ? c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists))
+    const int wgs = nfit == 1 ? one_query_wgs(c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists)))
                               : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
     par_jobs((size_t)nq, [&](size_t i) {
         out[i] = kind[i] == 0 ? 0 : (kind[i] == 2 ? k1 : post_query_bytes(c, imgs[i], wgs));

@@ -1776,8 +1776,13 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
 }
 
 // ---------------------------------------------------------------- K1': pairs
+#ifdef PF_K1P_WPE  // experiment builds: waves per SIMD the pair kernel's registers are sized for
+#define PF_K1P_BOUNDS __launch_bounds__(kPairThreads) __attribute__((amdgpu_waves_per_eu(PF_K1P_WPE, PF_K1P_WPE)))
+#else
+#define PF_K1P_BOUNDS __launch_bounds__(kPairThreads, 4)
+#endif
 template <bool PACKED, bool GTAB>
-__global__ __launch_bounds__(kPairThreads, 4) void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
+__global__ PF_K1P_BOUNDS void fas_pairs_kernel(DevStore st, const uint8_t* __restrict__ pool,
                                                         const QImageRef* __restrict__ refs,
                                                         const PairBlock* __restrict__ blocks,
                                                         const int32_t* __restrict__ order,

@@ -75,6 +75,10 @@ for S in "$@"; do
         # rehearse:N[:W]  bench.py's N > 1 path with N gloo ranks on this one GPU (tools/rehearse_multi.sh)
         R=${S#rehearse:}; N=${R%%:*}; W=cfg4; [[ $R == *:* ]] && W=${R#*:}
         bash tools/rehearse_multi.sh $TAG $N $W || exit 11 ;;
+    cfg3v:*)
+        # cfg3v:V  cfg 3 (30 steps) with the variant library exp/v/V
+        V=${S#cfg3v:}
+        timeout -k 10 600 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg3 --steps 30 --warmup 5 $Q > $O/cfg3v_$V.json 2> $O/cfg3v_$V.err || exit 4 ;;
     cfg5v:*)
         # cfg5v:V  cfg 5 at one context with the variant library exp/v/V
         V=${S#cfg5v:}

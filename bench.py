@@ -790,7 +790,8 @@ def main():
                     help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
     ap.add_argument("--no-cfg3", action="store_true",
                     help="cfg2 at N = 1: skip the cfg-3 sub-record (collaborative FoF top-10, 64 users per step)")
-    ap.add_argument("--cfg3-steps", type=int, default=20, help="timed steps of the cfg-3 sub-record")
+    ap.add_argument("--cfg3-steps", type=int, default=50,
+                    help="timed steps of the cfg-3 sub-record (with 5 warmup steps: the query stream of --workload cfg3)")
     ap.add_argument("--n1-steps", type=int, default=5,
                     help="N > 1: steps rank 0 times the same workload unsharded on its own GPU (n1_same_workload)")
     args = ap.parse_args()
@@ -814,7 +815,7 @@ def main():
     t1 = time.time()
     # the cfg-3 sub-record of the default N = 1 line (the north star's FoF half, BASELINE cfg 3)
     sub3 = args.workload == "cfg2" and world == 1 and not args.no_cfg3
-    W3 = 3
+    W3 = 5  # the sub-record's warmup: with --cfg3-steps 50 the same seeded users as --workload cfg3's defaults
     # rank 0 at N = 1, before this process touches the GPU: the CPU baselines (forked, pinned
     # children) and the rocprofv3 PMC pass (a child running this same command)
     want_kernel = "fas_scan_kernel" if args.scan_kernel == "stream" else "fas_post_kernel"

@@ -259,7 +259,10 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 uint32_t post_mode(int nq) {
     static const bool tr = pf::debug_long("k5_transposed", 0) != 0;
     static const bool st = pf::debug_long("k5_static", 0) != 0;  // A/B: static hand-out for one query
-    return nq == 1 ? (st ? 0u : 1u) : (tr ? 2u : 0u);
+    // one query: each XCD's workgroups take a contiguous range of every static round's blocks
+    // (neighbouring blocks share the cache lines at their list segments' ends); PF_DEBUG k5_xcd=0 A/B
+    static const bool xcd = pf::debug_long("k5_xcd", 1) != 0;
+    return nq == 1 ? ((st ? 0u : 1u) | (xcd ? 4u : 0u)) : (tr ? 2u : 0u);
 }
 
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once

@@ -259,10 +259,12 @@ void emit(const Ranked& r, int i, int topk, int32_t* ou, float* os, int32_t* oc)
 uint32_t post_mode(int nq) {
     static const bool tr = pf::debug_long("k5_transposed", 0) != 0;
     static const bool st = pf::debug_long("k5_static", 0) != 0;  // A/B: static hand-out for one query
-    // one query: each XCD's workgroups take a contiguous range of every static round's blocks
-    // (neighbouring blocks share the cache lines at their list segments' ends); PF_DEBUG k5_xcd=0 A/B
+    // each XCD's workgroups take a contiguous range of every static round's blocks (neighbouring
+    // blocks share the cache lines at their list segments' ends); the query-major batch grid too
+    // (a query's workgroups are a multiple of 8 there, so bx mod 8 is still the XCD); k5_xcd=0 A/B
     static const bool xcd = pf::debug_long("k5_xcd", 1) != 0;
-    return nq == 1 ? ((st ? 0u : 1u) | (xcd ? 4u : 0u)) : (tr ? 2u : 0u);
+    const uint32_t x = xcd ? 4u : 0u;
+    return nq == 1 ? ((st ? 0u : 1u) | x) : (tr ? 2u : x);
 }
 
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once

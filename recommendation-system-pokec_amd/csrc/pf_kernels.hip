@@ -1311,9 +1311,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const uint32_t B = (uint32_t)ps.bsize;
     const bool short_excl = H.n_excl <= kPostThreads;
     const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;  // the query's, once
-    // mode bit 2 (one query): the workgroups of XCD x (bx mod 8 under the round-robin dispatch) take
-    // blocks [x nbx/8, (x + 1) nbx/8) of each static round, so a list segment's boundary cache
-    // lines are shared inside one L2 instead of fetched by two XCDs
+    // mode bit 2 (one query, query-major batches): the workgroups of XCD x (bx mod 8 under the
+    // round-robin dispatch when nbx is a multiple of 8) take blocks [x nbx/8, (x + 1) nbx/8) of each
+    // static round, so a list segment's boundary cache lines are shared inside one L2 instead of
+    // fetched by two XCDs (cfg 2 PMC traffic 236 -> 175 MB per launch, r4w -> r5h)
     const int pb = ((mode & 4u) && (nbx & 7) == 0) ? (bx & 7) * (nbx >> 3) + (bx >> 3) : bx;
     for (int blk = blk_begin + pb; blk < blk_end;) {
         const uint32_t c0 = (uint32_t)blk * B;

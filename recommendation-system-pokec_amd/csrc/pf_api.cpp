@@ -601,7 +601,16 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         if (!strcmp(sk, "stream")) c->scan_kind = PF_SCAN_STREAM;
         else if (!strcmp(sk, "postings") && c->hp.ok) c->scan_kind = PF_SCAN_POSTINGS;
     }
+    // the job pipeline's two aux streams are created here with the context's own, so the three
+    // take consecutive hardware queues whatever streams the host process creates later (created
+    // at the first job call, after a torch stream pool, they ran the cfg-3 sub-record of the
+    // default bench line at 0.466 vs 0.415 ms per step, r5l)
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        (pf::debug_long("lazy_aux", 0) == 0 &&
+         (hipStreamCreateWithFlags(&c->jb.aux, hipStreamNonBlocking) != hipSuccess ||
+          hipStreamCreateWithFlags(&c->jb.aux2, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c->jb.ev_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->jb.ev_join, hipEventDisableTiming) != hipSuccess)) ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         c->err = "stream/event creation failed";
         return bail(PF_ENODEV);

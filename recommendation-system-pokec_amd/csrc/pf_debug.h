@@ -12,6 +12,7 @@
 //   k5_static=1           one-query postings scans with the static block hand-out (A/B)
 //   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 16; A/B)
 //   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; A/B)
+//   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
 //   k5_xcd=0|1            K5: contiguous block ranges per XCD in each static round (default 1; A/B)
 //   chunk_plan=W1:W2:..   relative chunk sizes of large job-pipeline calls (default 1:1:1; A/B)
 //   load_threads=N        loader threads (default: min(16, hardware threads))

@@ -30,8 +30,10 @@ launch on the kernel's stream:
               of the same command (a child process started before this one touches the GPU;
               FETCH_SIZE KiB x 1024 x the gfx950 factor calibrated for the kernel's load widths,
               profiles/fetch_calib_*.json), null when rocprofv3 is absent or --no-pmc;
-  alg_effective_* = SURVEY D3's per-candidate record bytes (b_c, the metric's definition)
-              over the same time, an *effective* rate a postings scan can exceed the peak with.
+  d3_equiv_* = SURVEY D3's per-candidate record bytes (b_c, the metric's definition)
+              over the same time: an *equivalent* rate, NOT an HBM fraction (the postings scan
+              never reads those records, so d3_equiv_x_peak can exceed 1); roofline.frac is the
+              kernel's HBM fraction.
 CPU baseline: oracle/refcpu.cpp (the reference algorithm with its unordered_map data
 structures), one core, bounded sample of the same corpus, median per query; plus an
 all-cores context figure (one oracle per core).
@@ -225,17 +227,25 @@ def pmc_pass(args, select):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return {k: (None, "rocprofv3 not found") for k in select}
+    # one calibration for every kernel (profiles/fetch_calib_r2.json, tools/fetch_calib.hip): the
+    # postings scans' 4/8-B gathers take its k5_factor, the record-stream kernels (K1, K1': 16-B
+    # steps) its w16_stream factor; 2.0 (MI355X_MICROARCH.md) only when the file is absent
     factors = {}
+    cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
+    calib = None
+    if os.path.exists(cal):
+        try:
+            with open(cal) as f:
+                calib = json.load(f)
+        except Exception:
+            calib = None
     for k in select:
         factor, fsrc = 2.0, "MI355X_MICROARCH.md (16-B/lane streams)"
-        cal = os.path.join(ROOT, "profiles", "fetch_calib_r2.json")
-        if os.path.exists(cal) and k == "fas_post_kernel":  # 4/8-B loads; K1 / K1' read 16-B steps
-            try:
-                with open(cal) as f:
-                    c = json.load(f)
-                factor, fsrc = float(c["k5_factor"]), "profiles/fetch_calib_r2.json"
-            except Exception:
-                pass
+        if calib is not None:
+            if k in ("fas_post_kernel", "fas_slice_kernel"):
+                factor, fsrc = float(calib["k5_factor"]), "profiles/fetch_calib_r2.json k5_factor"
+            else:
+                factor, fsrc = float(calib["w16_stream"]["factor"]), "profiles/fetch_calib_r2.json w16_stream"
         factors[k] = (factor, fsrc)
     d = tempfile.mkdtemp(prefix="pf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = [prof, "--pmc", "FETCH_SIZE", "--kernel-include-regex", "|".join(select), "-T", "--output-format", "csv",
@@ -469,8 +479,8 @@ def cfg3_fields(st, steps, pmc):
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
                      "traffic_source": tsrc,
-                     "alg_effective_gbs": rate(alg_pl),
-                     "alg_effective_frac": None if rate(alg_pl) is None else rate(alg_pl) / HBM_PEAK_GBS,
+                     "d3_equiv_gbs": rate(alg_pl),
+                     "d3_equiv_x_peak": None if rate(alg_pl) is None else rate(alg_pl) / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_pl,
                      "pair_kernel_share_of_step": (ms / (elapsed * 1e3)) if elapsed > 0 else None},
     }
@@ -730,7 +740,7 @@ def run_cfg5(args, world, rank, local):
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_ms else rate(traffic) / HBM_PEAK_GBS,
                      "traffic_source": tsrc,
-                     "alg_effective_gbs": rate(alg_pl),
+                     "d3_equiv_gbs": rate(alg_pl),
                      "alg_bytes_per_launch": alg_pl,
                      "pair_kernel_share_of_step": (timing["pair_ms"] / (elapsed * 1e3)) if elapsed > 0 else None},
         "selfcheck_vs_sequential_64_users": selfcheck, "files_s": write_s, "open_s": open_s,
@@ -1015,11 +1025,11 @@ def main():
                      "dram_gbs": rate(traffic),
                      "dram_frac": None if traffic is None or not avg_launch_ms else rate(traffic) / HBM_PEAK_GBS,
                      "traffic_source": ({k: v for k, v in pmc.items() if k != "_raw"} if pmc else pmc_err),
-                     "alg_effective_gbs": alg_eff,
-                     "alg_effective_frac": None if alg_eff is None else alg_eff / HBM_PEAK_GBS,
+                     "d3_equiv_gbs": alg_eff,
+                     "d3_equiv_x_peak": None if alg_eff is None else alg_eff / HBM_PEAK_GBS,
                      "alg_bytes_per_launch": alg_bytes,
                      "note": ("achieved/frac: the bytes this kernel reads by its access pattern; "
-                              "alg_effective_*: SURVEY D3 record bytes b_c of every candidate over the same time (the "
+                              "d3_equiv_*: SURVEY D3 record bytes b_c of every candidate over the same time (the "
                               "postings scan reads only the query's lists, so that effective rate can pass the peak)")},
         "topk_selfcheck": consistent,
     }

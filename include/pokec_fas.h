@@ -272,15 +272,15 @@ int pf_scan_bytes(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, int64_t* ou
  * _interest FoF and the batched drivers) since pf_jobs_stats_reset(ctx, 1): jobs run,
  * candidate-list entries scored, FAS pairs scored by the pair kernel (K1'), their
  * SURVEY 8(d) D3 bytes (b_c of each pair's candidate), the bytes the pair-scoring stage
- * reads / writes for them by access pattern (pair_record_bytes: headers + record words for a
- * pair that walks its record; for collaborative friend groups the K1u walk's record words
- * once per group plus the per-pair hit lists it writes and K1' reads), the staged query-image
- * and union-table bytes (one per 512-pair / walk block), and the pair-scoring stage's device
- * time (HIP events around K1u + K1' in each launch) and launch count.  enable: bit 0 = time the pair kernel (HIP events around each
+ * reads for them by access pattern (pair_record_bytes: the 48-B headers + the record words
+ * of every pair's candidate), the staged query-image bytes (one image per 512-pair block),
+ * and the pair-scoring stage's device time (HIP events around K1' in each launch) and
+ * launch count.  enable: bit 0 = time the pair kernel (HIP events around each
  * launch), bit 1 = count pairs and bytes (one extra small kernel per launch); 0 stops
- * both.  Fields of a part that is off read 0.  pair_dispatches: the pair-kernel (K1')
- * dispatches since pf_open, never reset (a pair stage launches up to four, by image LDS
- * class), so a profiler's per-dispatch rows can be grouped into the stages they belong to. */
+ * both.  Fields of a part that is off read 0.  pair_dispatches: every pair-kernel (K1')
+ * dispatch since pf_open (the job pipeline's stages, up to three per stage by image LDS
+ * class, and pf_fas_pairs), never reset, so a profiler's per-dispatch rows can be grouped
+ * into the calls they belong to. */
 typedef struct pf_jobs_stats {
     int64_t jobs, candidates, pairs;
     int64_t pair_alg_bytes, pair_record_bytes, pair_image_bytes;

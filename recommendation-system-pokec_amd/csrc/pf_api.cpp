@@ -226,6 +226,7 @@ int run_pairs(pf_ctx* c, const std::vector<int32_t>& qidx, const std::vector<std
         HIPCHK(c, pf::launch_pairs(c->ds, c->d_pool.as<uint8_t>(), c->d_refs.as<pf::QImageRef>(), im.max_lds, im.gtab,
                                    c->d_blocks.as<pf::PairBlock>(), (int)blocks.size(), nullptr, c->d_slots.as<int32_t>(), dsc,
                                    c->stream));
+        c->jb.n_dispatch += !blocks.empty();  // pf_jobs_stats.pair_dispatches counts every K1' dispatch
         const float* res = c->h_scores.as<float>();
         HIPCHK(c, hipMemcpyAsync(c->h_scores.p, dsc, npairs * sizeof(float), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -267,6 +268,12 @@ uint32_t post_mode(int nq) {
     return nq == 1 ? ((st ? 0u : 1u) | x) : (tr ? 2u : x);
 }
 
+// K5s mode word: bit 0 = claimed slices past each wave's first (PF_DEBUG k5s_static=1: static)
+uint32_t slice_mode() {
+    static const bool st = pf::debug_long("k5s_static", 0) != 0;
+    return st ? 0u : 1u;
+}
+
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
@@ -277,6 +284,27 @@ constexpr int kBatchBlocksPerWgDefault = 16;
 // PF_DEBUG k5_batch_blocks=N (A/B)
 int batch_blocks_per_wg() {
     static const int n = (int)std::max(1L, pf::debug_long("k5_batch_blocks", kBatchBlocksPerWgDefault));
+    return n;
+}
+
+// The postings-scan kernel: K5s (wave-private slices) when PF_DEBUG k5_slice=1, else K5
+bool use_slice() {
+    static const bool on = pf::debug_long("k5_slice", 0) != 0;
+    return on;
+}
+// dynamic LDS of one image's postings scan, for the kernel in use
+uint32_t post_image_lds(const pf::QPostHead* h) {
+    const int nl = h->n_tok + h->n_club + h->n_friend;
+    return use_slice() ? pf::slice_lds(h->n_tok, nl) : pf::post_lds(pf::post_var_lds(h->n_tok, nl));
+}
+int post_image_per_cu(const pf::QPostHead* h) {
+    const int nl = h->n_tok + h->n_club + h->n_friend;
+    return use_slice() ? pf::slice_blocks_per_cu(pf::slice_lds(h->n_tok, nl))
+                       : pf::post_blocks_per_cu(pf::post_var_lds(h->n_tok, nl));
+}
+// Slices per wave of a batched K5s launch (PF_DEBUG k5s_batch_slices=N, A/B)
+int batch_slices_per_wave() {
+    static const int n = (int)std::max(1L, pf::debug_long("k5s_batch_slices", 16));
     return n;
 }
 
@@ -336,8 +364,8 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     std::vector<int> pcu(nq), order(nq);
     for (int q = 0; q < nq; ++q) {
         const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[q]->data() + sizeof(pf::QConst));
-        vl[q] = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
-        pcu[q] = pf::post_blocks_per_cu(vl[q]);
+        vl[q] = use_slice() ? post_image_lds(h) : pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
+        pcu[q] = post_image_per_cu(h);
         order[q] = q;
     }
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pcu[a] > pcu[b]; });
@@ -357,8 +385,18 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // cover a few queries at a time and share their lists and cells in L2; with one resident
     // round looping over every query's range instead, 256 queries run at once and L2 hits
     // collapse (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
-    const int blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
-                               : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
+    const int64_t cand_begin = std::min<int64_t>((int64_t)c->wb_begin * c->ps.bsize, c->ps.n);
+    const int64_t cand_end = std::min<int64_t>((int64_t)c->wb_end * c->ps.bsize, c->ps.n);
+    const int64_t nslices = (cand_end - cand_begin + pf::slice_cands() - 1) / pf::slice_cands();
+    int blocks;
+    if (use_slice()) {
+        const int64_t waves = (nslices + batch_slices_per_wave() - 1) / batch_slices_per_wave();
+        blocks = nq == 1 ? std::max(1, one_query_wgs(c->num_cus * per_cu))
+                         : (int)std::max<int64_t>(1, (waves + pf::slice_waves() - 1) / pf::slice_waves());
+    } else {
+        blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
+                         : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
+    }
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
@@ -385,12 +423,20 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         int q1 = q0;
         uint32_t vmax = 0;
         while (q1 < nq && pcu[order[q1]] == pcu[order[q0]]) vmax = std::max(vmax, vl[order[q1++]]);
-        HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
-                                  nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
-                                  c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
-                                  reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
-                                  reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
-                                  (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
+        if (use_slice())
+            HIPCHK(c, pf::launch_slice(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
+                                       nq == 1 ? wave_lds : vmax, q1 - q0, (int)cand_begin, (int)cand_end, k, blocks,
+                                       c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
+                                       reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
+                                       reinterpret_cast<const int32_t*>(base + offs_b) + q0, slice_mode(),
+                                       (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
+        else
+            HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
+                                      nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
+                                      c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
+                                      reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
+                                      reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
+                                      (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
         q0 = q1;
     }
     if (timed) {
@@ -475,7 +521,7 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         ex.push_back(u);
         pf::build_query_post(c->hc, c->hp, i, ex, imgs[q]);
         const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[q].data() + sizeof(pf::QConst));
-        fits[q] = pf::post_lds(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend)) <= kK5LdsCap;
+        fits[q] = post_image_lds(h) <= kK5LdsCap;
     });
     std::vector<const std::vector<uint8_t>*> pi;
     std::vector<int32_t> prow, sidx, srow;
@@ -993,7 +1039,7 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
         ex.push_back(q[i]);
         pf::build_query_post(c->hc, c->hp, x, ex, imgs[i]);
         const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[i].data() + sizeof(pf::QConst));
-        kind[i] = pf::post_lds(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend)) <= kK5LdsCap ? 1 : 2;
+        kind[i] = post_image_lds(h) <= kK5LdsCap ? 1 : 2;
     }, 1);
     int nfit = 0, max_tok = 0, max_lists = 0;
     for (int i = 0; i < nq; ++i) {

@@ -147,6 +147,19 @@ __device__ __forceinline__ uint32_t record_words(const uint4& h2, bool packed) {
     return h2.y + h2.z + (packed ? h2.w : 2 * h2.w);
 }
 
+// ---------------------------------------------------------------- cross-workgroup hand-off
+// A workgroup publishes its k-list (agent-scope stores, drained by s_waitcnt vmcnt(0)) and then
+// takes a ticket; the holder of the last ticket reads every list (agent-scope loads).  The
+// ticket is an acquire-release RMW at agent scope, so the hand-off is ordered by the memory
+// model (release: the lists before the ticket; acquire: the reads after it), not only by the
+// hardware's issue order.  PF_TICKET_ORDER=__ATOMIC_RELAXED builds the relaxed form (A/B).
+#ifndef PF_TICKET_ORDER
+#define PF_TICKET_ORDER __ATOMIC_ACQ_REL
+#endif
+__device__ __forceinline__ unsigned int take_ticket(unsigned int* p) {
+    return __hip_atomic_fetch_add(p, 1u, PF_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- wave top-k
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);

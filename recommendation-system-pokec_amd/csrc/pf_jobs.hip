@@ -720,16 +720,14 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
     topk_push(list, live ? score_key((float)s, ids[J.out_off + c]) : ~0ull, k, cl);
     const int nb = (J.cap + kCollabCands - 1) / kCollabCands;
     uint64_t* jp = parts + (size_t)blockIdx.y * gridDim.x * k;
-    // Hand-off (MI355X_MICROARCH.md, the measured sc1 form, table row 1): ONE wave stores its list
-    // sc1 and waits for the stores, its lane 0 takes an agent-scope ticket, and the block whose
-    // ticket came last reads every list with sc1 loads in that same wave after the ticket returned.
-    // The compiler fences pin the program order of the stores, the ticket and the loads (no
-    // hardware fence: an agent release / acquire would write back / invalidate L1 and L2 per block).
+    // Hand-off (pf_device.h take_ticket): ONE wave stores its list sc1 and waits for the stores,
+    // its lane 0 takes an acquire-release agent-scope ticket, and the block whose ticket came last
+    // reads every list with sc1 loads in that same wave after the ticket returned.
     if (cl < k) st_agent64(jp + (size_t)blockIdx.x * k + cl, list);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     unsigned t = 0;
-    if (cl == 0) t = __hip_atomic_fetch_add(&tickets[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cl == 0) t = take_ticket(&tickets[blockIdx.y]);
     t = (unsigned)__shfl((int)t, 0);
     if (t != (unsigned)nb - 1u) return;
     __atomic_signal_fence(__ATOMIC_SEQ_CST);

@@ -220,7 +220,7 @@ constexpr int kRoundToks = 64;
 constexpr int kRoundCap = PF_K5_RCAP * kPostThreads;
 constexpr uint32_t kPostIdxLimit = 1u << 24;  // entry = idx << 8 | tf (tokens) or | multiplicity (sets)
 constexpr int kPostMaxCols = 48;           // header packs the column mask into 48 bits
-constexpr int kPostMinShift = 9;           // cells of >= 512 candidates: a block spans at most 3
+constexpr int kPostMinShift = 7;           // cells of >= 128 candidates (one K5s slice; a 512-block reads whole cells)
 
 // One candidate list: entries [off, off + len) of the postings array, sorted by idx.
 // cells[cell_off + c] = first entry (relative) with idx >= c << shift, c = 0 .. ncells,

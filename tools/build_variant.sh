@@ -1,5 +1,5 @@
 #!/bin/bash
-# Experiment build of the engine library into exp/v/<name>/libpokec_fas.so (selected at run time
+# Experiment build of the engine library into vlib/<name>/libpokec_fas.so (selected at run time
 # with PF_LIB_PATH): a copy of the package built with extra compiler flags, e.g.
 #   tools/build_variant.sh k5t K5T=1
 #   tools/build_variant.sh q8 XFLAGS=-DPF_QUEUE_EXTRA=8
@@ -7,10 +7,10 @@ set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
-mkdir -p "$tmp/pkg" "$root/exp/v/$name"
+mkdir -p "$tmp/pkg" "$root/vlib/$name"
 cp -r "$root/recommendation-system-pokec_amd/csrc" "$root/recommendation-system-pokec_amd/Makefile" "$tmp/pkg/"
 ln -s "$root/include" "$tmp/include"
 make -C "$tmp/pkg" -j8 libpokec_fas.so "$@" > "$tmp/build.log" 2>&1 || { tail -20 "$tmp/build.log"; exit 1; }
-cp "$tmp/pkg/libpokec_fas.so" "$root/exp/v/$name/"
+cp "$tmp/pkg/libpokec_fas.so" "$root/vlib/$name/"
 rm -rf "$tmp"
-echo "exp/v/$name/libpokec_fas.so"
+echo "vlib/$name/libpokec_fas.so"

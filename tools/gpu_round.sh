@@ -3,14 +3,15 @@
 # Steps (each under its own time limit, chained: the first failure ends the script):
 #   tests        full GPU suite                         -> gpurun_out/TAG/gputest.log
 #   tests:EXPR   GPU tests matching -k EXPR             -> gpurun_out/TAG/gputest_k.log
+#   testse:E     full GPU suite under PF_DEBUG=E        -> gpurun_out/TAG/gputest_e.log
 #   bench        default bench line (cfg 2, CPU baseline + PMC pass) -> bench.json
 #   prof         rocprofv3 kernel trace + stats of a 20-step cfg-2 run -> prof_default/
 #   cfgN         bench.py --workload cfgN               -> cfgN.json
 #   quick        cfg 2, 100 steps, no CPU baseline / PMC -> quick.json
 #   quick4       cfg 4, 3 steps, no CPU baseline / PMC   -> quick4.json
-#   quickv:V / quick4v:V  the same with the variant library exp/v/V (tools/build_variant.sh)
+#   quickv:V / quick4v:V  the same with the variant library vlib/V (tools/build_variant.sh)
 #   cfg5c1       cfg 5 at one context with the host stage clocks (PF_DEBUG host_prof=1) -> cfg5c1.err
-#   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> exp/v/k5t) per-phase K5 clocks -> k5t.err
+#   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> vlib/k5t) per-phase K5 clocks -> k5t.err
 #   pmc:NAME:C1,C2..  one rocprofv3 --pmc pass over a 20-step cfg-2 run -> pmc_NAME/
 set -o pipefail
 TAG=$1
@@ -23,6 +24,10 @@ for S in "$@"; do
     case $S in
     tests)
         timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || exit 1 ;;
+    testse:*)
+        # the full GPU suite under PF_DEBUG=SETTINGS (e.g. testse:k5_slice=1)
+        E=${S#testse:}
+        timeout -k 10 900 env PF_DEBUG=$E python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest_e.log 2>&1 || exit 1 ;;
     tests:*)
         timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${S#tests:}" > $O/gputest_k.log 2>&1 || exit 1 ;;
     bench)
@@ -45,10 +50,10 @@ for S in "$@"; do
         timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 $Q > $O/quick.json 2> $O/quick.err || exit 5 ;;
     quickv:*)
         V=${S#quickv:}
-        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --steps 100 --warmup 10 $Q > $O/quick_$V.json 2> $O/quick_$V.err || exit 5 ;;
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --steps 100 --warmup 10 $Q > $O/quick_$V.json 2> $O/quick_$V.err || exit 5 ;;
     quick4v:*)
         V=${S#quick4v:}
-        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4_$V.json 2> $O/quick4_$V.err || exit 6 ;;
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4_$V.json 2> $O/quick4_$V.err || exit 6 ;;
     quickd:*|quick4d:*)
         # the same quick lines from another tree (e.g. a git worktree of an older commit under exp/)
         D=${S#*:}; N=$(basename $D); W=""; [[ $S == quick4d:* ]] && W="--workload cfg4 --steps 3 --warmup 1" || W="--steps 100 --warmup 10"
@@ -76,13 +81,13 @@ for S in "$@"; do
         R=${S#rehearse:}; N=${R%%:*}; W=cfg4; [[ $R == *:* ]] && W=${R#*:}
         bash tools/rehearse_multi.sh $TAG $N $W || exit 11 ;;
     cfg3v:*)
-        # cfg3v:V  cfg 3 (30 steps) with the variant library exp/v/V
+        # cfg3v:V  cfg 3 (30 steps) with the variant library vlib/V
         V=${S#cfg3v:}
-        timeout -k 10 600 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg3 --steps 30 --warmup 5 $Q > $O/cfg3v_$V.json 2> $O/cfg3v_$V.err || exit 4 ;;
+        timeout -k 10 600 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --workload cfg3 --steps 30 --warmup 5 $Q > $O/cfg3v_$V.json 2> $O/cfg3v_$V.err || exit 4 ;;
     cfg5v:*)
-        # cfg5v:V  cfg 5 at one context with the variant library exp/v/V
+        # cfg5v:V  cfg 5 at one context with the variant library vlib/V
         V=${S#cfg5v:}
-        timeout -k 10 900 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5v_$V.json 2> $O/cfg5v_$V.err || exit 4 ;;
+        timeout -k 10 900 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --workload cfg5 --contexts 1 --steps 5 --warmup 2 $Q > $O/cfg5v_$V.json 2> $O/cfg5v_$V.err || exit 4 ;;
     cfg5e:*)
         # cfg5e:SETTINGS  cfg 5 at one context under PF_DEBUG=SETTINGS (e.g. chunks=6)
         E=${S#cfg5e:}
@@ -92,17 +97,17 @@ for S in "$@"; do
         K=5; [[ $S == cfg5c1:* ]] && K=${S#cfg5c1:}
         timeout -k 10 900 env PF_DEBUG=host_prof=1 python3 bench.py --workload cfg5 --contexts 1 --steps $K --warmup 2 $Q > $O/cfg5c1_$K.json 2> $O/cfg5c1_$K.err || exit 4 ;;
     k5t|k5t:*)
-        # profiling build (K5T=1) per-phase K5 clocks; k5t:V uses exp/v/V
+        # profiling build (K5T=1) per-phase K5 clocks; k5t:V uses vlib/V
         V=k5t; [[ $S == k5t:* ]] && V=${S#k5t:}
-        timeout -k 10 300 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/$V.json 2> $O/$V.err || exit 7 ;;
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --steps 30 --warmup 5 $Q > $O/$V.json 2> $O/$V.err || exit 7 ;;
     pmcpasses:*)
         # pmcpasses:KERNEL-REGEX  tools/pmc_passes.sh's five counter passes (TAG_KERNEL) over a short cfg-2 run
         K=${S#pmcpasses:}
         timeout -k 10 700 bash tools/pmc_passes.sh ${TAG}_$K $K || exit 8 ;;
     pmcv:*)
-        # pmcv:V:C1,C2..  one counter pass over 20 cfg-2 steps with the variant library exp/v/V (K5 rows only)
+        # pmcv:V:C1,C2..  one counter pass over 20 cfg-2 steps with the variant library vlib/V (K5 rows only)
         R=${S#pmcv:}; V=${R%%:*}; C=${R#*:}
-        timeout -s KILL 120 env PF_LIB_PATH=$PWD/exp/v/$V/libpokec_fas.so rocprofv3 --pmc ${C//,/ } --kernel-include-regex fas_post -d $O/pmcv_$V -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmcv_$V.json 2> $O/pmcv_$V.err || exit 8 ;;
+        timeout -s KILL 120 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so rocprofv3 --pmc ${C//,/ } --kernel-include-regex fas_post -d $O/pmcv_$V -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmcv_$V.json 2> $O/pmcv_$V.err || exit 8 ;;
     pmc:*)
         R=${S#pmc:}; N=${R%%:*}; C=${R#*:}
         timeout -s KILL 120 rocprofv3 --pmc ${C//,/ } -d $O/pmc_$N -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmc_$N.json 2> $O/pmc_$N.err || exit 8 ;;

@@ -762,6 +762,63 @@ def run_cfg5(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def solo_shards(args, eng, pf, torch, qstream, warm, steps, Q, k, n_cand, stream, n1_ms):
+    """A one-GPU projection of cfg 4's N-GPU strong scaling (no multi-GPU node needed): each of the
+    S shards pf_set_shard(r, S) gives a rank, timed ALONE on this whole GPU over the same 1,024-query
+    steps; the projected N = S step is the slowest shard + the cross-shard merge (timed here on S
+    gathered key lists) + an all-gather estimate for S x Q x k x 8 B over xGMI.  What does not divide
+    by S shows as sum(shard ms) - the N = 1 step: per-query costs every shard pays again (the query
+    image staged per workgroup, the fused merge, the launch)."""
+    S = args.solo_shards
+    sptr = stream.cuda_stream
+    out = torch.empty((Q, k), dtype=torch.int64, device="cuda")
+    ns = max(1, min(steps, args.solo_steps))
+    per = []
+    for r in range(S):
+        eng.set_shard(r, S)
+        eng.scan_keys_async(qstream[0], k, out.data_ptr(), sptr)  # warm this shard's launch shape
+        torch.cuda.synchronize()
+        eng.profile_sample(1)
+        eng.profile_reset()
+        ta = time.perf_counter()
+        for i in range(warm, warm + ns):
+            eng.scan_keys_async(qstream[i], k, out.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - ta) * 1e3 / ns
+        kms, nl = eng.profile_read()
+        eng.profile_sample(0)
+        lay = eng.layout()
+        per.append({"shard": r, "ms_per_step": wall, "kernel_ms": kms / nl if nl else None,
+                    "shard_cands": int(lay.shard_cands), "shard_entries": int(lay.shard_entries)})
+    eng.set_shard(0, 1)
+    # the merge of S gathered lists (pf_merge_keys_async, the N = S step's last kernel), timed alone
+    gathered = torch.full((S, Q, k), -1, dtype=torch.int64, device="cuda")
+    for r in range(S):
+        gathered[r].copy_(out)
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    reps = 20
+    for _ in range(reps):
+        eng.merge_keys_async(gathered.data_ptr(), S, Q, k, out.data_ptr(), sptr)
+    torch.cuda.synchronize()
+    merge_ms = (time.perf_counter() - ta) * 1e3 / reps
+    # all-gather estimate: a ring moves (S - 1) / S of the S x Q x k x 8 B per rank over one xGMI link
+    # (~50 GB/s achieved of 153 GB/s peak per direction), plus ~25 us of collective latency
+    ag_bytes = S * Q * k * 8
+    ag_ms = 0.025 + (S - 1) / S * ag_bytes / 50e9 * 1e3
+    ms = [x["ms_per_step"] for x in per]
+    proj = max(ms) + merge_ms + ag_ms
+    return {"shards": S, "steps_per_shard": ns, "per_shard": per,
+            "shard_ms_max_over_mean": max(ms) / (sum(ms) / S),
+            "merge_ms": merge_ms, "allgather_ms_estimate": ag_ms, "allgather_bytes": ag_bytes,
+            "n1_ms_per_step": n1_ms, "sum_shard_ms": sum(ms),
+            "non_dividing_ms": sum(ms) - n1_ms,
+            "projected_ms_per_step": proj, "projected_value": Q * n_cand / (proj * 1e-3),
+            "projected_speedup_vs_n1": n1_ms / proj,
+            "note": "each shard timed alone on one whole GPU (the rank's work at N = S); projected N = S step = "
+                    "max shard + merge (timed) + all-gather (estimated); not a multi-GPU measurement"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -802,6 +859,10 @@ def main():
                     help="cfg2 at N = 1: skip the cfg-3 sub-record (collaborative FoF top-10, 64 users per step)")
     ap.add_argument("--cfg3-steps", type=int, default=50,
                     help="timed steps of the cfg-3 sub-record (with 5 warmup steps: the query stream of --workload cfg3)")
+    ap.add_argument("--solo-shards", type=int, default=0,
+                    help="cfg4 at N = 1: also time each of S shards alone on this GPU and project the N = S "
+                         "step (solo_shards record)")
+    ap.add_argument("--solo-steps", type=int, default=3, help="timed steps per shard of --solo-shards")
     ap.add_argument("--n1-steps", type=int, default=5,
                     help="N > 1: steps rank 0 times the same workload unsharded on its own GPU (n1_same_workload)")
     args = ap.parse_args()
@@ -1042,6 +1103,9 @@ def main():
         rec["speedup_vs_cpu"] = value / base["value"] if base.get("value") else None
     elif rank == 0:
         rec["cpu_baseline"] = None
+    if cfg4 and world == 1 and args.solo_shards > 1:
+        rec["solo_shards"] = solo_shards(args, eng, pf, torch, qstream, warm, steps, Q, k, n_cand, stream,
+                                         elapsed * 1e3 / steps)
     if sub3:
         # cfg 3 (BASELINE configs[2]) on the same engine: recommend_collaborative(u, 10, 10000) for
         # 64 seeded users per step, one engine context (the default line's own replica)

@@ -187,6 +187,11 @@ int pf_recommend_clubs_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq, 
                              int32_t candidate_limit, int32_t* out_uid, float* out_score,
                              int32_t* out_count, uint64_t* ticket);
 int pf_wait(pf_ctx* ctx, uint64_t ticket);
+/* The highest ticket whose call has completed (its outputs written): every ticket <= it is
+ * done, by pf_wait or by another call that completed the pending ones first.  0 when no
+ * asynchronous call has completed (or ctx is NULL).  Bindings drop their references to a
+ * call's output buffers once its ticket is <= this. */
+uint64_t pf_completed_ticket(const pf_ctx* ctx);
 
 /* Ordered, de-duplicated, limit-truncated 2-hop candidate list of uid
  * (flavour PF_FOF_GRAPH or PF_FOF_COLLAB).  Writes at most `cap` ids; *n gets

@@ -924,6 +924,12 @@ int pf_wait(pf_ctx* c, uint64_t ticket) {
     return pf::jobs_wait(c, ticket);
 }
 
+uint64_t pf_completed_ticket(const pf_ctx* c) {
+    if (!c) return 0;
+    // tickets are handed out in launch order and completed in launch order
+    return c->jb.pending.empty() ? c->jb.next_ticket - 1 : c->jb.pending.front().ticket - 1;
+}
+
 int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {
     if (!c || !n || (cap > 0 && !out)) return PF_EINVAL;
     if (flavour != PF_FOF_GRAPH && flavour != PF_FOF_COLLAB) return PF_EINVAL;

@@ -11,12 +11,15 @@
 #include <cstdlib>
 #include <cstdint>
 #include <deque>
+#include <exception>
 #include <string>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <utility>
 #include <vector>
+
+#include <unistd.h>
 
 #include "pf_batch.h"
 #include "pf_jobs.h"
@@ -266,9 +269,23 @@ namespace pf {
 // chunk: three chunks per cfg-5 step.)
 class WorkPool {
   public:
+    // Leaked on purpose (workers outlive static destruction).  A process forked after first use
+    // has no workers (only the forking thread survives a fork): it gets a pool of its own.
     static WorkPool& get() {
-        static WorkPool* p = new WorkPool();  // leaked on purpose: workers outlive static destruction
-        return *p;
+        static std::atomic<WorkPool*> pool{nullptr};
+        static std::atomic<pid_t> owner{0};
+        const pid_t me = getpid();
+        WorkPool* w = pool.load(std::memory_order_acquire);
+        if (w && owner.load(std::memory_order_relaxed) == me) return *w;
+        static std::mutex gm;
+        std::lock_guard<std::mutex> g(gm);
+        w = pool.load(std::memory_order_acquire);
+        if (!w || owner.load(std::memory_order_relaxed) != me) {
+            w = new WorkPool();
+            owner.store(me, std::memory_order_relaxed);
+            pool.store(w, std::memory_order_release);
+        }
+        return *w;
     }
     int workers() const { return (int)ts_.size(); }
     // fn(i) for i in [0, n), on the caller and up to `helpers` workers
@@ -290,6 +307,8 @@ class WorkPool {
         }
         std::unique_lock<std::mutex> g(t.m);
         t.cv.wait(g, [&] { return t.active == 0; });
+        // every worker has left the task (it lives on this stack): only now rethrow an item's error
+        if (t.err) std::rethrow_exception(t.err);
     }
 
   private:
@@ -299,11 +318,20 @@ class WorkPool {
         std::atomic<size_t> next{0};
         int slots = 0;   // workers that may still join (under mu_)
         int active = 0;  // workers inside (under m)
+        std::exception_ptr err;  // the first item's exception (under m); the other items are skipped
         std::mutex m;
         std::condition_variable cv;
     };
     static void work(Task& t) {
-        for (size_t i; (i = t.next.fetch_add(1)) < t.n;) (*t.fn)(i);
+        for (size_t i; (i = t.next.fetch_add(1)) < t.n;) {
+            try {
+                (*t.fn)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(t.m);
+                if (!t.err) t.err = std::current_exception();
+                t.next.store(t.n);
+            }
+        }
     }
     WorkPool() {
         const int n = (int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()) - 1u);

@@ -147,17 +147,50 @@ __device__ __forceinline__ uint32_t record_words(const uint4& h2, bool packed) {
     return h2.y + h2.z + (packed ? h2.w : 2 * h2.w);
 }
 
+// ---------------------------------------------------------------- wave scans
+// Inclusive prefix sum of one u32 per lane over the wave by DPP (row shifts 1, 2, 4, 8 inside each
+// 16-lane row, then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3): six VALU
+// steps with no LDS round trip (a __shfl_up ladder is six dependent ds_bpermute's).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_last(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+
 // ---------------------------------------------------------------- cross-workgroup hand-off
-// A workgroup publishes its k-list (agent-scope stores, drained by s_waitcnt vmcnt(0)) and then
-// takes a ticket; the holder of the last ticket reads every list (agent-scope loads).  The
-// ticket is an acquire-release RMW at agent scope, so the hand-off is ordered by the memory
-// model (release: the lists before the ticket; acquire: the reads after it), not only by the
-// hardware's issue order.  PF_TICKET_ORDER=__ATOMIC_RELAXED builds the relaxed form (A/B).
-#ifndef PF_TICKET_ORDER
-#define PF_TICKET_ORDER __ATOMIC_ACQ_REL
+// A workgroup publishes its k-list (agent-scope sc1 stores, drained by s_waitcnt vmcnt(0)) and
+// then takes a ticket; the holder of the last ticket reads every list (agent-scope sc1 loads).
+// PF_TICKET_MODE selects the ticket's ordering:
+//   0 (default) relaxed ticket, no fence: the lists reach the coherence point before the ticket
+//     is issued (the wait) and the reads are issued after it returns (a data dependence), so the
+//     hand-off is ordered by the hardware's issue order; tests/test_gpu_parity.py
+//     test_fused_topk_hand_off_stress compares thousands of fused merges with K8's ranking;
+//   1 release ticket, and the last ticket's holder alone runs an agent acquire fence before its
+//     reads (ticket_acquire): ordered by the memory model; K5 185.0 / 185.7 vs 179.6 us per
+//     cfg-2 launch relaxed (r6d, one box: buffer_wbl2 per workgroup, buffer_inv per merge);
+//   2 acquire-release ticket: 186.3 us.
+#ifndef PF_TICKET_MODE
+#define PF_TICKET_MODE 0
 #endif
 __device__ __forceinline__ unsigned int take_ticket(unsigned int* p) {
-    return __hip_atomic_fetch_add(p, 1u, PF_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT);
+#if PF_TICKET_MODE == 2
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#elif PF_TICKET_MODE == 1
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+// the last ticket's holder, before it reads the published lists
+__device__ __forceinline__ void ticket_acquire() {
+#if PF_TICKET_MODE == 1
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
 }
 
 // ---------------------------------------------------------------- wave top-k

@@ -91,11 +91,7 @@ template <int NW = kJobWaves>
 __device__ __forceinline__ int block_scan_incl(int v, int* wsum, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
+    x = (int)wave_incl_scan((uint32_t)x);
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
     int before = 0;
@@ -350,10 +346,7 @@ __global__ __launch_bounds__(kGatherThreads) void gather_kernel(DevJobsStore g, 
 #pragma unroll
             for (int k = 0; k < 4; ++k) { v[k] = hist[tid * 4 + k]; t += v[k]; }
             int x = t;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(x, o);
-                if (tid >= o) x += y;
-            }
+            x = (int)wave_incl_scan((uint32_t)x);
             int run = x - t;
 #pragma unroll
             for (int k = 0; k < 4; ++k) { hist[tid * 4 + k] = run; run += v[k]; }
@@ -420,10 +413,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_pairs_kernel(const PairBl
             t += v[u];
         }
         int x = t;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (tid >= o) x += y;
-        }
+        x = (int)wave_incl_scan((uint32_t)x);
         int run = x - t;
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
@@ -730,6 +720,7 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
     if (cl == 0) t = take_ticket(&tickets[blockIdx.y]);
     t = (unsigned)__shfl((int)t, 0);
     if (t != (unsigned)nb - 1u) return;
+    ticket_acquire();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     uint64_t acc = ~0ull;
     const int n = nb * k;
@@ -750,12 +741,8 @@ constexpr int kClubBuf = 512;  // contributions per round (LDS: 2 x 12 B each)
 
 __device__ __forceinline__ int wave_excl_prefix(int x, int lane, int& total) {
     int v = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o);
-        if (lane >= o) v += y;
-    }
-    total = __shfl(v, 63);
+    v = (int)wave_incl_scan((uint32_t)v);
+    total = (int)wave_last((uint32_t)v);
     return v - x;
 }
 

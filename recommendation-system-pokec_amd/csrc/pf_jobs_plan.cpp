@@ -442,10 +442,21 @@ int jobs_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
 
 namespace {
 
+// Before a graph / view upload rewrites buffers the device may still read: the context's stream
+// waits for every pending asynchronous call's last work (W.done, recorded on aux2 after its K7,
+// the clubs jobs' K8 and the result copies), which nothing on the context's stream orders.
+int wait_pending_on_stream(pf_ctx* c) {
+    auto& J = c->jb;
+    for (const auto& p : J.pending)
+        if (J.ws[p.slot].done) HIPCHK(c, hipStreamWaitEvent(c->stream, J.ws[p.slot].done, 0));
+    return PF_OK;
+}
+
 // the node arrays grew (pf_set_adj named new uids): upload them again
 int sync_nodes(pf_ctx* c) {
     auto& J = c->jb;
     if (!J.nodes_dirty) return PF_OK;
+    if (const int rc = wait_pending_on_stream(c); rc != PF_OK) return rc;
     const int32_t M = (int32_t)J.g_uid.size();
     std::vector<int64_t> off(M, 0);  // the new nodes have no base row
     std::vector<int64_t> old((size_t)J.js.M);
@@ -487,6 +498,7 @@ int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, st
             es.push_back(E{node_of(c, kv.first), kv.second.first, (int32_t)kv.second.second.size(), &kv.second.second});
     for (const E& x : es)
         if (x.node < 0) return c->fail(PF_EINTERNAL, "adjacency override names an unmapped uid");
+    if (const int rc = wait_pending_on_stream(c); rc != PF_OK) return rc;
     std::sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.node != b.node ? a.node < b.node : a.ver > b.ver; });
     std::vector<int32_t> node(es.size()), ver(es.size()), len(es.size()), nbr;
     std::vector<int64_t> off(es.size());

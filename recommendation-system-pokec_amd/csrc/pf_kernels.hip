@@ -507,12 +507,8 @@ __device__ __forceinline__ float pair_epilogue(const QView& v, const DevStore& s
     const bool fr_it = dense && q.n_friends > 0 && nf > 0 && ifr > 0;
     const uint32_t nit = dense ? ncol + (club_it ? 1u : 0u) + (fr_it ? 1u : 0u) : 0u;
     uint32_t x = nit;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
-    const uint32_t base = x - nit, total = (uint32_t)__shfl((int)x, 63);
+    x = wave_incl_scan(x);
+    const uint32_t base = x - nit, total = wave_last(x);
     constexpr uint32_t kQueue = kHitSlots * 64u / 4u;
     // A wave whose items exceed the queue takes two rounds: the lanes whose items end within it
     // (a prefix of the lanes) first, then the others from the queue's start; only a second round
@@ -866,6 +862,7 @@ __device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, in
     }
     __syncthreads();
     if (!misc[0]) return;
+    ticket_acquire();
     // the group's lists: workgroups g, g + ng, ... (n_g * k keys over the waves, 4 loads in flight)
     {
         uint64_t l2 = ~0ull;
@@ -897,6 +894,7 @@ __device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, in
         if (lane == 0) t = take_ticket(&sy->done);
         t = (unsigned)__shfl((int)t, 0);
         if (t == (unsigned)ng - 1u) {
+            ticket_acquire();
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             uint64_t fin = ~0ull;
             const int n = ng * k;
@@ -1127,13 +1125,9 @@ __device__ __forceinline__ void wave_prefix(uint32_t* gpre, const uint2* rng, in
         const int j = b + lane;
         const uint32_t len = j < nl ? rng[j].y - rng[j].x : 0u;
         uint32_t x = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-            if (lane >= o) x += y;
-        }
+        x = wave_incl_scan(x);
         if (j < nl) gpre[j] = carry + x - len;
-        carry += (uint32_t)__shfl((int)x, 63);
+        carry += wave_last(x);
     }
     if (lane == 0) gpre[nl] = carry;
 }
@@ -1171,12 +1165,7 @@ __device__ __forceinline__ void build_map(uint64_t* mb, uint8_t* mc, uint2* mn, 
         mn[k] = make_uint2(rng[j].x - s, (uint32_t)lane);
     }
     wave_sync();
-    uint32_t c = lane < kMW ? (uint32_t)__popcll(mb[lane]) : 0u, x = c;
-#pragma unroll
-    for (int o = 1; o < kMW; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
+    const uint32_t c = lane < kMW ? (uint32_t)__popcll(mb[lane]) : 0u, x = wave_incl_scan(c);
     if (lane < kMW) mc[lane] = (uint8_t)(x - c);
 }
 
@@ -1514,12 +1503,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     tot += nk[kk];
                 }
                 uint32_t incl = tot;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-                    if (lane >= o) incl += y;
-                }
-                const uint32_t wn = (uint32_t)__shfl((int)incl, 63);
+                incl = wave_incl_scan(incl);
+                const uint32_t wn = wave_last(incl);
                 uint32_t wb = 0;
                 if (lane == 0) wb = atomicAdd(&misc[1], wn);
                 wb = (uint32_t)__shfl((int)wb, 0);
@@ -2059,12 +2044,8 @@ __global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
                     tot += nk[kk];
                 }
                 uint32_t incl = tot;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-                    if (lane >= o) incl += y;
-                }
-                const uint32_t wn = (uint32_t)__shfl((int)incl, 63);
+                incl = wave_incl_scan(incl);
+                const uint32_t wn = wave_last(incl);
                 {
                     uint32_t h0 = incl - tot;
 #pragma unroll

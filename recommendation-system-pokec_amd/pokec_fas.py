@@ -28,7 +28,7 @@ EXPORTS = ["pf_abi_version", "pf_open", "pf_close", "pf_last_error", "pf_num_use
            "pf_set_shard", "pf_scan_keys_async", "pf_merge_keys_async", "pf_decode_keys", "pf_layout",
            "pf_last_scan_ms", "pf_profile_reset", "pf_profile_read", "pf_profile_sample", "pf_set_scan_kernel",
            "pf_scan_bytes", "pf_jobs_stats_reset", "pf_jobs_stats_read", "pf_recommend_interest_async",
-           "pf_recommend_collab_async", "pf_recommend_clubs_async", "pf_wait"]
+           "pf_recommend_collab_async", "pf_recommend_clubs_async", "pf_wait", "pf_completed_ticket"]
 # include/pokec_io.h: loaders and hold-out drivers
 IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "pf_dataset_desc", "pf_dataset_info_get", "pf_dataset_column",
               "pf_dataset_profile_order", "pf_dataset_adj_order", "pf_dataset_profile_json", "pf_dataset_club_name",
@@ -100,6 +100,8 @@ def lib():
         for fn in ("pf_recommend_interest_async", "pf_recommend_collab_async", "pf_recommend_clubs_async"):
             getattr(L, fn).argtypes = [V, V, I32, I32, I32, V, V, V, ctypes.POINTER(ctypes.c_uint64)]
         L.pf_wait.argtypes = [V, ctypes.c_uint64]
+        L.pf_completed_ticket.argtypes = [V]
+        L.pf_completed_ticket.restype = ctypes.c_uint64
         L.pf_set_adj.argtypes = [V, I32, V, I32]
         L.pf_set_shard.argtypes = [V, I32, I32]
         L.pf_set_scan_kernel.argtypes = [V, I32]
@@ -206,6 +208,7 @@ class FasEngine:
         oc = np.zeros(max(len(q), 1), np.int32)
         self._check(getattr(self._L, fn)(self.h, q.ctypes.data, len(q), k, *extra, ou.ctypes.data,
                                          os_.ctypes.data, oc.ctypes.data), fn)
+        self._prune_inflight()
         return [(ou[i * k:i * k + oc[i]].copy(), os_[i * k:i * k + oc[i]].copy()) for i in range(len(q))]
 
     # -- asynchronous calls (pokec_fas.h): the handle keeps the output arrays alive until wait()
@@ -234,6 +237,14 @@ class FasEngine:
 
     def recommend_clubs_collab_async(self, users, topk, candidate_limit=10000):
         return self._topk_async("pf_recommend_clubs_async", users, topk, candidate_limit)
+
+    def _prune_inflight(self):
+        """Drop the output arrays of calls the engine has completed (a synchronous call completes
+        every pending one first), so callers that never wait() do not keep them alive."""
+        if self._inflight:
+            done = int(self._L.pf_completed_ticket(self.h))
+            for t in [t for t in self._inflight if t <= done]:
+                del self._inflight[t]
 
     def wait(self, p):
         """Results of an asynchronous call (and of every earlier one), as the synchronous form's."""

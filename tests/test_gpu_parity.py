@@ -655,6 +655,55 @@ def test_full_size_kernels_agree(full):
             assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32)), (world, kern, q[i])
 
 
+def test_full_size_batch_1024(full):
+    """BASELINE cfg 4's launch shape at full size: ONE batched postings-scan call of 1,024 seeded
+    queries over the 1,632,803-user corpus (the query-major batch grid, LDS-class launches) against
+    the record-stream scan (K1, an independent kernel) for every query (ids and score bits), and
+    against the oracle (the reference algorithm, recommender_graph.cpp:46-52,97-101 per query) for
+    three of them."""
+    c, eng, oracle = full
+    rng = np.random.default_rng(44)
+    q = [int(x) for x in rng.integers(1, 1632804, 1024)]
+    k = 10
+    eng.set_scan_kernel(2)
+    post = eng.recommend_interest_all(q, k)
+    eng.set_scan_kernel(1)
+    stream = eng.recommend_interest_all(q, k)
+    eng.set_scan_kernel(0)
+    bad = [u for u, p, s in zip(q, post, stream)
+           if list(p[0]) != list(s[0]) or not np.array_equal(p[1].view(np.uint32), s[1].view(np.uint32))]
+    assert not bad, (len(bad), bad[:5])
+    assert all(len(p[0]) == k for p in post)
+    picks = [0, 511, 1023]
+    ref = oracle().interest([q[i] for i in picks], k, tl.PF_MODE_ALL, 0)
+    for i, r in zip(picks, ref):
+        assert list(post[i][0]) == list(r[0]), q[i]
+        assert np.array_equal(post[i][1].view(np.uint32), r[1].view(np.uint32)), q[i]
+
+
+def test_fused_topk_hand_off_stress(full):
+    """The collaborative kernel's fused top-k (K4': every 64-candidate block publishes its k best,
+    the last ticket's holder merges; pf_device.h take_ticket, relaxed by default) against K8's
+    ranking of the same scores (topk > 64 leaves the ranking to K8): 2,048 seeded users at limit
+    10,000 on the full corpus (cfg 3's configuration), thousands of multi-block jobs, every fused
+    list equal to K8's first ten (ids and score bits)."""
+    c, eng, _ = full
+    uid, off, _ = _adjacency(c.desc_ptr())
+    deg = np.diff(off)
+    rng = np.random.default_rng(57)
+    users = [int(x) for x in rng.choice(uid[(deg > 0) & (uid >= 1)], 2048, replace=False)]
+    fused = eng.recommend_collaborative(users, 10, 10000)
+    ranked = eng.recommend_collaborative(users, 65, 10000)
+    multi = 0
+    for u, f, r in zip(users, fused, ranked):
+        n = min(10, len(r[0]))
+        assert len(f[0]) == n, u
+        assert list(f[0]) == list(r[0][:n]), u
+        assert np.array_equal(f[1].view(np.uint32), r[1][:n].view(np.uint32)), u
+        multi += len(r[0]) == 65  # at least 65 candidates: more than one 64-candidate block
+    assert multi >= 1000, multi
+
+
 def _adjacency(ptr):
     """(adj_uid, adj_off, adj_nbr) views of a pf_corpus_desc (no copy)."""
     import ctypes

@@ -1169,6 +1169,28 @@ __device__ __forceinline__ void build_map(uint64_t* mb, uint8_t* mc, uint2* mn, 
     if (lane < kMW) mc[lane] = (uint8_t)(x - c);
 }
 
+// A term item: the slot of a (candidate, column)'s first hit in the round and the column's hit
+// count there (kItemRunMax: count the run by the hit flags instead)
+constexpr uint32_t kItemRunShift = 11, kItemSlotMask = (1u << kItemRunShift) - 1u, kItemRunMax = 31;
+static_assert(kRoundCap <= (int)kItemSlotMask + 1, "item slots fit 11 bits");
+// hits of a candidate's column segment [lo, hi) of the round (its mask's bits there), capped
+__device__ __forceinline__ uint32_t hit_run(uint64_t m, uint32_t lo, uint32_t hi) {
+    return min((uint32_t)__popcll((m >> lo) & low_bits(hi - lo)), kItemRunMax);
+}
+// dot + slot[r + 1] + ... + slot[r + run - 1], added in that order (recommender.cpp:74-85 sums a
+// column's products one by one): the reads are independent, four issued ahead of the adds
+__device__ __forceinline__ double run_dot(const double* slot, uint32_t r, uint32_t run, double dot) {
+    for (uint32_t k = 1; k < run; k += 4) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = k + u < run ? slot[r + k + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k + u < run) dot += v[u];
+    }
+    return dot;
+}
+
 // product of one shared token, recommender.cpp:74-85: wA * wB, wB = tf * idf
 __device__ __forceinline__ double tok_product(const PTok* pt, int j, uint32_t tf) {
     const PTok v = pt[j];
@@ -1526,12 +1548,14 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const uint32_t p = kp[u] & 1023u, jr = (kp[u] >> 10) & 63u, tf = kp[u] >> 16;
                     const uint64_t below = mask[p] & low_bits(jr);
                     const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 8);
-                    const uint32_t lo = seg[jr] & 0xFFu;
+                    const uint32_t sg = seg[jr], lo = sg & 0xFFu;
                     const bool first = (below >> lo) == 0ull;
                     hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     // the column's first hit holds its norm, the others their product (one per lane here,
-                    // so the terms below only add them up)
+                    // so the terms below only add them up); the first also records its column's hit count
+                    // in the round (item[r], read once by the compaction below)
                     slot[r] = first ? kn[u] : tok_product(pt, ja + (int)jr, tf);
+                    if (first) item[r] = (uint16_t)hit_run(mask[p], lo, (sg >> 8) & 0xFFu);
                 }
                 for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {
                     const int j = round_list(gpre, ja, jb, g0 + f);
@@ -1542,9 +1566,11 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const uint32_t jr = (uint32_t)(j - ja);
                     const uint64_t below = mask[p] & low_bits(jr);
                     const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 9);
-                    const bool first = (below >> (seg[jr] & 0xFFu)) == 0ull;
+                    const uint32_t sg = seg[jr];
+                    const bool first = (below >> (sg & 0xFFu)) == 0ull;
                     hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     slot[r] = first ? ps.pnorm[x] : tok_product(pt, ja + (int)jr, e & 0xFFu);
+                    if (first) item[r] = (uint16_t)hit_run(mask[p], sg & 0xFFu, (sg >> 8) & 0xFFu);
                 }
                 K5T(7);
                 __syncthreads();
@@ -1553,34 +1579,44 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 {
                 // the wave's items (first hits of whole columns; the owner carries a split column),
                 // compacted so the terms run on dense lanes
+                // (in place: an item is written at or below the slot it was read from, after the read)
                 uint16_t* wit = item + wb;
                 uint32_t ni = 0;
                 for (uint32_t r0 = wb; r0 < wb + wn; r0 += 64) {
                     const uint32_t r = r0 + (uint32_t)lane;
                     bool is = false;
+                    uint32_t run = 0;
                     if (r < wb + wn) {
                         const uint32_t h = hit[r];
+                        run = item[r];
                         is = (h & kHitFirst) && !(seg[(h >> 8) & 63u] & kSegSplit);
                     }
                     const uint64_t bal = __ballot(is);
-                    if (is) wit[ni + (uint32_t)__popcll(bal & low_bits((uint32_t)lane))] = (uint16_t)r;
+                    wave_sync();
+                    if (is) wit[ni + (uint32_t)__popcll(bal & low_bits((uint32_t)lane))] = (uint16_t)(r | run << kItemRunShift);
                     ni += (uint32_t)__popcll(bal);
                 }
                 wave_sync();
                 for (uint32_t i = (uint32_t)lane; i < ni; i += 64) {
-                    const uint32_t r = wit[i];
+                    const uint32_t it = wit[i];
+                    const uint32_t r = it & kItemSlotMask, run = it >> kItemRunShift;
                     const uint32_t h = hit[r];
                     const uint32_t jr = (h >> 8) & 63u, sg = seg[jr];
-                    const uint32_t hi = (sg >> 8) & 0xFFu;
                     const int t = (int)((sg >> 16) & 0xFFu);
+                    const double nrm = slot[r];
                     double dot = tok_product(pt, ja + (int)jr, h & 0xFFu);
-                    for (uint32_t r2 = r + 1; r2 < wb + wn; ++r2) {  // the column's further hits, tid ascending
-                        const uint32_t h2 = hit[r2];
-                        const uint32_t j2 = (h2 >> 8) & 63u;
-                        if ((h2 & kHitCand) || j2 >= hi) break;
-                        dot += slot[r2];  // the hit's product (placed above)
+                    if (run < kItemRunMax) {
+                        dot = run_dot(slot, r, run, dot);  // the column's further hits, tid ascending
+                    } else {  // a long run (>= kItemRunMax hits): walk it by the hit flags
+                        const uint32_t hi = (sg >> 8) & 0xFFu;
+                        for (uint32_t r2 = r + 1; r2 < wb + wn; ++r2) {
+                            const uint32_t h2 = hit[r2];
+                            const uint32_t j2 = (h2 >> 8) & 63u;
+                            if ((h2 & kHitCand) || j2 >= hi) break;
+                            dot += slot[r2];
+                        }
                     }
-                    slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, slot[r]);
+                    slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, nrm);
                 }
                 }
                 wave_sync();
@@ -2076,9 +2112,11 @@ __global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
                     const uint32_t jr = (uint32_t)(j - ja);
                     const uint64_t below = mask[p] & low_bits(jr);
                     const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kSliceRcap, 9);
-                    const bool first = (below >> (seg[jr] & 0xFFu)) == 0ull;
+                    const uint32_t sg = seg[jr];
+                    const bool first = (below >> (sg & 0xFFu)) == 0ull;
                     hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     slot[r] = first ? ps.pnorm[x] : tok_product(pt, ja + (int)jr, e & 0xFFu);
+                    if (first) item[r] = (uint16_t)hit_run(mask[p], sg & 0xFFu, (sg >> 8) & 0xFFu);
                 }
                 wave_sync();
                 K5T(8);

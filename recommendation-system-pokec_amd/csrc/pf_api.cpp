@@ -268,6 +268,15 @@ uint32_t post_mode(int nq) {
     return nq == 1 ? ((st ? 0u : 1u) | x) : (tr ? 2u : x);
 }
 
+// Candidates per claimed block past a one-query K5 launch's static rounds (PF_DEBUG k5_tail=N,
+// A/B; 0 or >= the block size: whole blocks).  r6g, one box: whole blocks 177.0 us, 256 177.2,
+// 128 177.5 / 178.6, 64 180.2: the claimed tail is not where a launch loses time
+
+uint32_t tail_block_cands() {
+    static const long n = pf::debug_long("k5_tail", 0);
+    return (uint32_t)std::max(0L, n);
+}
+
 // K5s mode word: bit 0 = claimed slices past each wave's first (PF_DEBUG k5s_static=1: static)
 uint32_t slice_mode() {
     static const bool st = pf::debug_long("k5s_static", 0) != 0;
@@ -436,7 +445,8 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
                                       c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
                                       reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
                                       reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
-                                      (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
+                                      tail_block_cands(), (timed && q0 == 0) ? e0 : nullptr,
+                                      (timed && q1 == nq) ? e1 : nullptr, s));
         q0 = q1;
     }
     if (timed) {

@@ -1247,7 +1247,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                                                               const uint32_t* __restrict__ img_off, int32_t blk_begin,
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-                                                              const int32_t* __restrict__ out_rows, uint32_t mode) {
+                                                              const int32_t* __restrict__ out_rows, uint32_t mode,
+                                                              uint32_t tail_bs) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // mode bit 1 (batches): the grid is transposed, blockIdx.x = the query and blockIdx.y = the block
     // group, so the workgroups resident at once are many queries on the same candidate blocks and
@@ -1320,9 +1321,15 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // or (mode bit 0) the next unclaimed block of the query from a counter in its ScanSync, so the
     // blocks past the first resident round go to the workgroups that finish first.
     unsigned int* next_blk = &sync[qy].next;
-    // dynamic mode (one query): whole static rounds of nbx blocks, then the tail blocks by claim
+    // dynamic mode (one query): whole static rounds of nbx blocks, then the rest of the range by
+    // claim, in blocks of tail_bs candidates: the ~117 blocks past three static rounds of a cfg-2
+    // launch would run on ~11 % of the workgroups; cut four times finer they spread over ~470
     const int tail = (mode & 1u) ? blk_begin + max(1, (blk_end - blk_begin) / nbx) * nbx : blk_end;
     const uint32_t B = (uint32_t)ps.bsize;
+    const uint32_t cend = min((uint32_t)blk_end * B, (uint32_t)ps.n);  // the range's end
+    const uint32_t tbs = (tail_bs > 0u && tail_bs < B) ? tail_bs : B;
+    const uint32_t cst = min((uint32_t)tail * B, cend);                 // the claimed part's start
+    const int blk_last = tail + (int)((cend - cst + tbs - 1) / tbs);
     const bool short_excl = H.n_excl <= kPostThreads;
     const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;  // the query's, once
     // mode bit 2 (one query, query-major batches): the workgroups of XCD x (bx mod 8 under the
@@ -1330,9 +1337,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // static round, so a list segment's boundary cache lines are shared inside one L2 instead of
     // fetched by two XCDs (cfg 2 PMC traffic 236 -> 175 MB per launch, r4w -> r5h)
     const int pb = ((mode & 4u) && (nbx & 7) == 0) ? (bx & 7) * (nbx >> 3) + (bx >> 3) : bx;
-    for (int blk = blk_begin + pb; blk < blk_end;) {
-        const uint32_t c0 = (uint32_t)blk * B;
-        const uint32_t c1 = min(c0 + B, (uint32_t)ps.n) - 1;  // last candidate of the block
+    for (int blk = blk_begin + pb; blk < blk_last;) {
+        const uint32_t bsz = blk < tail ? B : tbs;  // this block's candidates
+        const uint32_t c0 = blk < tail ? (uint32_t)blk * B : cst + (uint32_t)(blk - tail) * tbs;
+        const uint32_t c1 = min(c0 + bsz, cend) - 1;  // last candidate of the block
         // 1. headers of the owned candidates and every list's range in this block: all loads
         // issued before the first wait, one memory round trip.  (Loading the next static block's
         // headers and ranges before this block's FAS measured slower: 184.8 -> 188.0 us, r4n,
@@ -1348,7 +1356,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
-            if (!(c <= c1 && (uint32_t)(kk * kPostThreads + tid) < B)) {
+            if (!(c <= c1 && (uint32_t)(kk * kPostThreads + tid) < bsz)) {
                 ha[kk] = make_uint4(0, 0, 0, 0);
                 hb[kk] = make_uint4(0, 0, 0, 0);
             }
@@ -1379,7 +1387,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         // barrier of its own), else bisect and walk until past the block
         if (short_excl) {
             const uint32_t p = ex0 - c0;
-            if (tid < H.n_excl && p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
+            if (tid < H.n_excl && p < bsz) atomicOr(&exb[p >> 5], 1u << (p & 31));
         } else {
             uint32_t lo = 0, hi = (uint32_t)H.n_excl;
             while (lo < hi) {  // first entry >= c0
@@ -1391,14 +1399,14 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 const uint32_t x = b + tid;
                 const uint32_t e = x < hi ? excl[x] : ~0u;
                 const uint32_t p = e - c0;
-                if (p < B) atomicOr(&exb[p >> 5], 1u << (p & 31));
-                if (__syncthreads_or(e >= c0 + B)) break;  // sorted: the rest lies beyond the block
+                if (p < bsz) atomicOr(&exb[p >> 5], 1u << (p & 31));
+                if (__syncthreads_or(e >= c0 + bsz)) break;  // sorted: the rest lies beyond the block
             }
         }
         // 2. clubs / friends
         walk_sets(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e) {
             const uint32_t p = (e >> 8) - c0;
-            if (p < B) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
+            if (p < bsz) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
         });
         K5T(2);
         __syncthreads();
@@ -1412,7 +1420,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const int p = kk * kPostThreads + tid;
             const uint32_t ct = cnt[p];
-            if ((uint32_t)p >= B || c0 + p > c1 || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
+            if ((uint32_t)p >= bsz || c0 + p > c1 || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
             const uint64_t cm = (uint64_t)ha[kk].x | ((uint64_t)(ha[kk].y & 0xFFFFu) << 32);
             pend[kk] = cm & q.colmask;
             double s = 0.0;
@@ -1496,7 +1504,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     for (int u = 0; u < U; ++u) {
                         const uint32_t p = (ent[u] >> 8) - c0;
                         kp[u] = ~0u;
-                        if (js[u] >= 0 && p < B) {
+                        if (js[u] >= 0 && p < bsz) {
                             const uint32_t jr = (uint32_t)(js[u] - ja);
                             kp[u] = p | jr << 10 | (ent[u] & 0xFFu) << 16;
                             atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << jr);
@@ -1506,7 +1514,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {  // one-token rounds past the cap
                     const int j = round_list(gpre, ja, jb, g0 + f);
                     const uint32_t p = (ps.post[K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 6)] >> 8) - c0;
-                    if (p < B) atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << (j - ja));
+                    if (p < bsz) atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << (j - ja));
                 }
                 K5T(4);
                 __syncthreads();
@@ -1562,7 +1570,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const uint32_t x = K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 7);
                     const uint32_t e = ps.post[x];
                     const uint32_t p = (e >> 8) - c0;
-                    if (p >= B) continue;
+                    if (p >= bsz) continue;
                     const uint32_t jr = (uint32_t)(j - ja);
                     const uint64_t below = mask[p] & low_bits(jr);
                     const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kRoundCap, 9);
@@ -2376,13 +2384,14 @@ uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFix
 
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                       const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
+                       const int32_t* out_rows, uint32_t mode, uint32_t tail_bs, hipEvent_t e0, hipEvent_t e1,
+                       hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
     // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
     const dim3 grid = (mode & 2u) ? dim3(nq, blocks) : dim3(blocks, nq);
     hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
-                          pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode);
+                          pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs);
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;

@@ -258,6 +258,8 @@ def pmc_pass(args, select):
         cmd.append("--no-cfg3")
     if args.sync_calls:
         cmd.append("--sync-calls")
+    if args.eval_sync:
+        cmd.append("--eval-sync")
     try:
         r = subprocess.run(["timeout", "-s", "KILL", "240"] + cmd, capture_output=True, text=True,
                            env={**os.environ, "TMPDIR": os.environ.get("TMPDIR", "/tmp")})
@@ -658,18 +660,39 @@ def run_cfg5(args, world, rank, local):
         dist.all_gather(parts, t)
         return [p.cpu().numpy() for p in parts]
 
-    def step():
-        def part(t):
-            return ds.eval_recommendation_tests(engs[t], S, CFG5_TOPK, rank * C + t, nsh, args.cfg5_batch)
-        parts = [part(0)] if pool is None else list(pool.map(part, range(C)))
+    def summarize(parts):
         hs = gather(np.stack([h for h, _ in parts]))  # per rank [C, entries, 3]
         cs = gather(np.stack([c for _, c in parts]))
         hits = pf.merge_shards([h[t] for h in hs for t in range(C)])  # shard order rank * C + t
         club = pf.merge_shards([c[t] for c in cs for t in range(C)])
         return pf.rec_tests_summary(hits, club), len(hits)
 
-    for _ in range(warm):
-        step()
+    def step():
+        def part(t):
+            return ds.eval_recommendation_tests(engs[t], S, CFG5_TOPK, rank * C + t, nsh, args.cfg5_batch)
+        return summarize([part(0)] if pool is None else list(pool.map(part, range(C))))
+
+    # one context: the asynchronous driver call (pf_eval_recommendation_tests_async) leaves each
+    # step's last chunk on the device; the next step plans and launches its first chunk before that
+    # chunk is unpacked, so the host's planning hides behind the device (--eval-sync: the old form)
+    use_async = C == 1 and not args.eval_sync
+
+    def steps_async(n):
+        prev, out = None, None
+        for _ in range(n):
+            cur = ds.eval_recommendation_tests_async(eng, S, CFG5_TOPK, rank, nsh, args.cfg5_batch)
+            if prev is not None:
+                out = summarize([ds.eval_wait(eng, prev)])
+            prev = cur
+        if prev is not None:
+            out = summarize([ds.eval_wait(eng, prev)])
+        return out
+
+    if use_async:
+        steps_async(warm)
+    else:
+        for _ in range(warm):
+            step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -677,8 +700,11 @@ def run_cfg5(args, world, rank, local):
     for e in engs:
         e.jobs_stats_reset(time_pairs=True, count=False)
     ts = time.perf_counter()
-    for _ in range(steps):
-        summary, n_eval = step()
+    if use_async:
+        summary, n_eval = steps_async(steps)
+    else:
+        for _ in range(steps):
+            summary, n_eval = step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -744,6 +770,8 @@ def run_cfg5(args, world, rank, local):
                      "alg_bytes_per_launch": alg_pl,
                      "pair_kernel_share_of_step": (timing["pair_ms"] / (elapsed * 1e3)) if elapsed > 0 else None},
         "selfcheck_vs_sequential_64_users": selfcheck, "files_s": write_s, "open_s": open_s,
+        "driver_calls": "asynchronous (pf_eval_recommendation_tests_async: step i + 1 planned beside step i's "
+                        "last device chunk)" if use_async else "synchronous",
     }
     if rank == 0 and world == 1 and base is not None:
         rec["cpu_baseline"] = base
@@ -839,6 +867,8 @@ def main():
                          "thread; default 1 (cfg3: the asynchronous calls overlap the host planning; cfg5: one "
                          "context 99.6k-113.4k users/s against 99.0k-121.2k with three on the round-4 boxes, "
                          "DESIGN.md section 5)")
+    ap.add_argument("--eval-sync", action="store_true",
+                    help="cfg5: the synchronous driver call per step instead of the asynchronous one")
     ap.add_argument("--sync-calls", action="store_true",
                     help="cfg3: the synchronous recommender calls instead of the asynchronous ones")
     ap.add_argument("--async-depth", type=int, default=ASYNC_DEPTH,

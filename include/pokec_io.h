@@ -162,6 +162,16 @@ int pf_eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_si
 int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
                                  int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
                                  double* out_club, int32_t cap, int32_t* n_plan);
+/* Asynchronous form of pf_eval_recommendation_tests (BASELINE cfg 5's step): the batches are
+ * planned and queued as the synchronous form does, but the call returns with its last chunk still
+ * on the device; out_hits / out_club are written when pf_wait(ctx, *ticket) returns, or when the
+ * next call on the context that uses the job pipeline completes it first (that call plans and
+ * launches its own first chunk before, so one context overlaps step i + 1's host planning with
+ * step i's last device chunk).  The caller keeps the output buffers alive until then; *n_plan
+ * is written before this returns. */
+int pf_eval_recommendation_tests_async(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                       int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
+                                       double* out_club, int32_t cap, int32_t* n_plan, uint64_t* ticket);
 /* digests of the plan entries this shard evaluates (layout as the sequential _digest forms) */
 int pf_eval_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t shard,
                                    int32_t nshards, int32_t batch, uint64_t* out_digest, int32_t cap,

@@ -769,7 +769,9 @@ void pf_close(pf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     c->jb.pending.clear();  // calls never waited for: their outputs are not written
+    c->jb.carry = pf::JobsState::Carry{};
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->jb.aux2) (void)hipStreamSynchronize(c->jb.aux2);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     for (auto& st : c->stage) {
         if (st.done) (void)hipEventDestroy(st.done);
@@ -937,7 +939,9 @@ int pf_wait(pf_ctx* c, uint64_t ticket) {
 uint64_t pf_completed_ticket(const pf_ctx* c) {
     if (!c) return 0;
     // tickets are handed out in launch order and completed in launch order
-    return c->jb.pending.empty() ? c->jb.next_ticket - 1 : c->jb.pending.front().ticket - 1;
+    uint64_t t = c->jb.pending.empty() ? c->jb.next_ticket - 1 : c->jb.pending.front().ticket - 1;
+    if (c->jb.carry.on) t = std::min(t, c->jb.carry.ticket - 1);
+    return t;
 }
 
 int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, int32_t* out, int32_t cap, int32_t* n) {

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <unordered_map>
 #include <utility>
+#include <functional>
 #include <vector>
 
 struct pf_ctx;
@@ -75,6 +76,13 @@ struct HpLap {
 // Runs every job on the device job pipeline (pf_jobs_plan.cpp): one chain of device stages per
 // chunk of jobs.  0 = OK, else a PF_* status.
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs);
+// run_jobs leaving the last chunk on the device as the context's carried call (pf_jobs_plan.cpp):
+// done(jobs) runs when it is finished (by carry_wait, the next job call, or any drain)
+int run_jobs_carry(pf_ctx* c, std::vector<Job>&& jobs, uint64_t ticket, std::function<void(std::vector<Job>&)> done);
+// the carried call with this ticket (or earlier) finished; its status
+int carry_wait(pf_ctx* c, uint64_t ticket);
+// a ticket of the context's asynchronous calls (pf_wait completes every call up to it)
+uint64_t next_call_ticket(pf_ctx* c);
 // A batched driver call (its versioned edit set) starts or ends (pf_jobs_plan.cpp).
 void jobs_view_scope(pf_ctx* c);
 const std::unordered_map<int32_t, std::vector<int32_t>>& base_adj(const pf_ctx* c);

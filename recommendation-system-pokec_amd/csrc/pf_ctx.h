@@ -128,6 +128,7 @@ struct JobsState {
     uint64_t edit_gen = 1, view_gen = 0;         // the uploaded edit table is current when equal
     const void* view_over = nullptr;             // the batched drivers' versioned edits last uploaded
     size_t view_over_n = 0;
+    bool view_has_over = false;                  // the uploaded table holds versioned edits
     uint64_t call_gen = 0, view_call = 0;        // batched driver calls (jobs_view_scope)
     DevView view{};
     DBuf d_view_node, d_view_ver, d_view_off, d_view_len, d_view_nbr;
@@ -169,6 +170,19 @@ struct JobsState {
     };
     std::deque<Pending> pending;                 // launch order
     uint64_t next_ticket = 1;
+    // A batched driver call whose last chunk is still on the device (pf_eval_recommendation_tests_async):
+    // the next job call plans and launches its first chunk, then finishes this one (the chunk's
+    // unpack and the driver's per-user results), so the host's planning of step i + 1 runs beside
+    // the device's last chunk of step i.  Any other use of the pipeline finishes it first.
+    struct Carry {
+        bool on = false;
+        int slot = 0;                                // the workspace its last chunk holds
+        uint64_t ticket = 0;
+        std::vector<Job> jobs;
+        std::function<void(std::vector<Job>&)> done; // the driver's results from the finished jobs
+    } carry;
+    uint64_t carry_done = 0;                     // the last carried ticket finished
+    int carry_rc = PF_OK;                        // its status (an error drops the call's results)
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
     bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)
     bool stats_count = false;                    // pair counters (bit 1)

@@ -1294,39 +1294,24 @@ int eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size,
 
 int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
                               int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, uint64_t* digest,
-                              int32_t cap, int32_t* n_plan) {
+                              int32_t cap, int32_t* n_plan, uint64_t* ticket = nullptr) {
     if (!ctx || !ds || !n_plan || (cap > 0 && !digest && (!out_hits || !out_club)) || bad_shard(shard, nshards, batch))
         return PF_EINVAL;
     pf::HpLap hl;
     ViewScope scope(ctx);
     const auto planp = cached_plan(ds, 1, sample_size, [&]() { return plan_rec(ds, sample_size); });
-    const Plan& plan = *planp;
     hl.lap(pf::kHpPlan);
-    *n_plan = (int32_t)plan.size();
+    *n_plan = (int32_t)planp->size();
     const auto& base = pf::base_adj(ctx);
-    std::vector<int32_t> mine;
-    for (int32_t i = shard; i < (int32_t)plan.size(); i += nshards) mine.push_back(i);
-    for (size_t b = 0; b < mine.size(); b += (size_t)batch) {
-        const size_t e = std::min(mine.size(), b + (size_t)batch);
-        // per user: graph (= interest, recommender_graph.cpp:224-227), collaborative, clubs; limit 5000
-        std::vector<pf::Job> jobs(3 * (e - b));
+    auto mine = std::make_shared<std::vector<int32_t>>();
+    for (int32_t i = shard; i < (int32_t)planp->size(); i += nshards) mine->push_back(i);
+    // the per-user results of plan entries mine[b .. e) from their finished jobs (3 per user);
+    // everything it reads is captured by value, so a carried call can run it later
+    auto score = [planp, mine, ds, topk, out_hits, out_club, digest, cap](std::vector<pf::Job>& jobs, size_t b,
+                                                                          size_t e) {
+        const Plan& plan = *planp;
         for (size_t x = b; x < e; ++x) {
-            const PlanEntry& pe = plan[mine[x]];
-            for (int kind = 0; kind < 3; ++kind) {
-                pf::Job& J = jobs[3 * (x - b) + kind];
-                J.kind = kind == 0 ? pf::kJobInterest : (kind == 1 ? pf::kJobCollab : pf::kJobClubs);
-                J.uid = pe.uid;
-                J.topk = topk;
-                J.limit = 5000;
-                J.view.base = &base;  // a fresh adj_mod per user: only its own row edited
-                J.view.own = pe.uid;
-                J.view.own_row = &pe.newf;
-            }
-        }
-        const int rc = pf::run_jobs(ctx, jobs);
-        if (rc != PF_OK) return rc;
-        for (size_t x = b; x < e; ++x) {
-            const int32_t i = mine[x];
+            const int32_t i = (*mine)[x];
             if (i >= cap) continue;
             const PlanEntry& pe = plan[i];
             auto any_held = [&](const pf::Job& J) {
@@ -1359,6 +1344,30 @@ int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_
                 out_club[2 * (size_t)i + 1] = (double)hit / (double)actual.size();
             }
         }
+    };
+    for (size_t b = 0; b < mine->size(); b += (size_t)batch) {
+        const size_t e = std::min(mine->size(), b + (size_t)batch);
+        // per user: graph (= interest, recommender_graph.cpp:224-227), collaborative, clubs; limit 5000
+        std::vector<pf::Job> jobs(3 * (e - b));
+        for (size_t x = b; x < e; ++x) {
+            const PlanEntry& pe = (*planp)[(*mine)[x]];
+            for (int kind = 0; kind < 3; ++kind) {
+                pf::Job& J = jobs[3 * (x - b) + kind];
+                J.kind = kind == 0 ? pf::kJobInterest : (kind == 1 ? pf::kJobCollab : pf::kJobClubs);
+                J.uid = pe.uid;
+                J.topk = topk;
+                J.limit = 5000;
+                J.view.base = &base;  // a fresh adj_mod per user: only its own row edited
+                J.view.own = pe.uid;
+                J.view.own_row = &pe.newf;
+            }
+        }
+        if (ticket && e == mine->size())  // the last batch stays on the device (its results: pf_wait)
+            return pf::run_jobs_carry(ctx, std::move(jobs), *ticket,
+                                      [score, b, e](std::vector<pf::Job>& js) { score(js, b, e); });
+        const int rc = pf::run_jobs(ctx, jobs);
+        if (rc != PF_OK) return rc;
+        score(jobs, b, e);
     }
     return PF_OK;
 }
@@ -1385,6 +1394,16 @@ int pf_eval_holdout_friends_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sa
                                    int32_t nshards, int32_t batch, uint64_t* out_digest, int32_t cap, int32_t* n_plan) {
     if (cap > 0 && !out_digest) return PF_EINVAL;
     return eval_holdout_friends(ctx, ds, sample_size, shard, nshards, batch, nullptr, out_digest, cap, n_plan);
+}
+
+int pf_eval_recommendation_tests_async(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
+                                       int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
+                                       double* out_club, int32_t cap, int32_t* n_plan, uint64_t* ticket) {
+    if (!ticket || (cap > 0 && (!out_hits || !out_club))) return PF_EINVAL;
+    if (!ctx) return PF_EINVAL;
+    *ticket = pf::next_call_ticket(ctx);
+    return eval_recommendation_tests(ctx, ds, sample_size, topk, shard, nshards, batch, out_hits, out_club, nullptr,
+                                     cap, n_plan, ticket);
 }
 
 int pf_eval_recommendation_tests_digest(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,

@@ -449,6 +449,7 @@ int wait_pending_on_stream(pf_ctx* c) {
     auto& J = c->jb;
     for (const auto& p : J.pending)
         if (J.ws[p.slot].done) HIPCHK(c, hipStreamWaitEvent(c->stream, J.ws[p.slot].done, 0));
+    if (J.carry.on && J.ws[J.carry.slot].done) HIPCHK(c, hipStreamWaitEvent(c->stream, J.ws[J.carry.slot].done, 0));
     return PF_OK;
 }
 
@@ -483,8 +484,11 @@ int sync_nodes(pf_ctx* c) {
 int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, std::vector<int32_t>>>* over) {
     auto& J = c->jb;
     const size_t on = over ? over->size() : 0;
-    if (J.view_gen == J.edit_gen && J.view_over == (const void*)over && J.view_over_n == on &&
-        J.view_call == J.call_gen)
+    // current: the same edits and the same versioned edit set (a call's over map may reuse a freed
+    // one's address, so a non-null set is current only within the driver call that uploaded it)
+    if (J.view_gen == J.edit_gen &&
+        (over == nullptr ? !J.view_has_over
+                         : (J.view_over == (const void*)over && J.view_over_n == on && J.view_call == J.call_gen)))
         return PF_OK;
     struct E { int32_t node, ver; int32_t len; const std::vector<int32_t>* row; };
     std::vector<E> es;
@@ -530,6 +534,7 @@ int sync_view(pf_ctx* c, const std::unordered_map<int32_t, std::pair<int32_t, st
     J.view_gen = J.edit_gen;
     J.view_over = over;
     J.view_over_n = on;
+    J.view_has_over = on > 0;
     J.view_call = J.call_gen;
     return PF_OK;
 }
@@ -1197,7 +1202,8 @@ int finish_pending(pf_ctx* c) {
 }  // namespace
 
 // Every pending asynchronous call unpacked (before any other use of the job pipeline's state).
-int jobs_drain(pf_ctx* c) {
+// The pending asynchronous recommender calls, unpacked (the carried driver call stays in flight).
+int drain_calls(pf_ctx* c) {
     int rc = PF_OK;
     while (!c->jb.pending.empty()) {
         const int r = finish_pending(c);
@@ -1206,14 +1212,38 @@ int jobs_drain(pf_ctx* c) {
     return rc;
 }
 
+// The carried driver call: wait for its last chunk, unpack it, hand the jobs to its driver.
+int finish_carry(pf_ctx* c) {
+    auto& J = c->jb;
+    if (!J.carry.on) return PF_OK;
+    JobsState::Carry cr = std::move(J.carry);
+    J.carry = JobsState::Carry{};
+    int rc = finish_chunk(c, cr.jobs, J.ws[cr.slot], nullptr);
+    if (rc == PF_OK && cr.done) cr.done(cr.jobs);
+    J.carry_done = cr.ticket;
+    J.carry_rc = rc;
+    return rc;
+}
+
+int jobs_drain(pf_ctx* c) {
+    int rc = drain_calls(c);
+    const int r = finish_carry(c);
+    return rc != PF_OK ? rc : r;
+}
+
 namespace {
 
-int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector<int32_t>>* raw_out) {
+// leave != nullptr: the call's last chunk stays on the device as the context's carried call (the
+// jobs move into it; leave->done gets them once finished).  A carried call of an earlier driver
+// call is finished right after this call's first chunk is launched.
+int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector<int32_t>>* raw_out,
+            JobsState::Carry* leave = nullptr) {
     auto& J = c->jb;
     if (!J.ok) return c->fail(PF_EUNSUPP, "device job pipeline unavailable: " + J.why);
     (void)hipSetDevice(c->device);
-    int rc0 = jobs_drain(c);  // asynchronous calls in flight finish first (they hold the workspaces)
+    int rc0 = drain_calls(c);  // asynchronous calls in flight finish first (they hold the workspaces)
     if (rc0 != PF_OK) return rc0;
+
     for (Job& jb : jobs) jb.out.clear();
     if (jobs.empty()) return PF_OK;
     int rc = sync_nodes(c);
@@ -1256,12 +1286,17 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         const size_t len = std::max<size_t>(kPipeJobs / 4, (n * w + wsum - 1) / wsum);
         return std::min(n, b + len);
     };
-    int slot = 0;
+    int slot = J.carry.on ? (J.carry.slot ^ 1) : 0;  // the carried call holds the other workspace
     JobsState::Ws* pending = nullptr;
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
         (void)hipStreamSynchronize(c->stream);
         if (J.aux2) (void)hipStreamSynchronize(J.aux2);
         for (auto& w : J.ws) w.active = false;
+        if (J.carry.on) {  // its results are dropped; pf_eval_wait reports the error
+            J.carry_done = J.carry.ticket;
+            J.carry_rc = code;
+            J.carry = JobsState::Carry{};
+        }
         return code;
     };
     size_t b = 0;
@@ -1289,6 +1324,10 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         JobsState::Ws& W = J.ws[slot];
         rc = launch_chunk(c, jobs, P, b, e, W);
         if (rc != PF_OK) return drain(rc);
+        if (J.carry.on) {  // the device runs this chunk behind the carried call's last one
+            rc = finish_carry(c);
+            if (rc != PF_OK) return drain(rc);
+        }
         if (pending) {
             rc = finish_chunk(c, jobs, *pending, raw_out);
             if (rc != PF_OK) return drain(rc);
@@ -1298,16 +1337,41 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         b = e;
         hl.skip();
     }
+    if (pending && leave && !raw && pending->active) {  // the last chunk stays on the device
+        leave->on = true;
+        leave->slot = (int)(pending - J.ws);
+        leave->jobs = std::move(jobs);
+        J.carry = std::move(*leave);
+        return PF_OK;
+    }
     if (pending) {
         rc = finish_chunk(c, jobs, *pending, raw_out);
         if (rc != PF_OK) return drain(rc);
     }
+    if (leave && leave->done) leave->done(jobs);  // nothing left on the device: finished now
+    if (leave) J.carry_done = leave->ticket;
     return PF_OK;
 }
 
 }  // namespace
 
 int run_jobs(pf_ctx* c, std::vector<Job>& jobs) { return run_all(c, jobs, false, nullptr); }
+
+int run_jobs_carry(pf_ctx* c, std::vector<Job>&& jobs, uint64_t ticket, std::function<void(std::vector<Job>&)> done) {
+    JobsState::Carry cr;
+    cr.ticket = ticket;
+    cr.done = std::move(done);
+    std::vector<Job> js = std::move(jobs);
+    return run_all(c, js, false, nullptr, &cr);
+}
+
+uint64_t next_call_ticket(pf_ctx* c) { return c->jb.next_ticket++; }
+
+int carry_wait(pf_ctx* c, uint64_t ticket) {
+    auto& J = c->jb;
+    if (J.carry.on && J.carry.ticket <= ticket) return finish_carry(c);
+    return J.carry_done >= ticket ? J.carry_rc : PF_OK;
+}
 
 // An asynchronous call: planned and launched now into a free workspace slot (the oldest pending
 // call is unpacked first when both are taken), unpacked into the caller's buffers by pf_wait.
@@ -1387,7 +1451,8 @@ int jobs_wait(pf_ctx* c, uint64_t ticket) {
         const int r = finish_pending(c);
         if (rc == PF_OK) rc = r;
     }
-    return rc;
+    const int r = carry_wait(c, ticket);
+    return rc != PF_OK ? rc : r;
 }
 
 int jobs_stats_reset(pf_ctx* c, int enable) {

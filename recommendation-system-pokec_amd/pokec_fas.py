@@ -35,7 +35,7 @@ IO_EXPORTS = ["pf_dataset_load", "pf_dataset_load_cached", "pf_dataset_free", "p
               "pf_compute_normalizers", "pf_holdout_friends", "pf_recommendation_tests",
               "pf_eval_holdout_friends", "pf_eval_recommendation_tests", "pf_holdout_friends_digest",
               "pf_recommendation_tests_digest", "pf_eval_holdout_friends_digest",
-              "pf_eval_recommendation_tests_digest"]
+              "pf_eval_recommendation_tests_digest", "pf_eval_recommendation_tests_async"]
 PF_LOAD_REFERENCE_CAP = 100000
 
 
@@ -141,6 +141,8 @@ def lib():
         L.pf_recommendation_tests_digest.argtypes = [V, V, I32, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_eval_holdout_friends_digest.argtypes = [V, V, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
         L.pf_eval_recommendation_tests_digest.argtypes = [V, V, I32, I32, I32, I32, I32, V, I32, ctypes.POINTER(I32)]
+        L.pf_eval_recommendation_tests_async.argtypes = [V, V, I32, I32, I32, I32, I32, V, V, I32, ctypes.POINTER(I32),
+                                                         ctypes.POINTER(ctypes.c_uint64)]
         _lib = L
     return _lib
 
@@ -474,6 +476,32 @@ class Dataset:
         eng._check(rc, "pf_eval_recommendation_tests")
         return hits[:n.value], club[:n.value]
 
+
+    class EvalPending:
+        def __init__(self, hits, club, n, ticket):
+            self.hits, self.club, self.n, self.ticket = hits, club, n, ticket
+
+    def eval_recommendation_tests_async(self, eng, sample_size, topk, shard=0, nshards=1, batch=128):
+        """pf_eval_recommendation_tests_async: returns at once with the last chunk on the device;
+        eval_wait(eng, p) gives eval_recommendation_tests's (hits, club).  The engine keeps the output
+        arrays alive until the call completes."""
+        cap = max(int(sample_size), 1)
+        hits = np.full((cap, 3), -1, np.int8)
+        club = np.full((cap, 2), np.nan)
+        n = ctypes.c_int32()
+        t = ctypes.c_uint64()
+        rc = self._L.pf_eval_recommendation_tests_async(eng.h, self.h, sample_size, topk, shard, nshards, batch,
+                                                        hits.ctypes.data, club.ctypes.data, cap, ctypes.byref(n),
+                                                        ctypes.byref(t))
+        eng._check(rc, "pf_eval_recommendation_tests_async")
+        p = Dataset.EvalPending(hits, club, n.value, t.value)
+        eng._inflight[p.ticket] = p
+        return p
+
+    def eval_wait(self, eng, p):
+        eng._check(self._L.pf_wait(eng.h, p.ticket), "pf_wait")
+        eng._prune_inflight()
+        return p.hits[:p.n], p.club[:p.n]
 
     # -- per-user result digests (pokec_io.h pf_result_digest): parity probes of the drivers
     def holdout_friends_digest(self, eng, sample_size):

@@ -792,6 +792,40 @@ def test_driver_digests_match_reference():
     eng.close()
 
 
+def test_async_driver_calls_equal_sync():
+    """pf_eval_recommendation_tests_async (cfg 5's step with its last chunk left on the device):
+    chained calls, each completing the previous one after launching its own first chunk, a
+    synchronous recommender call completing a carried one, and multi-batch / pipelined-chunk calls
+    all give the synchronous driver's per-user results, and the digests still equal the reference's."""
+    import tempfile
+    pf = tl.product()
+    m = tl.manifest()["corpora"]["A"]
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        ds = pf.Dataset(d)
+    eng = pf.FasEngine(ds.desc_ptr(), 0)
+
+    def same(a, b):
+        return np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1], equal_nan=True)
+
+    for n, batch in ((m["digest_rectest"], 128), (600, 2048), (600, 200)):
+        ref = ds.eval_recommendation_tests(eng, n, 10, 0, 1, batch)
+        p1 = ds.eval_recommendation_tests_async(eng, n, 10, 0, 1, batch)
+        p2 = ds.eval_recommendation_tests_async(eng, n, 10, 0, 1, batch)
+        assert same(ds.eval_wait(eng, p2), ref), (n, batch)
+        assert same(ds.eval_wait(eng, p1), ref), (n, batch)
+        p3 = ds.eval_recommendation_tests_async(eng, n, 10, 0, 1, batch)
+        eng.recommend_collaborative([1, 2, 3], 10, 1000)  # a synchronous job call completes p3 first
+        assert same(ds.eval_wait(eng, p3), ref), (n, batch)
+        for nsh in (2, 3):  # shards, each carried in turn
+            ps = [ds.eval_recommendation_tests_async(eng, n, 10, s, nsh, batch) for s in range(nsh)]
+            parts = [ds.eval_wait(eng, p) for p in ps]
+            assert np.array_equal(pf.merge_shards([h for h, _ in parts]), ref[0]), (n, batch, nsh)
+    _, rect = tl.golden_digests("A", "rectests_digest.txt")
+    assert np.array_equal(ds.recommendation_tests_digest(eng, m["digest_rectest"], 10), rect)
+    eng.close()
+
+
 @pytest.mark.parametrize("wide_fmt", [False, True], ids=["packed", "wide"])
 def test_device_df_idf_norms_and_any_token_ids(wide_fmt):
     """F3 on the device (pf_idf.hip) with token ids anywhere in int32 (the reference

@@ -264,8 +264,9 @@ uint32_t post_mode(int nq) {
     // blocks share the cache lines at their list segments' ends); the query-major batch grid too
     // (a query's workgroups are a multiple of 8 there, so bx mod 8 is still the XCD); k5_xcd=0 A/B
     static const bool xcd = pf::debug_long("k5_xcd", 1) != 0;
+    static const bool dyn = pf::debug_long("k5_dyn", 0) != 0;  // every block claimed per XCD group (A/B)
     const uint32_t x = xcd ? 4u : 0u;
-    return nq == 1 ? ((st ? 0u : 1u) | x) : (tr ? 2u : x);
+    return nq == 1 ? ((st ? 0u : 1u) | x | (dyn ? 8u : 0u)) : (tr ? 2u : x);
 }
 
 // Candidates per claimed block past a one-query K5 launch's static rounds (PF_DEBUG k5_tail=N,

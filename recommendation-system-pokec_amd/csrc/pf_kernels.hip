@@ -18,7 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <unordered_map>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 
@@ -37,6 +39,15 @@ __device__ unsigned long long g_k5t[16];
 // K1': staging, walk, epilogue, total, dense, assembly, overflow, waves, fas, then the epilogue's
 // waves past the item queue (per-lane fallback), items, epilogue waves
 __device__ unsigned long long g_k1t[12];
+#endif
+
+#ifdef PF_K5_BLOCKLOG
+// profiling build only (tools/build_variant.sh blog XFLAGS=-DPF_K5_BLOCKLOG): K5's per-block start /
+// end times (s_memrealtime, 100 MHz, one clock for every CU), summarised by launch_post
+constexpr unsigned kBlogCap = 16384;
+__device__ unsigned long long g_blog_t[2 * kBlogCap];
+__device__ unsigned int g_blog_meta[kBlogCap];
+__device__ unsigned int g_blog_n;
 #endif
 
 // Orders a wave's LDS accesses across its lanes (LDS serves a wave's operations in order;
@@ -1329,7 +1340,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const uint32_t cend = min((uint32_t)blk_end * B, (uint32_t)ps.n);  // the range's end
     const uint32_t tbs = (tail_bs > 0u && tail_bs < B) ? tail_bs : B;
     const uint32_t cst = min((uint32_t)tail * B, cend);                 // the claimed part's start
-    const int blk_last = tail + (int)((cend - cst + tbs - 1) / tbs);
+    int blk_last = tail + (int)((cend - cst + tbs - 1) / tbs);
     const bool short_excl = H.n_excl <= kPostThreads;
     const uint32_t ex0 = short_excl && H.n_excl > 0 ? excl[min(tid, H.n_excl - 1)] : ~0u;  // the query's, once
     // mode bit 2 (one query, query-major batches): the workgroups of XCD x (bx mod 8 under the
@@ -1337,10 +1348,27 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // static round, so a list segment's boundary cache lines are shared inside one L2 instead of
     // fetched by two XCDs (cfg 2 PMC traffic 236 -> 175 MB per launch, r4w -> r5h)
     const int pb = ((mode & 4u) && (nbx & 7) == 0) ? (bx & 7) * (nbx >> 3) + (bx >> 3) : bx;
-    for (int blk = blk_begin + pb; blk < blk_last;) {
+    // mode bit 3 (one query): every block claimed, per group g = bx mod 8 (with round-robin dispatch,
+    // one XCD) from a contiguous eighth of the range, in order, from the group's own counter.  The
+    // workgroups dispatched last (the third and fourth of a CU) lose VALU arbitration to the older
+    // ones by age and ran their static blocks ~25 % slower every round (r6j block log): claimed
+    // blocks let the faster workgroups take more.  The next block is claimed at the start of a
+    // block's last text round, so the claim's round trip hides behind that round.
+    const bool xdyn = (mode & 8u) != 0u;
+    const int xng = min(8, nbx), xg = bx % xng;
+    const int x_lo = blk_begin + (int)((int64_t)(blk_end - blk_begin) * xg / xng);
+    const int x_hi = blk_begin + (int)((int64_t)(blk_end - blk_begin) * (xg + 1) / xng);
+    const int x_nwg = (nbx - xg + xng - 1) / xng;
+    unsigned int* xctr = &sync[qy].xcd_next[xg * 16];
+    if (xdyn) blk_last = x_hi;
+    for (int blk = xdyn ? x_lo + bx / xng : blk_begin + pb; blk < blk_last;) {
+        unsigned int xclaim = 0;
         const uint32_t bsz = blk < tail ? B : tbs;  // this block's candidates
         const uint32_t c0 = blk < tail ? (uint32_t)blk * B : cst + (uint32_t)(blk - tail) * tbs;
         const uint32_t c1 = min(c0 + bsz, cend) - 1;  // last candidate of the block
+#ifdef PF_K5_BLOCKLOG
+        const unsigned long long blog_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         // 1. headers of the owned candidates and every list's range in this block: all loads
         // issued before the first wait, one memory round trip.  (Loading the next static block's
         // headers and ranges before this block's FAS measured slower: 184.8 -> 188.0 us, r4n,
@@ -1452,7 +1480,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
         int nrounds = (int)misc[3];  // written before the barrier above
+        if (xdyn && nrounds == 0 && tid == 0) xclaim = atomicAdd(xctr, 1u);
         for (int rnd = 0; rnd < nrounds; ++rnd) {
+            if (xdyn && rnd == nrounds - 1 && tid == 0) xclaim = atomicAdd(xctr, 1u);
             const uint2 rr = rtab[rnd];
             Round R;
             R.ja = (int)(rr.x & 0xFFFFu);
@@ -1712,7 +1742,21 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) topk_push(best, keys[kk], k, lane);
         K5T(12);
-        if ((mode & 1u) && blk + nbx >= tail) {
+#ifdef PF_K5_BLOCKLOG
+        if (tid == 0) {
+            const unsigned i = atomicAdd(&g_blog_n, 1u);
+            if (i < kBlogCap) {
+                g_blog_t[2 * i] = blog_t0;
+                g_blog_t[2 * i + 1] = __builtin_amdgcn_s_memrealtime();
+                g_blog_meta[i] = (unsigned)bx | (unsigned)blk << 16;
+            }
+        }
+#endif
+        if (xdyn) {
+            if (tid == 0) misc[0] = (uint32_t)(x_lo + x_nwg) + xclaim;
+            __syncthreads();
+            blk = (int)misc[0];
+        } else if ((mode & 1u) && blk + nbx >= tail) {
             // the tail past the static rounds from the query's counter: one claim per workgroup
             // (every workgroup claiming every block serialised ~3,000 atomics on one address).
             // misc[0] was last read before this block's first barrier; claimed here, not at the
@@ -2382,6 +2426,50 @@ uint32_t post_var_lds(int n_tok, int n_lists) {
 }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 
+#ifdef PF_K5_BLOCKLOG
+// per-block times of one launch: the span, and per static round (blk / nbx) the blocks' start and
+// end offsets and durations (us, from the launch's first block start)
+static void blog_report(int nbx) {
+    static unsigned long long t[2 * kBlogCap];
+    static unsigned int meta[kBlogCap];
+    unsigned int n = 0;
+    hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_blog_n), sizeof n);
+    n = n < kBlogCap ? n : kBlogCap;
+    hipMemcpyFromSymbol(t, HIP_SYMBOL(g_blog_t), 2 * n * sizeof(unsigned long long));
+    hipMemcpyFromSymbol(meta, HIP_SYMBOL(g_blog_meta), n * sizeof(unsigned));
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (unsigned i = 0; i < n; ++i) { t0 = t[2 * i] < t0 ? t[2 * i] : t0; t1 = t[2 * i + 1] > t1 ? t[2 * i + 1] : t1; }
+    fprintf(stderr, "k5blog: %u blocks, span %.1f us\n", n, (t1 - t0) / 100.0);
+    static int dumps = 0;
+    if (const char* path = getenv("PF_BLOG_OUT"); path && dumps++ < 3) {  // raw rows: wg blk start end (us)
+        char fn[512];
+        snprintf(fn, sizeof fn, "%s.%d.csv", path, dumps);
+        if (FILE* f = fopen(fn, "w")) {
+            for (unsigned i = 0; i < n; ++i)
+                fprintf(f, "%u,%u,%.2f,%.2f\n", meta[i] & 0xFFFFu, meta[i] >> 16, (t[2 * i] - t0) / 100.0,
+                        (t[2 * i + 1] - t0) / 100.0);
+            fclose(f);
+        }
+    }
+    for (int r = 0; r < 8; ++r) {
+        std::vector<double> d, st, en;
+        for (unsigned i = 0; i < n; ++i) {
+            const int blk = (int)(meta[i] >> 16);
+            if (blk / nbx != r) continue;
+            d.push_back((t[2 * i + 1] - t[2 * i]) / 100.0);
+            st.push_back((t[2 * i] - t0) / 100.0);
+            en.push_back((t[2 * i + 1] - t0) / 100.0);
+        }
+        if (d.empty()) continue;
+        std::sort(d.begin(), d.end()); std::sort(st.begin(), st.end()); std::sort(en.begin(), en.end());
+        auto pc = [](const std::vector<double>& v, double q) { return v[(size_t)(q * (v.size() - 1))]; };
+        fprintf(stderr, "k5blog: round %d: %zu blocks, dur p10/50/90/max %.1f/%.1f/%.1f/%.1f, start min/50/max %.1f/%.1f/%.1f, end min/50/max %.1f/%.1f/%.1f\n",
+                r, d.size(), pc(d, .1), pc(d, .5), pc(d, .9), d.back(), st.front(), pc(st, .5), st.back(), en.front(),
+                pc(en, .5), en.back());
+    }
+}
+#endif
+
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
                        const int32_t* out_rows, uint32_t mode, uint32_t tail_bs, hipEvent_t e0, hipEvent_t e1,
@@ -2392,6 +2480,15 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
     const dim3 grid = (mode & 2u) ? dim3(nq, blocks) : dim3(blocks, nq);
     hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
                           pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs);
+#ifdef PF_K5_BLOCKLOG
+    {
+        static int calls = 0;
+        hipStreamSynchronize(s);
+        if (++calls % 10 == 0 && nq == 1) blog_report(blocks);
+        const unsigned zero = 0;
+        hipMemcpyToSymbol(HIP_SYMBOL(g_blog_n), &zero, sizeof zero);
+    }
+#endif
 #ifdef PF_K5_TIMERS
     {
         static int calls = 0;

@@ -1097,36 +1097,14 @@ __device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L,
                       L.off + ps.cells[K5CHK(L.cell_off + (c1 >> L.shift) + 1, ps.n_cells, 2)]);
 }
 
-// Flattened walk over the entries of lists rng[0 .. nl): thread i takes flat entries
-// i + 256u (u < 2) of every 512-entry group, loads them together, then calls f(list, entry)
-template <class F>
-__device__ __forceinline__ void walk_sets(const PostStore& ps, const uint2* rng, int nl, F f) {
-    constexpr int U = 2;
-    uint32_t total = 0;
-    for (int j = 0; j < nl; ++j) total += rng[j].y - rng[j].x;
-    for (uint32_t f0 = 0; f0 < total; f0 += U * kPostThreads) {
-        int js[U];
-        uint32_t xs[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) { js[u] = -1; xs[u] = 0; }
-        uint32_t pre = 0;
-        for (int j = 0; j < nl && pre < f0 + U * kPostThreads; ++j) {
-            const uint2 r = rng[j];
-            const uint32_t len = r.y - r.x;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t fl = f0 + threadIdx.x + kPostThreads * u;
-                if (fl - pre < len) { js[u] = j; xs[u] = r.x + (fl - pre); }
-            }
-            pre += len;
-        }
-        uint32_t ent[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) ent[u] = js[u] >= 0 ? ps.post[K5CHK(xs[u], ps.n_post, 3)] : 0u;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (js[u] >= 0) f(js[u], ent[u]);
+// the set list of flat entry f < spre[n]: the last j with spre[j] <= f (a nonempty one)
+__device__ __forceinline__ int set_list(const uint32_t* spre, int n, uint32_t f) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (spre[mid] <= f) lo = mid; else hi = mid - 1;
     }
+    return lo;
 }
 
 // gpre[j] = sum of the lengths of ranges 0 .. j-1 (j <= nl), by one wave
@@ -1294,7 +1272,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     uint2* rng = reinterpret_cast<uint2*>(pl + nl);
     uint2* rtab = rng + nl;  // the block's rounds (ja | jb << 16, ca | ce << 16), <= n_tok of them
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rtab + H.n_tok + 1);
-    uint8_t* colof = reinterpret_cast<uint8_t*>(gpre + H.n_tok + 1);  // token -> active column index
+    uint32_t* spre = gpre + H.n_tok + 1;  // the set lists' prefix [nsets + 1]
+    uint8_t* colof = reinterpret_cast<uint8_t*>(spre + nsets + 1);  // token -> active column index
     uint64_t* mapb = reinterpret_cast<uint64_t*>(base + kLdsMapB);
     uint2* mapn = reinterpret_cast<uint2*>(base + kLdsMapN);
     uint8_t* mapc = reinterpret_cast<uint8_t*>(base + kLdsMapC);
@@ -1431,11 +1410,31 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 if (__syncthreads_or(e >= c0 + bsz)) break;  // sorted: the rest lies beyond the block
             }
         }
-        // 2. clubs / friends
-        walk_sets(ps, rng + H.n_tok, nsets, [&](int j, uint32_t e) {
-            const uint32_t p = (e >> 8) - c0;
-            if (p < bsz) atomicAdd(&cnt[p], (e & 0xFFu) << (j < H.n_club ? 0 : 16));
-        });
+        // 2. clubs / friends, by waves 1-3 while wave 0 plans the rounds: each computes the set
+        // lists' prefix itself (the same values, so no barrier) and takes flat entries by bisection
+        // (the round-4 walk scanned every set list per entry group on every thread: 17 us of a
+        // cfg-2 launch, r6l)
+        if (tid >= 64 && nsets > 0) {
+            wave_prefix(spre, rng + H.n_tok, nsets, lane);
+            wave_sync();
+            const uint32_t tot = spre[nsets];
+            constexpr uint32_t kSetThreads = kPostThreads - 64;
+            for (uint32_t f0 = (uint32_t)tid - 64u; f0 < tot; f0 += 2u * kSetThreads) {
+                int js[2];
+                uint32_t e[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint32_t f = f0 + u * kSetThreads;
+                    js[u] = f < tot ? set_list(spre, nsets, f) : -1;
+                    e[u] = js[u] >= 0 ? ps.post[K5CHK(rng[H.n_tok + js[u]].x + (f - spre[js[u]]), ps.n_post, 3)] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint32_t p = (e[u] >> 8) - c0;
+                    if (js[u] >= 0 && p < bsz) atomicAdd(&cnt[p], (e[u] & 0xFFu) << (js[u] < H.n_club ? 0 : 16));
+                }
+            }
+        }
         K5T(2);
         __syncthreads();
         K5T(1);
@@ -1783,6 +1782,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     }
     // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
     uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
+
     post_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
 }
 
@@ -1845,16 +1845,6 @@ __host__ __device__ inline uint32_t slice_shared_var(int n_tok, int nl) {
 }
 __host__ __device__ inline uint32_t slice_wave_bytes(int n_tok, int nl) {
     return (kWsFixed + 8u * (uint32_t)nl + 4u * (uint32_t)(nl + 2) + 15u) & ~15u;
-}
-
-// the set list of flat entry f < spre[n]: the last j with spre[j] <= f (a nonempty one)
-__device__ __forceinline__ int set_list(const uint32_t* spre, int n, uint32_t f) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (spre[mid] <= f) lo = mid; else hi = mid - 1;
-    }
-    return lo;
 }
 
 __global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
@@ -2296,7 +2286,8 @@ __global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
 constexpr int kMergeThreads = 1024;
 __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_t* __restrict__ in, int32_t nparts,
                                                                    int64_t part_stride, int64_t query_stride, int32_t k,
-                                                                   uint64_t* __restrict__ out) {
+                                                                   uint64_t* __restrict__ out,
+                                                                   const int32_t* __restrict__ out_rows) {
     __shared__ uint64_t sc[16 * 64];
     const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t total = (int64_t)nparts * k;
@@ -2321,7 +2312,8 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const uint64_
         uint64_t acc = ~0ull;
         const int n = (int)(blockDim.x >> 6) * k;
         for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        if (lane < k) out[(size_t)q * k + lane] = acc;
+        const int row = out_rows ? out_rows[q] : q;
+        if (lane < k) out[(size_t)row * k + lane] = acc;
     }
 }
 
@@ -2419,10 +2411,10 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 }
 
 // K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | PList[n_lists] | ranges[n_lists] |
-// prefix[n_tok + 1] | token -> column u8[n_tok]
+// rounds[n_tok + 1] | token prefix[n_tok + 1] | set prefix[n_sets + 1] | token -> column u8[n_tok]
 uint32_t post_var_lds(int n_tok, int n_lists) {
-    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 8 * (n_tok + 1) + 4 * (n_tok + 1) + n_tok +
-                      15) & ~15u;
+    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 8 * (n_tok + 1) + 4 * (n_tok + 1) +
+                      4 * (n_lists - n_tok + 1) + n_tok + 15) & ~15u;
 }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }
 
@@ -2478,8 +2470,8 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
     // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
     // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
     const dim3 grid = (mode & 2u) ? dim3(nq, blocks) : dim3(blocks, nq);
-    hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps,
-                          pool, img_off, blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs);
+    hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps, pool, img_off,
+                          blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs);
 #ifdef PF_K5_BLOCKLOG
     {
         static int calls = 0;
@@ -2575,7 +2567,7 @@ hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int
                         uint64_t* out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     hipLaunchKernelGGL(topk_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, s, in, nparts, part_stride, query_stride,
-                       k, out);
+                       k, out, (const int32_t*)nullptr);
     return hipGetLastError();
 }
 

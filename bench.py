@@ -882,7 +882,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE pass (traffic = null)")
     ap.add_argument("--time-every", type=int, default=1,
-                    help="HIP-event timing on every n-th scan launch of the timed region (1 = all)")
+                    help="HIP-event timing on every n-th scan launch of the timed region (1 = all).  A timed "
+                         "launch costs ~4 us of stream time (r6q, one box: 182.2 us per cfg-2 step timing every "
+                         "launch, 179.9 every 2nd, 177.5 every 4th, 178.0 none); the default times every launch "
+                         "so the line's average is over the same launches as rocprof's")
     ap.add_argument("--scan-kernel", choices=["auto", "stream", "postings"], default="auto",
                     help="all-candidates scan kernel (auto = postings when the corpus fits its encoding)")
     ap.add_argument("--no-cfg3", action="store_true",

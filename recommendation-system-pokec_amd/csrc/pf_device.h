@@ -200,10 +200,43 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-    return ((uint64_t)hi << 32) | lo;
+// v of lane ^ m (m = 1, 2, 4, 8, 15, 16 or 32, a constant after unrolling) with no LDS round trip:
+// DPP quad permutes, row mirrors and row rotations inside a 16-lane row, the gfx950 permlane swaps
+// across rows (a __shfl_xor is a ds_bpermute: ~20 dependent ones made a 64-key sort ~1.5 us)
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v, int m) {
+    switch (m) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    case 4: {  // row_half_mirror (i -> 7 - i), then quad_perm [3,2,1,0]: i -> 7 - (i ^ 3) = i ^ 4
+        const int h = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);
+        return (uint32_t)__builtin_amdgcn_mov_dpp(h, 0x1B, 0xf, 0xf, false);
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);   // row_ror:8
+    case 15: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false);  // row_mirror
+    case 16: {  // odd rows of the first operand swapped with even rows of the second
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16u) ? r[0] : r[1];
+    }
+    case 32: {  // upper half of the first operand swapped with lower half of the second
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32u) ? r[0] : r[1];
+    }
+    default: return (uint32_t)__shfl_xor((int)v, m);
+    }
+}
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v, int m) {
+    return ((uint64_t)lane_xor32((uint32_t)(v >> 32), m) << 32) | lane_xor32((uint32_t)v, m);
+}
+// v of lane 63 - lane (= lane ^ 63)
+__device__ __forceinline__ uint64_t lane_rev64(uint64_t v) { return lane_xor64(lane_xor64(lane_xor64(v, 15), 16), 32); }
+// the smallest v over the wave, in every lane
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m <= 32; m <<= 1) {
+        const uint64_t y = lane_xor64(v, m);
+        v = y < v ? y : v;
+    }
+    return v;
 }
 
 // ascending bitonic sort of one key per lane across the wave
@@ -212,7 +245,7 @@ __device__ __forceinline__ uint64_t wave_sort64(uint64_t x, int lane) {
     for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t y = shfl_xor64(x, j);
+            const uint64_t y = lane_xor64(x, j);
             const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
             x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
         }
@@ -227,14 +260,11 @@ __device__ __forceinline__ uint64_t wave_sort64(uint64_t x, int lane) {
 static __device__ __attribute__((noinline)) uint64_t topk_insert(uint64_t list, uint64_t x, uint64_t thr, uint64_t m,
                                                                   int k, int lane) {
     if (__popcll(m) > 3) {
-        uint64_t xs = wave_sort64(x < thr ? x : ~0ull, lane);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)xs, 63 - lane);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(xs >> 32), 63 - lane);
-        const uint64_t rev = ((uint64_t)hi << 32) | lo;
+        const uint64_t rev = lane_rev64(wave_sort64(x < thr ? x : ~0ull, lane));
         uint64_t y = list < rev ? list : rev;  // bitonic: the 64 smallest of both lists
 #pragma unroll
         for (int j = 32; j > 0; j >>= 1) {
-            const uint64_t z = shfl_xor64(y, j);
+            const uint64_t z = lane_xor64(y, j);
             y = (lane & j) ? (y < z ? z : y) : (y < z ? y : z);
         }
         return y;

@@ -837,83 +837,120 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the low n bits
+__device__ __forceinline__ uint64_t low_bits(uint32_t n) { return n >= 64u ? ~0ull : ((1ull << n) - 1ull); }
+
+// The k smallest keys of nl ascending k-lists (list w at at(w), read with L1-bypassing loads), ascending
+// in lanes < k, by one wave.  Any k distinct keys of the lists bound the k-th smallest from above:
+// t0 = the smaller of the k-th smallest list head (when there are >= k lists: a wave sort of each
+// lane's smallest head) and the smallest k-th key of a list.  Only keys <= t0 are gathered, into buf
+// (LDS, 64 keys) while they fit, and sorted once; a list is read only down to its first key past t0.
+// (The k-th keys alone bound it loosely: ~450 of a cfg-2 XCD group's 1,280 keys pass.)  More than 64
+// such keys take the push path.  The 128 lists of a one-query launch's XCD group went through five
+// 64-key sort-and-merge pushes per wave before.
+template <class At>
+__device__ __forceinline__ uint64_t merge_lists(At at, int nl, int k, uint64_t* buf, int lane) {
+    uint64_t tk = ~0ull, hd = ~0ull;
+    for (int w = lane; w < nl; w += 64) {
+        const uint64_t x = ld_agent(at(w) + k - 1), h = ld_agent(at(w));
+        tk = x < tk ? x : tk;
+        hd = h < hd ? h : hd;
+    }
+    uint64_t t0 = wave_min64(tk);
+    if (nl >= k) {
+        const uint64_t th = rdlane64(wave_sort64(hd, lane), k - 1);
+        t0 = th < t0 ? th : t0;
+    }
+    uint32_t ns = 0;
+    for (int w0 = 0; w0 < nl; w0 += 64) {
+        const int w = w0 + lane;
+        const uint64_t* L = at(min(w, nl - 1));
+        for (int e0 = 0; e0 < k; e0 += 4) {
+            uint64_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = (w < nl && e0 + u < k) ? ld_agent(L + e0 + u) : ~0ull;
+            bool more = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool in = x[u] <= t0 && x[u] != ~0ull;
+                const uint64_t m = __ballot(in);
+                const uint32_t pos = ns + (uint32_t)__popcll(m & low_bits((uint32_t)lane));
+                if (in && pos < 64u) buf[pos] = x[u];
+                ns += (uint32_t)__popcll(m);
+                more = in;  // the batch's last key in range: the list may hold more below t0
+            }
+            if (!__ballot(more)) break;  // ascending lists: nothing further down is <= t0
+        }
+    }
+    if (ns <= 64u) return wave_sort64(lane < (int)ns ? buf[lane] : ~0ull, lane);
+    uint64_t acc = ~0ull;
+    for (int w0 = 0; w0 < nl; w0 += 64) {
+        const int w = w0 + lane;
+        const uint64_t* L = at(min(w, nl - 1));
+        for (int e = 0; e < k; ++e) {
+            const uint64_t x = w < nl ? ld_agent(L + e) : ~0ull;
+            const bool in = x <= t0 && x != ~0ull;
+            if (!__ballot(in)) break;
+            topk_push(acc, in ? x : ~0ull, k, lane);
+        }
+    }
+    return acc;
+}
+
 // The scans' (K5, K1) fused cross-block merge, in two levels.  The workgroups of group g = bx mod 8 (with the
 // round-robin dispatch, the workgroups of one XCD) publish their k-lists and take a ticket on the
-// group's counter; the group's last workgroup merges the group's lists (all four waves) into slot
-// nbx + g and takes a ticket on the query's counter; the last of those merges the <= 8 group
-// lists into out[row].  Each counter sees ~nbx / 8 tickets: with one counter for all 1,024
-// workgroups of a one-query launch the tail cost ~15 us of a 185 us launch (r4n, a no-merge build).
-// parts: per query (nbx + 8) lists of k keys.  Hand-offs (pf_device.h take_ticket): a list is
-// published with write-through stores drained before an acquire-release ticket and read with
-// L1-bypassing loads after it.
-__device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, int* misc, ScanSync* __restrict__ sync,
+// group's counter; the group's last workgroup merges the group's lists into slot nbx + g and takes
+// a ticket on the query's counter; the last of those merges the <= 8 group lists into out[row].
+// Each counter sees ~nbx / 8 tickets: with one counter for all 1,024 workgroups of a one-query
+// launch the tail cost ~15 us of a 185 us launch (r4n, a no-merge build).  After the workgroup's
+// own list only wave 0 runs: no barrier on the launch's critical path past the last block.
+// parts: per query (nbx + 8) lists of k keys.  sc: LDS for max(nw * k, 64) keys.  Hand-offs
+// (pf_device.h take_ticket): a list is published with write-through stores drained before the
+// ticket and read with L1-bypassing loads after it.
+__device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, ScanSync* __restrict__ sync,
                                           uint64_t* __restrict__ parts, uint64_t* __restrict__ out,
                                           const int32_t* __restrict__ out_rows, int qy, int bx, int nbx) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
     __syncthreads();
     if (lane < k) sc[wave * k + lane] = list;
     __syncthreads();
+    if (wave != 0) return;
     ScanSync* sy = sync + qy;
     uint64_t* qparts = parts + (size_t)qy * (nbx + 8) * k;
     const int ng = min(8, nbx), g = bx % ng, n_g = (nbx - g + ng - 1) / ng;
-    auto merge_sc = [&]() {  // wave 0: the nw wave lists in sc
-        uint64_t acc = ~0ull;
+    uint64_t acc;
+    {  // the workgroup's list: its waves' lists (one sort when they fit a wave)
         const int n = nw * k;
-        for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
-        return acc;
-    };
-    if (wave == 0) {
-        const uint64_t acc = merge_sc();
-        if (lane < k) st_agent(qparts + (size_t)bx * k + lane, acc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // program order: stores, wait, ticket
-        unsigned t = 0;
-        if (lane == 0) t = take_ticket(&sy->grp[g * 16]);
-        if (lane == 0) misc[0] = t == (unsigned)n_g - 1u;
+        if (n <= 64) {
+            acc = wave_sort64(lane < n ? sc[lane] : ~0ull, lane);
+        } else {
+            acc = ~0ull;
+            for (int b = 0; b < n; b += 64) topk_push(acc, b + lane < n ? sc[b + lane] : ~0ull, k, lane);
+        }
     }
-    __syncthreads();
-    if (!misc[0]) return;
+    if (lane < k) st_agent(qparts + (size_t)bx * k + lane, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // program order: stores, wait, ticket
+    unsigned t = 0;
+    if (lane == 0) t = take_ticket(&sy->grp[g * 16]);
+    t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+    if (t != (unsigned)n_g - 1u) return;
     ticket_acquire();
-    // the group's lists: workgroups g, g + ng, ... (n_g * k keys over the waves, 4 loads in flight)
-    {
-        uint64_t l2 = ~0ull;
-        const int n = n_g * k;
-        for (int base = wave * 256; base < n; base += nw * 256) {
-            uint64_t x[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = base + u * 64 + lane;
-                x[u] = ~0ull;
-                if (i < n) {
-                    const int w = i / k;
-                    x[u] = ld_agent(qparts + (size_t)(g + w * ng) * k + (i - w * k));
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) topk_push(l2, x[u], k, lane);
-        }
-        __syncthreads();
-        if (lane < k) sc[wave * k + lane] = l2;
-        __syncthreads();
-    }
-    if (wave == 0) {
-        const uint64_t acc = merge_sc();
-        if (lane < k) st_agent(qparts + (size_t)(nbx + g) * k + lane, acc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        unsigned t = 0;
-        if (lane == 0) t = take_ticket(&sy->done);
-        t = (unsigned)__shfl((int)t, 0);
-        if (t == (unsigned)ng - 1u) {
-            ticket_acquire();
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            uint64_t fin = ~0ull;
-            const int n = ng * k;
-            for (int b = 0; b < n; b += 64) topk_push(fin, b + lane < n ? ld_agent(qparts + (size_t)nbx * k + b + lane) : ~0ull, k, lane);
-            const int row = out_rows ? out_rows[qy] : qy;
-            if (lane < k) out[(size_t)row * k + lane] = fin;
-        }
-    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    // the group's lists: workgroups g, g + ng, ...
+    acc = merge_lists([&](int w) { return qparts + (size_t)(g + w * ng) * k; }, n_g, k, sc, lane);
+    if (lane < k) st_agent(qparts + (size_t)(nbx + g) * k + lane, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    t = 0;
+    if (lane == 0) t = take_ticket(&sy->done);
+    t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+    if (t != (unsigned)ng - 1u) return;
+    ticket_acquire();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t fin = merge_lists([&](int w) { return qparts + (size_t)(nbx + w) * k; }, ng, k, sc, lane);
+    const int row = out_rows ? out_rows[qy] : qy;
+    if (lane < k) out[(size_t)row * k + lane] = fin;
 }
 
 template <bool PACKED, bool GTAB>
@@ -997,7 +1034,7 @@ __global__ __launch_bounds__(kScanThreads, 4) void fas_scan_kernel(DevStore st, 
         }
         topk_push(list, key, k, lane);
     }
-    post_tail(list, k, reinterpret_cast<uint64_t*>(scratch), reinterpret_cast<int*>(v.hits), sync, parts, out,
+    post_tail(list, k, reinterpret_cast<uint64_t*>(scratch), sync, parts, out,
               out_rows, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x);
 }
 
@@ -1089,7 +1126,6 @@ __device__ __forceinline__ uint32_t k5_chk(uint32_t i, uint32_t n, int what) {
 #define K5CHK(i, n, w) (i)
 #endif
 
-__device__ __forceinline__ uint64_t low_bits(uint32_t n) { return n >= 64u ? ~0ull : ((1ull << n) - 1ull); }
 
 // entries of list L for candidates [c0, c1] (cells c0 >> shift .. c1 >> shift)
 __device__ __forceinline__ uint2 list_range(const PostStore& ps, const PList& L, uint32_t c0, uint32_t c1) {
@@ -1783,7 +1819,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     // tail scratch in the (idle) slots: merge keys, then flag / threshold / block ids
     uint64_t* sc = reinterpret_cast<uint64_t*>(slot);
 
-    post_tail(best, k, sc, reinterpret_cast<int*>(sc + kPostWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
+    post_tail(best, k, sc, sync, parts, out, out_rows, qy, bx, nbx);
 }
 
 // ---------------------------------------------------------------- K5s: wave-private slice scan
@@ -2276,7 +2312,7 @@ __global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
         best = (best & 0xFFFFFFFF00000000ull) | (ps.hdr[2 * (size_t)idx + 1].w ^ 0x80000000u);
     }
     uint64_t* sc = reinterpret_cast<uint64_t*>(wbase0 + kWsMask);  // wave 0's masks + slots (post_tail syncs first)
-    post_tail(best, k, sc, reinterpret_cast<int*>(sc + kSliceWaves * kMaxTopK), sync, parts, out, out_rows, qy, bx, nbx);
+    post_tail(best, k, sc, sync, parts, out, out_rows, qy, bx, nbx);
 }
 
 // ---------------------------------------------------------------- K2: merge

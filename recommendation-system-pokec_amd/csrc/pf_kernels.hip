@@ -1095,10 +1095,11 @@ constexpr uint32_t kMapWords = kRoundCap / 64;
 constexpr uint32_t kLdsMapB = (kLdsCidx + 7) & ~7u;                            // u64 [2][kMapWords]
 constexpr uint32_t kLdsMapN = kLdsMapB + 2 * 8 * kMapWords;                   // uint2 [2][kRoundToks]
 constexpr uint32_t kLdsMapC = kLdsMapN + 2 * 8 * kRoundToks;                  // u8 [2][kMapWords]
-// per query column number: its token range j0 | j1 << 16; per active column index c: the column
-// numbers of active columns < c as a mask (a round's columns [ca, ce) = cpre[ce] & ~cpre[ca])
-constexpr uint32_t kLdsColj = (kLdsMapC + 2 * kMapWords + 7) & ~7u;           // u32 [kPostMaxCols]
-constexpr uint32_t kLdsCpre = kLdsColj + 4 * kPostMaxCols;                    // u64 [kPostMaxCols + 1]
+// per column number of the current round: the round-relative tokens before its end (a mask); per
+// active column index c: the column numbers of active columns < c as a mask (a round's columns
+// [ca, ce) = cpre[ce] & ~cpre[ca])
+constexpr uint32_t kLdsLmk = (kLdsMapC + 2 * kMapWords + 7) & ~7u;            // u64 [kPostMaxCols]
+constexpr uint32_t kLdsCpre = kLdsLmk + 8 * kPostMaxCols;                     // u64 [kPostMaxCols + 1]
 constexpr uint32_t kPostFixedLds = (kLdsCpre + 8 * (kPostMaxCols + 1) + 15) & ~15u;
 static_assert(kBlockCands == 2 * kPostThreads, "two candidates per thread");
 static_assert(kRoundCap < 65536 && kBlockCands <= kRoundCap, "u16 slots; a one-token round fits");
@@ -1313,13 +1314,12 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     uint64_t* mapb = reinterpret_cast<uint64_t*>(base + kLdsMapB);
     uint2* mapn = reinterpret_cast<uint2*>(base + kLdsMapN);
     uint8_t* mapc = reinterpret_cast<uint8_t*>(base + kLdsMapC);
-    uint32_t* colj = reinterpret_cast<uint32_t*>(base + kLdsColj);
+    uint64_t* lmk = reinterpret_cast<uint64_t*>(base + kLdsLmk);
     uint64_t* cpre = reinterpret_cast<uint64_t*>(base + kLdsCpre);
     stage(smem, img, sizeof(QConst));
     for (int j = tid; j < H.n_act; j += kPostThreads) {
         const QCol c = cols[j];
         scol[j] = c;
-        colj[c.t] = (uint32_t)c.j0 | (uint32_t)c.j1 << 16;
         for (int x = c.j0; x < c.j1; ++x) colof[x] = (uint8_t)j;
     }
     if (tid == 0) {  // prefix masks of the active columns (<= 48, ascending)
@@ -1536,6 +1536,12 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     seg[tid] = (uint32_t)lo | (uint32_t)hi << 8 | (uint32_t)c.t << 16 |
                                ((c.j0 < ja || c.j1 > jb) ? kSegSplit : 0u);
                 }
+                // per round column (number t): the round-relative tokens before its end (the owner sums
+                // take a candidate's hits in t as the mask bits below lmk[t] not taken by earlier columns)
+                if (tid < R.ce - R.ca) {
+                    const QCol c = scol[R.ca + tid];
+                    lmk[c.t] = low_bits((uint32_t)(min((int)c.j1, jb) - ja));
+                }
                 if (tid == 0) misc[1] = 0u;
                 // a. walk: the round's entries flattened over the workgroup, all loads in flight
                 constexpr int U = kRoundCap / kPostThreads;
@@ -1698,6 +1704,14 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             // e. the owners add the round's common columns in ascending order (the candidate's
             // columns among the round's: ~3 per round instead of every round column)
             const uint64_t rtm = cpre[R.ce] & ~cpre[R.ca];  // the round's columns, by column number
+            // the round's split columns (<= 2, the only ones not wholly inside it): its first if that
+            // began in an earlier round, its last if that goes on past it (column numbers, or -1)
+            int t_in = -1, t_on = -1;
+            if (R.ce > R.ca) {
+                const QCol cf = scol[R.ca], cl = scol[R.ce - 1];
+                if (cf.j0 < ja) t_in = cf.t;
+                if (cl.j1 > jb) t_on = cl.t;
+            }
 #pragma unroll
             for (int kk = 0; kk < kCandsPerThread; ++kk) {
                 const int p = kk * kPostThreads + tid;
@@ -1707,14 +1721,12 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 uint32_t rr = F > 0 ? hbase[p] : 0u;
                 for (uint64_t pr = pend[kk] & rtm; pr; pr &= pr - 1) {
                     const int t = __ffsll((unsigned long long)pr) - 1;
-                    const uint32_t cj = colj[t];
-                    const int cj0 = (int)(cj & 0xFFFFu), cj1 = (int)(cj >> 16);
-                    const uint64_t lm = low_bits((uint32_t)(min(cj1, jb) - ja));
+                    const uint64_t lm = lmk[t];  // (stale in an empty round: mr is 0 there)
                     const uint64_t h = mr & lm;
                     mr &= ~lm;
                     const uint32_t r0 = rr;
                     rr += (uint32_t)__popcll(h);
-                    if (cj0 >= ja && cj1 <= jb) {
+                    if (t != t_in && t != t_on) {
                         sum[kk] += h ? slot[r0] : q.sig0_col[t];
                         continue;
                     }
@@ -1730,7 +1742,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                         cnrm[kk] = slot[r0];
                         chit |= 1u << kk;
                     }
-                    if (cj1 <= jb) {
+                    if (t != t_on) {
                         const bool hh = (chit >> kk) & 1u;
                         sum[kk] += (hh && cdot[kk] != 0.0) ? text_term(q, t, cdot[kk], cnrm[kk]) : q.sig0_col[t];
                         cdot[kk] = 0.0;

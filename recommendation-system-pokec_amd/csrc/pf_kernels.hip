@@ -1631,10 +1631,11 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const bool first = (below >> lo) == 0ull;
                     hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     // the column's first hit holds its norm, the others their product (one per lane here,
-                    // so the terms below only add them up); the first also records its column's hit count
-                    // in the round (item[r], read once by the compaction below)
+                    // so the terms below only add them up); the first hit of a column wholly inside the
+                    // round records the column's hit count in the round (>= 1), every other slot 0 (item[r],
+                    // read once by the compaction below)
                     slot[r] = first ? kn[u] : tok_product(pt, ja + (int)jr, tf);
-                    if (first) item[r] = (uint16_t)hit_run(mask[p], lo, (sg >> 8) & 0xFFu);
+                    item[r] = (first && !(sg & kSegSplit)) ? (uint16_t)hit_run(mask[p], lo, (sg >> 8) & 0xFFu) : (uint16_t)0;
                 }
                 for (uint32_t f = (uint32_t)(tid + kRoundCap); f < F; f += kPostThreads) {
                     const int j = round_list(gpre, ja, jb, g0 + f);
@@ -1649,7 +1650,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                     const bool first = (below >> (sg & 0xFFu)) == 0ull;
                     hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
                     slot[r] = first ? ps.pnorm[x] : tok_product(pt, ja + (int)jr, e & 0xFFu);
-                    if (first) item[r] = (uint16_t)hit_run(mask[p], sg & 0xFFu, (sg >> 8) & 0xFFu);
+                    item[r] = (first && !(sg & kSegSplit)) ? (uint16_t)hit_run(mask[p], sg & 0xFFu, (sg >> 8) & 0xFFu) : (uint16_t)0;
                 }
                 K5T(7);
                 __syncthreads();
@@ -1663,13 +1664,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                 uint32_t ni = 0;
                 for (uint32_t r0 = wb; r0 < wb + wn; r0 += 64) {
                     const uint32_t r = r0 + (uint32_t)lane;
-                    bool is = false;
-                    uint32_t run = 0;
-                    if (r < wb + wn) {
-                        const uint32_t h = hit[r];
-                        run = item[r];
-                        is = (h & kHitFirst) && !(seg[(h >> 8) & 63u] & kSegSplit);
-                    }
+                    const uint32_t run = r < wb + wn ? (uint32_t)item[r] : 0u;
+                    const bool is = run != 0u;
                     const uint64_t bal = __ballot(is);
                     wave_sync();
                     if (is) wit[ni + (uint32_t)__popcll(bal & low_bits((uint32_t)lane))] = (uint16_t)(r | run << kItemRunShift);

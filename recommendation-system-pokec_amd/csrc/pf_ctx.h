@@ -119,8 +119,8 @@ struct JobsState {
     // stream (both latency-bound, independent), joined before the pair kernel
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // K7 (clubs), the clubs jobs' K8 and a chunk's result copies run on aux2 after its pair
-    // kernel (Ws::ev_pairs), beside K4' and the next chunk (pf_jobs_plan.cpp launch_chunk)
+    // K4' (collaborative), K8, K7 (clubs) and a chunk's result copies run on aux2 after its pair
+    // kernel (Ws::ev_pairs), beside the next chunk's pair kernel (pf_jobs_plan.cpp launch_chunk)
     hipStream_t aux2 = nullptr;
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
@@ -143,7 +143,7 @@ struct JobsState {
         int64_t acc_jobs = 0;      // clubs jobs the accumulators hold
         PinBuf h_plan, h_out;
         hipEvent_t done = nullptr;  // recorded after the chunk's result copies (on aux2)
-        hipEvent_t ev_pairs = nullptr, ev_main = nullptr;  // the pair kernel / K4' + K8 queued on the context's stream
+        hipEvent_t ev_pairs = nullptr, ev_main = nullptr;  // the pair kernel queued on the context's stream / K4' + K8 there (collab_main=1)
         ~Ws() {
             if (done) (void)hipEventDestroy(done);
             if (ev_pairs) (void)hipEventDestroy(ev_pairs);

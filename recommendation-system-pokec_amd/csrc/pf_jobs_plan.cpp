@@ -1052,26 +1052,30 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
-    // K7 (clubs, one latency-bound wave per job) and its jobs' K8 go to the second aux stream once
-    // the pairs are scored, beside K4' and the next chunk's gathers and pair kernel (r4k trace: K7
-    // ran 0.8-1.4 ms per cfg-5 chunk between two pair kernels with the device mostly idle); the
-    // chunk's result copies follow there after the context stream's K4' / K8 (W.ev_main), and
-    // W.done is recorded last on that stream.  Jobs write disjoint regions of the slot's buffers.
+    // K4' (collaborative, fused top-k), the interest jobs' K8, K7 (clubs) and its jobs' K8 go to the
+    // second aux stream once the pairs are scored, so the context's stream goes straight on to the
+    // next chunk's pair kernel (cfg-3 trace r7e: K4' + K8 ~40 us of every ~400-us step sat between
+    // two pair kernels); K7 ran 0.8-1.4 ms per cfg-5 chunk between two pair kernels with the device
+    // mostly idle (r4k).  The chunk's result copies follow there, and W.done is recorded last on
+    // that stream.  Jobs write disjoint regions of the slot's buffers.  (PF_DEBUG collab_main=1: K4'
+    // and K8 on the context's stream as before, the A/B)
     const hipStream_t s2 = J.aux2;
+    static const bool collab_main = debug_long("collab_main", 0) != 0;
+    const hipStream_t sc = collab_main ? s : s2;
     HIPCHK(c, hipEventRecord(W.ev_pairs, s));
+    HIPCHK(c, hipStreamWaitEvent(s2, W.ev_pairs, 0));
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
                             W.d_slots.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(), W.d_parts.as<uint64_t>(),
-                            d_tk, d_keys, ktop, s));
+                            d_tk, d_keys, ktop, sc));
     HIPCHK(c, launch_job_topk(d_dj, d_jt, n_topk_main, W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
-                              W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, s));
-    HIPCHK(c, hipEventRecord(W.ev_main, s));
-    HIPCHK(c, hipStreamWaitEvent(s2, W.ev_pairs, 0));
+                              W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, sc));
+    if (collab_main) HIPCHK(c, hipEventRecord(W.ev_main, s));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
                            W.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                            d_ncand, (int64_t)J.js.n_club_ids, s2));
     HIPCHK(c, launch_job_topk(d_dj, d_jt + n_topk_main, (int)jix_topk.size() - n_topk_main, W.d_fl.as<float>(),
                               W.d_ids.as<int32_t>(), W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, s2));
-    HIPCHK(c, hipStreamWaitEvent(s2, W.ev_main, 0));
+    if (collab_main) HIPCHK(c, hipStreamWaitEvent(s2, W.ev_main, 0));
     // ---- results: keys (top-k jobs), counts, the fail flag; full lists for the others
     std::vector<int32_t> tpos(dj.size(), -1);
     for (size_t t = 0; t < jix_topk.size(); ++t) tpos[jix_topk[t]] = (int32_t)t;

@@ -14,7 +14,7 @@
 //   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; A/B)
 //   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
 //   collab_main=1         the job pipeline's K4' / K8 on the context's stream after the pair kernel
-//                         instead of the second aux stream (A/B)
+//                         also in chunks without clubs jobs (A/B)
 //   k5_xcd=0|1            K5: contiguous block ranges per XCD in each static round (default 1; A/B)
 //   k5_tail=N             K5: candidates per claimed block past a one-query launch's static rounds
 //                         (default 0 = whole blocks; A/B)

@@ -1052,16 +1052,18 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
             }
     }
     hl.lap(kHpCollab);  // images, gathers, pairs launched
-    // K4' (collaborative, fused top-k), the interest jobs' K8, K7 (clubs) and its jobs' K8 go to the
-    // second aux stream once the pairs are scored, so the context's stream goes straight on to the
-    // next chunk's pair kernel (cfg-3 trace r7e: K4' + K8 ~40 us of every ~400-us step sat between
-    // two pair kernels); K7 ran 0.8-1.4 ms per cfg-5 chunk between two pair kernels with the device
-    // mostly idle (r4k).  The chunk's result copies follow there, and W.done is recorded last on
-    // that stream.  Jobs write disjoint regions of the slot's buffers.  (PF_DEBUG collab_main=1: K4'
-    // and K8 on the context's stream as before, the A/B)
+    // K7 (clubs) and its jobs' K8 go to the second aux stream once the pairs are scored (K7 ran
+    // 0.8-1.4 ms per cfg-5 chunk between two pair kernels with the device mostly idle, r4k), and so
+    // do K4' (collaborative, fused top-k) and the interest jobs' K8 when the chunk has no clubs jobs:
+    // the context's stream then goes straight on to the next chunk's pair kernel (cfg-3 trace r7e:
+    // K4' + K8 took ~40 us of every ~400-us step between two pair kernels; cfg3 +9 %, r7g).  With
+    // clubs jobs K4' stays on the context's stream beside K7 (behind K7 on one stream, cfg 5 ran
+    // 148k-162k vs 166k-171k users/s, r7h).  The chunk's result copies follow on the aux stream and
+    // W.done is recorded last there.  Jobs write disjoint regions of the slot's buffers.
+    // (PF_DEBUG collab_main=1: K4' and K8 on the context's stream always, the A/B)
     const hipStream_t s2 = J.aux2;
     static const bool collab_main = debug_long("collab_main", 0) != 0;
-    const hipStream_t sc = collab_main ? s : s2;
+    const hipStream_t sc = (collab_main || !jix_clubs.empty()) ? s : s2;
     HIPCHK(c, hipEventRecord(W.ev_pairs, s));
     HIPCHK(c, hipStreamWaitEvent(s2, W.ev_pairs, 0));
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),

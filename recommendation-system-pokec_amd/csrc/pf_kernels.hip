@@ -1305,8 +1305,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const int nsets = H.n_club + H.n_friend;
     const int nl = H.n_tok + nsets;
     PTok* pt = reinterpret_cast<PTok*>(base + kPostFixedLds);
-    PList* pl = reinterpret_cast<PList*>(pt + H.n_tok);
-    uint2* rng = reinterpret_cast<uint2*>(pl + nl);
+    // (the list descriptors are not staged: each block reads them from the image, an L2 hit, so a
+    // query with ~200 tokens still fits four workgroups per CU)
+    uint2* rng = reinterpret_cast<uint2*>(pt + H.n_tok);
     uint2* rtab = rng + nl;  // the block's rounds (ja | jb << 16, ca | ce << 16), <= n_tok of them
     uint32_t* gpre = reinterpret_cast<uint32_t*>(rtab + H.n_tok + 1);
     uint32_t* spre = gpre + H.n_tok + 1;  // the set lists' prefix [nsets + 1]
@@ -1332,10 +1333,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
         const QTok t = toks[j];
         pt[j] = PTok{t.wq, t.idf};
-        pl[j] = t.l;
     }
-    for (int j = tid; j < nsets; j += kPostThreads) pl[H.n_tok + j] = sets[j];
-    __syncthreads();  // the staged lists are read by other threads (ranges: thread j takes list j)
+    __syncthreads();  // the staged tables are read by other threads
     const QConst& q = *reinterpret_cast<const QConst*>(smem);
     uint64_t best = ~0ull;
 #ifdef PF_K5_TIMERS
@@ -1395,7 +1394,8 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
             ha[kk] = ps.hdr[2 * (size_t)c];
             hb[kk] = ps.hdr[2 * (size_t)c + 1];
         }
-        for (int j = tid; j < nl; j += kPostThreads) rng[j] = list_range(ps, pl[j], c0, c1);
+        for (int j = tid; j < nl; j += kPostThreads)
+            rng[j] = list_range(ps, j < H.n_tok ? toks[j].l : sets[j - H.n_tok], c0, c1);
 #pragma unroll
         for (int kk = 0; kk < kCandsPerThread; ++kk) {
             const uint32_t c = c0 + kk * kPostThreads + tid;
@@ -2457,7 +2457,7 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds) {
 // K5 dynamic LDS: QConst | fixed per-block arrays | PTok[n_tok] | PList[n_lists] | ranges[n_lists] |
 // rounds[n_tok + 1] | token prefix[n_tok + 1] | set prefix[n_sets + 1] | token -> column u8[n_tok]
 uint32_t post_var_lds(int n_tok, int n_lists) {
-    return (uint32_t)(sizeof(PTok) * n_tok + (sizeof(PList) + 8) * n_lists + 8 * (n_tok + 1) + 4 * (n_tok + 1) +
+    return (uint32_t)(sizeof(PTok) * n_tok + 8 * n_lists + 8 * (n_tok + 1) + 4 * (n_tok + 1) +
                       4 * (n_lists - n_tok + 1) + n_tok + 15) & ~15u;
 }
 uint32_t post_lds(uint32_t var_lds) { return (uint32_t)sizeof(QConst) + kPostFixedLds + var_lds; }

@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/r7t && mkdir -p $O
+for v in cur base cur base cur base; do
+  L=""; [ $v = base ] && L="env PF_LIB_PATH=$PWD/vlib/base/libpokec_fas.so"
+  timeout -k 10 300 $L python3 bench.py --workload cfg3 --steps 400 --warmup 10 --no-pmc --no-cpu-baseline > $O/cfg3_$v.json 2> $O/cfg3_$v.err || exit 1
+  (echo -n "$v "; cat $O/cfg3_$v.json) >> $O/cfg3_all.txt
+done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || exit 2

@@ -896,6 +896,10 @@ def main():
                     help="cfg4 at N = 1: also time each of S shards alone on this GPU and project the N = S "
                          "step (solo_shards record)")
     ap.add_argument("--solo-steps", type=int, default=3, help="timed steps per shard of --solo-shards")
+    ap.add_argument("--same-query", action="store_true",
+                    help="cfg2/cfg4 analysis only (not the workload): every query of every step is the first "
+                         "query of the stream, so a batch's lists are all shared (bounds what a query-tiled "
+                         "batch could save; the line's config says so)")
     ap.add_argument("--n1-steps", type=int, default=5,
                     help="N > 1: steps rank 0 times the same workload unsharded on its own GPU (n1_same_workload)")
     args = ap.parse_args()
@@ -977,6 +981,8 @@ def main():
     steps, warm = args.steps, args.warmup
     rng = np.random.default_rng(3 if cfg4 else 2)  # same query stream on every rank (SURVEY D1 seeds)
     qstream = rng.integers(1, args.users + 1, size=(warm + steps, Q)).astype(np.int32)
+    if args.same_query:  # analysis: perfect list sharing inside every batch (not the metric's workload)
+        qstream[:] = qstream[0, 0]
     # a dedicated stream: the engine, the all-gather and the copies are all ordered on it
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -1104,8 +1110,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded Pokec-shaped corpus, tools/pokec_synth.cpp; no Pokec data offline)",
-        "config": {"workload": wl_name,
-                   "workload_key": workload, "n_users": args.users, "queries_per_step": Q, "topk": k,
+        "config": {"workload": wl_name + (" [ANALYSIS: --same-query, every query the same user]" if args.same_query else ""),
+                   "workload_key": workload + ("_samequery" if args.same_query else ""), "n_users": args.users,
+                   "queries_per_step": Q, "topk": k,
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,

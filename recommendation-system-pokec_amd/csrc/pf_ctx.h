@@ -122,6 +122,7 @@ struct JobsState {
     // K4' (collaborative), K8, K7 (clubs) and a chunk's result copies run on aux2 after its pair
     // kernel (Ws::ev_pairs), beside the next chunk's pair kernel (pf_jobs_plan.cpp launch_chunk)
     hipStream_t aux2 = nullptr;
+    int pp = 0;  // the last chunk's ping-pong stream (1: aux, 0: the context's; pf_jobs_plan.cpp launch_chunk)
     std::unordered_set<int32_t> edited;          // uids whose adj_list row differs from the open-time row
     // open-time row of each edited uid (present, row): an edit back to it drops the override
     std::unordered_map<int32_t, std::pair<bool, std::vector<int32_t>>> orig;

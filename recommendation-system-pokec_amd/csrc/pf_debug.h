@@ -13,6 +13,8 @@
 //   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 16; A/B)
 //   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; A/B)
 //   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
+//   chunk_pingpong=0      the job pipeline's chunks all gather on the aux stream and score on the
+//                         context's stream behind an event (A/B; default: alternate the two)
 //   collab_main=1         the job pipeline's K4' / K8 on the context's stream after the pair kernel
 //                         also in chunks without clubs jobs (A/B)
 //   k5_xcd=0|1            K5: contiguous block ranges per XCD in each static round (default 1; A/B)

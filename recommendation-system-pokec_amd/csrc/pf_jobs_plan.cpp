@@ -960,8 +960,19 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     // the plan goes up on the aux stream, where this chunk's gathers follow it at once: they run
     // beside the previous chunk's pair kernel (their slot's buffers were released when that slot's
     // previous chunk was unpacked); r3ab: cfg 3 +3 % over forking them from the context's stream
-    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, J.aux));
-    HIPCHK(c, hipEventRecord(J.ev_fork, J.aux));
+    // Ping-pong (default): consecutive chunks alternate between the aux stream and the context's
+    // stream for their upload, gathers, images and pair kernel, so a chunk's pair kernel follows
+    // its own gathers in stream order (no cross-stream wait in front of it: ~20 us per chunk in the
+    // r7l trace) and may start beside the previous chunk's pair kernel.  A chunk's workspace slot is
+    // reused only after its W.done (the caller waits it), so the two streams never share a slot's
+    // buffers in flight.  (PF_DEBUG chunk_pingpong=0: the gathers on the aux stream, the images
+    // and the pair kernel on the context's stream behind an event, as before)
+    static const bool pingpong = debug_long("chunk_pingpong", 1) != 0;
+    if (pingpong) J.pp ^= 1;
+    const hipStream_t up = (!pingpong || J.pp) ? J.aux : s;  // upload, K9, K3, dispatch orders
+    const hipStream_t sp = pingpong ? up : s;                // images, pair kernel, K4' / K8 with clubs
+    HIPCHK(c, hipMemcpyAsync(W.d_plan.p, h, total, hipMemcpyHostToDevice, up));
+    if (!pingpong) HIPCHK(c, hipEventRecord(J.ev_fork, up));
     uint8_t* d = W.d_plan.as<uint8_t>();
     const DevJob* d_dj = reinterpret_cast<const DevJob*>(d + o_dj);
     const int32_t* d_p32 = reinterpret_cast<const int32_t*>(d + o_p32);
@@ -1001,24 +1012,24 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         if (want > W.acc_jobs) {
             const size_t words = (size_t)want * (size_t)std::max(J.js.n_club_ids, 1);
             HIPCHK(c, W.d_acc.ensure(words * 8));
-            HIPCHK(c, hipMemsetAsync(W.d_acc.p, 0, W.d_acc.cap, s));
+            HIPCHK(c, hipMemsetAsync(W.d_acc.p, 0, W.d_acc.cap, sp));
             W.acc_jobs = want;
         }
     }
     // ---- the stages, in stream order; the gathers and dispatch orders run on the aux stream and
     // join before the pair kernel, beside the images
-    HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, fail word) is up
-    HIPCHK(c, launch_expand_pairs(d_gen, (int)gens.size(), d_gpool, (int)nblk, d_blk, J.aux));  // K9: the blocks
+    if (!pingpong) HIPCHK(c, hipStreamWaitEvent(s, J.ev_fork, 0));  // the plan (images, fail word) is up
+    HIPCHK(c, launch_expand_pairs(d_gen, (int)gens.size(), d_gpool, (int)nblk, d_blk, up));  // K9: the blocks
     HIPCHK(c, launch_gather(J.js, J.view, d_dj, (int)dj.size(), d_p32, d_p64, W.d_ht.as<int32_t>(),
                             W.d_seq.as<int32_t>(), W.d_slots.as<int32_t>(), W.d_ids.as<int32_t>(),
-                            d_ncand, J.aux));
+                            d_ncand, up));
     for (int k = 0, o = 0; k < 3; o += nb_c[k++])  // each launch's dispatch order (relative to its blocks)
-        HIPCHK(c, launch_order_pairs(d_blk + o, nb_c[k], W.d_slots.as<int32_t>(), hc.n, d_ord + o, J.aux));
-    HIPCHK(c, hipEventRecord(J.ev_join, J.aux));
+        HIPCHK(c, launch_order_pairs(d_blk + o, nb_c[k], W.d_slots.as<int32_t>(), hc.n, d_ord + o, up));
+    if (!pingpong) HIPCHK(c, hipEventRecord(J.ev_join, up));
     if (!resident)
         HIPCHK(c, launch_qimages(c->ds, J.js, d_ij, n_small, n_lds - n_small, (int)ij.size() - n_lds,
-                                 W.d_img.as<uint8_t>(), W.d_scr.as<uint32_t>(), d_fail, s));
-    HIPCHK(c, hipStreamWaitEvent(s, J.ev_join, 0));
+                                 W.d_img.as<uint8_t>(), W.d_scr.as<uint32_t>(), d_fail, sp));
+    if (!pingpong) HIPCHK(c, hipStreamWaitEvent(s, J.ev_join, 0));
     const bool any_pairs = nblk > 0;
     hipEvent_t pe0 = nullptr, pe1 = nullptr;
     if ((J.stats_on || J.stats_count) && any_pairs) {
@@ -1031,20 +1042,20 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
         pe0 = J.stat_ev[J.stat_used].first;
         pe1 = J.stat_ev[J.stat_used].second;
         ++J.stat_used;
-        HIPCHK(c, hipEventRecord(pe0, s));
+        HIPCHK(c, hipEventRecord(pe0, sp));
     }
     for (int k = 0, o = 0; k < 3; o += nb_c[k++]) {  // the pair-scoring stage (timed)
         HIPCHK(c, launch_pairs(c->ds, ipl, d_refs, lds_c[k], k == 2, d_blk + o, nb_c[k], d_ord + o,
-                               W.d_slots.as<int32_t>(), W.d_fl.as<float>(), s));
+                               W.d_slots.as<int32_t>(), W.d_fl.as<float>(), sp));
         J.n_dispatch += nb_c[k] > 0;
     }
     if (pe1) {
-        HIPCHK(c, hipEventRecord(pe1, s));
+        HIPCHK(c, hipEventRecord(pe1, sp));
         ++J.st_launches;
     }
     if (J.stats_count && any_pairs) {
         unsigned long long* acc = J.d_stats.as<unsigned long long>();
-        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)nblk, W.d_slots.as<int32_t>(), acc, s));
+        HIPCHK(c, launch_pair_stats(c->ds, d_blk, (int)nblk, W.d_slots.as<int32_t>(), acc, sp));
         for (const PairGen& g : gens)  // the staged image per pair block (QConst + tables)
             for (int f = 0; f < g.nf; ++f) {
                 const int32_t k = gp2[g.fl + f].x;
@@ -1063,15 +1074,15 @@ int launch_chunk(pf_ctx* c, std::vector<Job>& jobs, std::vector<JP>& P, size_t b
     // (PF_DEBUG collab_main=1: K4' and K8 on the context's stream always, the A/B)
     const hipStream_t s2 = J.aux2;
     static const bool collab_main = debug_long("collab_main", 0) != 0;
-    const hipStream_t sc = (collab_main || !jix_clubs.empty()) ? s : s2;
-    HIPCHK(c, hipEventRecord(W.ev_pairs, s));
+    const hipStream_t sc = (collab_main || !jix_clubs.empty()) ? sp : s2;
+    HIPCHK(c, hipEventRecord(W.ev_pairs, sp));
     HIPCHK(c, hipStreamWaitEvent(s2, W.ev_pairs, 0));
     HIPCHK(c, launch_collab(d_dj, d_jc, (int)jix_collab.size(), max_cap_collab, d_p32, W.d_fl.as<float>(),
                             W.d_slots.as<int32_t>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(), W.d_parts.as<uint64_t>(),
                             d_tk, d_keys, ktop, sc));
     HIPCHK(c, launch_job_topk(d_dj, d_jt, n_topk_main, W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                               W.d_slots.as<int32_t>(), d_ncand, d_keys, ktop, sc));
-    if (collab_main) HIPCHK(c, hipEventRecord(W.ev_main, s));
+    if (collab_main) HIPCHK(c, hipEventRecord(W.ev_main, sp));
     HIPCHK(c, launch_clubs(J.js, J.view, d_dj, d_jk, (int)jix_clubs.size(), d_p32, d_p64, W.d_fl.as<float>(),
                            W.d_acc.as<double>(), W.d_fl.as<float>(), W.d_ids.as<int32_t>(),
                            d_ncand, (int64_t)J.js.n_club_ids, s2));
@@ -1201,6 +1212,7 @@ int finish_pending(pf_ctx* c) {
     if (rc != PF_OK) {
         (void)hipStreamSynchronize(c->stream);
         if (J.aux2) (void)hipStreamSynchronize(J.aux2);
+        if (J.aux) (void)hipStreamSynchronize(J.aux);
     }
     return rc;
 }
@@ -1297,6 +1309,7 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
     auto drain = [&](int code) {  // an error with a chunk in flight: let it finish first
         (void)hipStreamSynchronize(c->stream);
         if (J.aux2) (void)hipStreamSynchronize(J.aux2);
+        if (J.aux) (void)hipStreamSynchronize(J.aux);
         for (auto& w : J.ws) w.active = false;
         if (J.carry.on) {  // its results are dropped; pf_eval_wait reports the error
             J.carry_done = J.carry.ticket;
@@ -1442,6 +1455,7 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
     if (rc != PF_OK) {
         (void)hipStreamSynchronize(c->stream);
         if (J.aux2) (void)hipStreamSynchronize(J.aux2);
+        if (J.aux) (void)hipStreamSynchronize(J.aux);
         J.ws[slot].active = false;
         return rc;
     }
@@ -1485,6 +1499,7 @@ int jobs_stats_read(pf_ctx* c, pf_jobs_stats* o) {
     unsigned long long v[3] = {0, 0, 0};
     if (J.d_stats.p) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (J.aux) HIPCHK(c, hipStreamSynchronize(J.aux));  // the counting kernels of ping-pong chunks
         HIPCHK(c, hipMemcpy(v, J.d_stats.p, sizeof v, hipMemcpyDeviceToHost));
     }
     double ms = 0.0;

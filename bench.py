@@ -941,7 +941,11 @@ def main():
         if not args.no_pmc:
             sel = {}
             if args.workload in ("cfg2", "cfg4"):
-                sel[want_kernel] = lambda v, k=args.steps: v[len(v) - k:] if len(v) >= k else []
+                # the timed launches: the last `steps` before the isolated-launch sample (cfg 2 at N = 1:
+                # min(steps, 20) launches after the timed region)
+                iso = min(args.steps, 20) if (args.workload == "cfg2" and args.queries_per_gpu == 1) else 0
+                sel[want_kernel] = (lambda v, k=args.steps, i=iso: v[len(v) - k - i:len(v) - i]
+                                    if len(v) >= k + i else [])
             if args.workload == "cfg3" or sub3:
                 # every K1' dispatch; the timed stages' ones are picked later by the engines'
                 # dispatch counters (pair_stage_traffic)
@@ -1047,12 +1051,32 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
     # sanity: the merged top-k of the last step rescored by the pair kernel
     last = final.cpu().numpy().view(np.uint64)
     uids, scores = pf.decode_keys(last[0])
     chk = eng.fas_pairs(np.full(len(uids), qstream[warm + steps - 1][0], np.int32), uids)
     consistent = bool(len(uids) == k and np.array_equal(chk.view(np.uint32), scores.view(np.uint32)))
+
+    # One query per step on a caller's stream runs on the engine's two scan lanes (pf_ctx.h
+    # ScanLane): consecutive launches overlap, so a launch's HIP events span its neighbours' tails.
+    # After the timed region, the same queries once more one at a time (synchronised, untimed by
+    # the step clock) give the kernel's isolated launch time beside it.
+    isolated = None
+    if Q == 1 and world == 1:
+        eng.profile_sample(1)
+        eng.profile_reset()
+        n_iso = min(steps, 20)
+        for i in range(warm, warm + n_iso):
+            eng.scan_keys_async(qstream[i], k, final.data_ptr(), sptr)
+            torch.cuda.synchronize()
+        iso_ms, iso_n = eng.profile_read()
+        eng.profile_sample(0)
+        if iso_n:
+            isolated = {"launches": iso_n, "avg_launch_ms": iso_ms / iso_n,
+                        "note": "the first timed queries again, one at a time after the timed region: the "
+                                "kernel's own duration (avg_launch_ms above spans the overlap of consecutive "
+                                "launches on the scan lanes)"}
+
 
     value = Q * n_cand * steps / elapsed
     # bytes per launch by the kernel's access pattern, over the queries timed (this rank's shard)
@@ -1134,6 +1158,12 @@ def main():
                               "postings scan reads only the query's lists, so that effective rate can pass the peak)")},
         "topk_selfcheck": consistent,
     }
+    if isolated is not None:
+        if phys_per_launch:
+            iso_bytes = float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in range(isolated["launches"])]))
+            isolated["achieved_gbs"] = iso_bytes / (isolated["avg_launch_ms"] * 1e-3) / 1e9
+            isolated["frac"] = isolated["achieved_gbs"] / HBM_PEAK_GBS
+        rec["roofline"]["isolated_launch"] = isolated
     if n1 is not None:
         rec["n1_same_workload"] = n1
     if per_rank is not None:

@@ -411,6 +411,33 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
     const size_t total = offs_b + rows_b + sync_b + pool_b;
+    // a single query on a caller's stream goes to the next scan lane (pf_ctx.h ScanLane): its
+    // upload and launch on the lane's stream, its row copied out on the caller's stream
+    pf_ctx::ScanLane* ln = nullptr;
+    static const bool lanes_on = pf::debug_long("scan_lanes", 1) != 0;
+    const hipStream_t caller = s;
+    uint64_t* out_keys = d_keys;
+    int32_t out_row0 = rows[order[0]];
+    if (lanes_on && nq == 1 && s != c->stream) {
+        const int li = c->lane_cur;
+        ln = &c->lane[li];
+        c->lane_cur ^= 1;
+        if (!ln->done) {
+            HIPCHK(c, hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
+            HIPCHK(c, hipEventCreateWithFlags(&ln->freed, hipEventDisableTiming));
+        }
+        // the lanes run on the context's stream and the job pipeline's aux stream (created at open):
+        // streams of their own would share the process's four hardware queues with them
+        // (PF_DEBUG lazy_aux=1: no aux stream yet, both lanes on the context's stream)
+        ln->st = (li == 0 || !c->jb.aux) ? c->stream : c->jb.aux;
+        if (ln->used) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed, 0));  // its last row was copied out
+        HIPCHK(c, ln->keys.ensure((size_t)k * sizeof(uint64_t)));
+        s = ln->st;
+        out_keys = ln->keys.as<uint64_t>();
+        orows[0] = 0;  // the lane's own one-row result
+    }
+    DBuf& pool_buf = ln ? ln->pool : c->d_pool;
+    DBuf& part_buf = ln ? ln->part : c->d_part;
     uint8_t* h = c->stage_acquire(total);
     if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
     std::memcpy(h, offs.data(), (size_t)nq * 4);
@@ -418,11 +445,11 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     std::memset(h + offs_b + rows_b, 0, sync_b);
     for (int i = 0; i < nq; ++i)
         std::memcpy(h + offs_b + rows_b + sync_b + offs[i], imgs[order[i]]->data(), imgs[order[i]]->size());
-    HIPCHK(c, c->d_pool.ensure(total));
-    HIPCHK(c, hipMemcpyAsync(c->d_pool.p, h, total, hipMemcpyHostToDevice, s));
+    HIPCHK(c, pool_buf.ensure(total));
+    HIPCHK(c, hipMemcpyAsync(pool_buf.p, h, total, hipMemcpyHostToDevice, s));
     HIPCHK(c, c->stage_release(s));
-    uint8_t* base = c->d_pool.as<uint8_t>();
-    HIPCHK(c, c->d_part.ensure((size_t)nq * (blocks + 8) * k * sizeof(uint64_t)));  // + 8 group lists (post_tail)
+    uint8_t* base = pool_buf.as<uint8_t>();
+    HIPCHK(c, part_buf.ensure((size_t)nq * (blocks + 8) * k * sizeof(uint64_t)));  // + 8 group lists (post_tail)
     hipEvent_t e0, e1;
     int rc = scan_events(c, timed, e0, e1);
     if (rc != PF_OK) return rc;
@@ -436,19 +463,27 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         if (use_slice())
             HIPCHK(c, pf::launch_slice(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
                                        nq == 1 ? wave_lds : vmax, q1 - q0, (int)cand_begin, (int)cand_end, k, blocks,
-                                       c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
-                                       reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
+                                       part_buf.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
+                                       reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, out_keys,
                                        reinterpret_cast<const int32_t*>(base + offs_b) + q0, slice_mode(),
                                        (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
         else
             HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
                                       nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
-                                      c->d_part.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
-                                      reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, d_keys,
+                                      part_buf.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
+                                      reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, out_keys,
                                       reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
                                       tail_block_cands(), (timed && q0 == 0) ? e0 : nullptr,
                                       (timed && q1 == nq) ? e1 : nullptr, s));
         q0 = q1;
+    }
+    if (ln) {  // the caller's stream: wait for the lane's launch, copy its row out, free the lane
+        HIPCHK(c, hipEventRecord(ln->done, s));
+        HIPCHK(c, hipStreamWaitEvent(caller, ln->done, 0));
+        HIPCHK(c, hipMemcpyAsync(d_keys + (size_t)out_row0 * k, out_keys, (size_t)k * sizeof(uint64_t),
+                                 hipMemcpyDeviceToDevice, caller));
+        HIPCHK(c, hipEventRecord(ln->freed, caller));
+        ln->used = true;
     }
     if (timed) {
         c->last_ev0 = e0;
@@ -774,6 +809,11 @@ void pf_close(pf_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->jb.aux2) (void)hipStreamSynchronize(c->jb.aux2);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    for (auto& ln : c->lane) {  // (their streams are the context's and the aux stream)
+        if (ln.st) (void)hipStreamSynchronize(ln.st);
+        if (ln.done) (void)hipEventDestroy(ln.done);
+        if (ln.freed) (void)hipEventDestroy(ln.freed);
+    }
     for (auto& st : c->stage) {
         if (st.done) (void)hipEventDestroy(st.done);
         if (st.p) (void)hipHostFree(st.p);

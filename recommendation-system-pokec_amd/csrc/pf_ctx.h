@@ -255,6 +255,19 @@ struct pf_ctx {
         }
         return hipEventRecord(st.done, s);
     }
+    // Two scan lanes for single-query calls made on a caller's stream (pf_scan_keys_async): each
+    // lane has its own stream, staging pool, merge parts and result row, so query i + 1's upload
+    // and launch need not wait for query i's launch to end: its workgroups fill the CUs that query
+    // i's last blocks leave idle.  The caller's stream waits for a lane's launch and copies its
+    // row out, in call order; a lane is reused after that copy (ev_freed).
+    struct ScanLane {
+        hipStream_t st = nullptr;
+        DBuf pool, part, keys;
+        hipEvent_t done = nullptr, freed = nullptr;
+        bool used = false;
+    };
+    ScanLane lane[2];
+    int lane_cur = 0;
     // scan-kernel timing pool (pf_profile_*)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
     size_t prof_used = 0;

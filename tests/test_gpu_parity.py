@@ -529,6 +529,29 @@ def test_cpp_facade_explicit_idf_matches_reference():
         assert items == (allg if key in allg else recs)[key], key
 
 
+def test_scan_lanes_match_synchronous_calls(big):
+    """Single-query scans on a caller's stream run on the context's two scan lanes (pf_ctx.h
+    ScanLane), consecutive launches overlapping, each row copied out on the caller's stream in call
+    order: every row equals the synchronous all-candidates call's top-k (ids and score bits)."""
+    import torch
+    c, eng, orc = big
+    pf = tl.product()
+    s = torch.cuda.Stream()
+    qs = [int(x) for x in np.random.default_rng(5).integers(1, 20001, 24)]
+    outs = [torch.empty((1, 10), dtype=torch.int64, device="cuda") for _ in qs]
+    for q, o in zip(qs, outs):
+        eng.scan_keys_async(np.array([q], np.int32), 10, o.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    ref = eng.recommend_interest_all(qs, 10)
+    for q, g, r in zip(qs[:6], ref, orc.interest(qs[:6], 10, tl.PF_MODE_ALL, 0)):
+        assert list(g[0]) == list(r[0]) and np.array_equal(g[1].view(np.uint32), r[1].view(np.uint32)), q
+    for q, o, r in zip(qs, outs, ref):
+        uids, scores = pf.decode_keys(o.cpu().numpy().view(np.uint64)[0])
+        assert list(uids) == list(r[0]), q
+        assert np.array_equal(np.asarray(scores, np.float32).view(np.uint32),
+                              np.asarray(r[1], np.float32).view(np.uint32)), q
+
+
 def test_profile_sampling_counts_and_results(big):
     """pf_profile_sample: with every = 3, launches 0, 3, 6 of nine are timed (positive device
     time), the untimed ones return the same keys as timed ones; every = 1 times all."""

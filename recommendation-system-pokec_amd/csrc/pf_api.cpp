@@ -264,7 +264,11 @@ uint32_t post_mode(int nq) {
     // blocks share the cache lines at their list segments' ends); the query-major batch grid too
     // (a query's workgroups are a multiple of 8 there, so bx mod 8 is still the XCD); k5_xcd=0 A/B
     static const bool xcd = pf::debug_long("k5_xcd", 1) != 0;
-    static const bool dyn = pf::debug_long("k5_dyn", 0) != 0;  // every block claimed per XCD group (A/B)
+    // every block claimed per XCD group (default; k5_dyn=0 A/B: static rounds, the tail claimed).
+    // Neutral on an isolated launch (178.8 vs 179.2 us, r6-era), but with the scan lanes the next
+    // query's workgroups start while this one's last blocks run, so a static share of blocks
+    // waits on workgroups dispatched late: cfg 2 1.13e10 -> 1.20e10 candidates/s (r8b / r8c)
+    static const bool dyn = pf::debug_long("k5_dyn", 1) != 0;
     const uint32_t x = xcd ? 4u : 0u;
     return nq == 1 ? ((st ? 0u : 1u) | x | (dyn ? 8u : 0u)) : (tr ? 2u : x);
 }
@@ -414,22 +418,23 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // a single query on a caller's stream goes to the next scan lane (pf_ctx.h ScanLane): its
     // upload and launch on the lane's stream, its row copied out on the caller's stream
     pf_ctx::ScanLane* ln = nullptr;
-    static const bool lanes_on = pf::debug_long("scan_lanes", 1) != 0;
+    static const int nlanes = (int)std::min(3L, pf::debug_long("scan_lanes", 2));
     const hipStream_t caller = s;
     uint64_t* out_keys = d_keys;
     int32_t out_row0 = rows[order[0]];
-    if (lanes_on && nq == 1 && s != c->stream) {
+    if (nlanes >= 2 && nq == 1 && s != c->stream) {
         const int li = c->lane_cur;
         ln = &c->lane[li];
-        c->lane_cur ^= 1;
+        c->lane_cur = (li + 1) % nlanes;
         if (!ln->done) {
             HIPCHK(c, hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
             HIPCHK(c, hipEventCreateWithFlags(&ln->freed, hipEventDisableTiming));
         }
-        // the lanes run on the context's stream and the job pipeline's aux stream (created at open):
+        // the lanes run on the context's stream and the job pipeline's aux streams (created at open):
         // streams of their own would share the process's four hardware queues with them
-        // (PF_DEBUG lazy_aux=1: no aux stream yet, both lanes on the context's stream)
-        ln->st = (li == 0 || !c->jb.aux) ? c->stream : c->jb.aux;
+        // (PF_DEBUG lazy_aux=1: no aux streams yet, every lane on the context's stream)
+        const hipStream_t ls[3] = {c->stream, c->jb.aux, c->jb.aux2};
+        ln->st = ls[li] ? ls[li] : c->stream;
         if (ln->used) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed, 0));  // its last row was copied out
         HIPCHK(c, ln->keys.ensure((size_t)k * sizeof(uint64_t)));
         s = ln->st;
@@ -809,7 +814,7 @@ void pf_close(pf_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->jb.aux2) (void)hipStreamSynchronize(c->jb.aux2);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
-    for (auto& ln : c->lane) {  // (their streams are the context's and the aux stream)
+    for (auto& ln : c->lane) {  // (their streams are the context's and the aux streams)
         if (ln.st) (void)hipStreamSynchronize(ln.st);
         if (ln.done) (void)hipEventDestroy(ln.done);
         if (ln.freed) (void)hipEventDestroy(ln.freed);

@@ -266,7 +266,7 @@ struct pf_ctx {
         hipEvent_t done = nullptr, freed = nullptr;
         bool used = false;
     };
-    ScanLane lane[2];
+    ScanLane lane[3];  // two by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 3 adds the aux2 stream)
     int lane_cur = 0;
     // scan-kernel timing pool (pf_profile_*)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;

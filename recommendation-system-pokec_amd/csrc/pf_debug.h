@@ -13,8 +13,10 @@
 //   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 16; A/B)
 //   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; A/B)
 //   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
-//   scan_lanes=0          single-query scans on a caller's stream launch on that stream (A/B; default:
-//                         two lanes, so consecutive queries' launches overlap)
+//   scan_lanes=N          single-query scans on a caller's stream: 0 or 1 launch on that stream (A/B);
+//                         default 2 lanes, so consecutive queries' launches overlap; 3 adds a lane
+//   k5_dyn=0              K5: one-query launches in static block rounds, the tail claimed (A/B;
+//                         default: every block claimed per XCD group)
 //   chunk_pingpong=0      the job pipeline's chunks all gather on the aux stream and score on the
 //                         context's stream behind an event (A/B; default: alternate the two)
 //   collab_main=1         the job pipeline's K4' / K8 on the context's stream after the pair kernel

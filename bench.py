@@ -850,7 +850,8 @@ def solo_shards(args, eng, pf, torch, qstream, warm, steps, Q, k, n_cand, stream
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: cfg2 200 single-query steps, ~30 ms; every other workload 50)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--users", type=int, default=N_USERS)
     ap.add_argument("--queries-per-gpu", type=int, default=1)
@@ -911,6 +912,8 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     if args.workload is None:
         args.workload = "cfg2" if world == 1 else "cfg4"
+    if args.steps is None:
+        args.steps = 200 if args.workload == "cfg2" else 50
     if args.contexts is None:
         args.contexts = 1
     if args.workload == "cfg5":
@@ -1040,6 +1043,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(warm, warm + steps):
         step(i)
+    t_submitted = time.perf_counter() - t_start  # the host's enqueue time for the K steps
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -1157,6 +1161,7 @@ def main():
                               "d3_equiv_*: SURVEY D3 record bytes b_c of every candidate over the same time (the "
                               "postings scan reads only the query's lists, so that effective rate can pass the peak)")},
         "topk_selfcheck": consistent,
+        "host_enqueue_ms_per_step": t_submitted * 1e3 / steps,
     }
     if isolated is not None:
         if phys_per_launch:

@@ -418,6 +418,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // a single query on a caller's stream goes to the next scan lane (pf_ctx.h ScanLane): its
     // upload and launch on the lane's stream, its row copied out on the caller's stream
     pf_ctx::ScanLane* ln = nullptr;
+    int lrow = 0;
     static const int nlanes = (int)std::min(3L, pf::debug_long("scan_lanes", 2));
     const hipStream_t caller = s;
     uint64_t* out_keys = d_keys;
@@ -428,22 +429,26 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         c->lane_cur = (li + 1) % nlanes;
         if (!ln->done) {
             HIPCHK(c, hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
-            HIPCHK(c, hipEventCreateWithFlags(&ln->freed, hipEventDisableTiming));
+            for (hipEvent_t& e : ln->freed) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         // the lanes run on the context's stream and the job pipeline's aux streams (created at open):
         // streams of their own would share the process's four hardware queues with them
         // (PF_DEBUG lazy_aux=1: no aux streams yet, every lane on the context's stream)
         const hipStream_t ls[3] = {c->stream, c->jb.aux, c->jb.aux2};
         ln->st = ls[li] ? ls[li] : c->stream;
-        if (ln->used) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed, 0));  // its last row was copied out
-        HIPCHK(c, ln->keys.ensure((size_t)k * sizeof(uint64_t)));
+        lrow = ln->row;
+        ln->row = (lrow + 1) % pf_ctx::kLaneRows;
+        if (ln->used[lrow]) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed[lrow], 0));  // the row was copied out
+        HIPCHK(c, ln->keys.ensure((size_t)pf_ctx::kLaneRows * pf::kMaxTopK * sizeof(uint64_t)));  // once
         s = ln->st;
-        out_keys = ln->keys.as<uint64_t>();
+        out_keys = ln->keys.as<uint64_t>() + (size_t)lrow * pf::kMaxTopK;
         orows[0] = 0;  // the lane's own one-row result
     }
     DBuf& pool_buf = ln ? ln->pool : c->d_pool;
     DBuf& part_buf = ln ? ln->part : c->d_part;
+    pf::HpLap lw;
     uint8_t* h = c->stage_acquire(total);
+    lw.lap(pf::kHpScanStageWait);
     if (!h) return c->fail(PF_ENOMEM, "pinned staging allocation failed");
     std::memcpy(h, offs.data(), (size_t)nq * 4);
     std::memcpy(h + offs_b, orows.data(), (size_t)nq * 4);
@@ -487,8 +492,8 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         HIPCHK(c, hipStreamWaitEvent(caller, ln->done, 0));
         HIPCHK(c, hipMemcpyAsync(d_keys + (size_t)out_row0 * k, out_keys, (size_t)k * sizeof(uint64_t),
                                  hipMemcpyDeviceToDevice, caller));
-        HIPCHK(c, hipEventRecord(ln->freed, caller));
-        ln->used = true;
+        HIPCHK(c, hipEventRecord(ln->freed[lrow], caller));
+        ln->used[lrow] = true;
     }
     if (timed) {
         c->last_ev0 = e0;
@@ -561,6 +566,8 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
              hipStream_t s, bool timed) {
     if (idx.empty()) return PF_OK;
     if (!c->use_post()) return scan_stream(c, idx, rows, k, d_keys, s, timed);
+    pf::HpLap lp;  // PF_DEBUG host_prof=1: image build / staging + launch clocks
+    if (pf::host_prof().on) pf::host_prof().ns[pf::kHpScanCalls] += 1000000000LL;
     // the query images (host, ~35 us each) on threads for a batch
     std::vector<std::vector<uint8_t>> imgs(idx.size());
     std::vector<uint8_t> fits(idx.size(), 1);
@@ -580,7 +587,9 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
         if (fits[q]) { pi.push_back(&imgs[q]); prow.push_back(rows[q]); }
         else { sidx.push_back(idx[q]); srow.push_back(rows[q]); }
     }
+    lp.lap(pf::kHpScanImage);
     int rc = scan_post(c, pi, prow, k, d_keys, s, timed);
+    lp.lap(pf::kHpScanLaunch);
     if (rc != PF_OK) return rc;
     return scan_stream(c, sidx, srow, k, d_keys, s, timed && pi.empty());
 }
@@ -636,7 +645,7 @@ HostProf::HostProf() {
 HostProf::~HostProf() {
     if (!on) return;
     static const char* nm[kHpStages] = {"workspaces", "prep", "layout", "staging", "wait", "decode", "launch-b",
-                                        "launch-a", "finish"};
+                                        "launch-a", "finish", "scan-image", "scan-launch", "scan-calls(n)", "scan-stage-wait"};
     fprintf(stderr, "pokec_fas host stages (s):");
     for (int i = 0; i < kHpStages; ++i) fprintf(stderr, " %s=%.3f", nm[i], (double)ns[i].load() * 1e-9);
     fprintf(stderr, "\n");
@@ -817,7 +826,8 @@ void pf_close(pf_ctx* c) {
     for (auto& ln : c->lane) {  // (their streams are the context's and the aux streams)
         if (ln.st) (void)hipStreamSynchronize(ln.st);
         if (ln.done) (void)hipEventDestroy(ln.done);
-        if (ln.freed) (void)hipEventDestroy(ln.freed);
+        for (hipEvent_t e : ln.freed)
+            if (e) (void)hipEventDestroy(e);
     }
     for (auto& st : c->stage) {
         if (st.done) (void)hipEventDestroy(st.done);

@@ -52,7 +52,8 @@ struct Job {
 // Host-side stage clocks of the batched drivers (PF_DEBUG host_prof=1: summed over the process and
 // printed to stderr at exit; profiling only).
 enum HostStage {
-    kHpPlan = 0, kHpPrep, kHpImages, kHpPack, kHpGpu, kHpUnpack, kHpStage2, kHpCollab, kHpFinish, kHpStages
+    kHpPlan = 0, kHpPrep, kHpImages, kHpPack, kHpGpu, kHpUnpack, kHpStage2, kHpCollab, kHpFinish,
+    kHpScanImage, kHpScanLaunch, kHpScanCalls, kHpScanStageWait, kHpStages  // (the scans' stages: pf_api.cpp scan_all)
 };
 struct HostProf {
     bool on = false;

@@ -256,15 +256,20 @@ struct pf_ctx {
         return hipEventRecord(st.done, s);
     }
     // Two scan lanes for single-query calls made on a caller's stream (pf_scan_keys_async): each
-    // lane has its own stream, staging pool, merge parts and result row, so query i + 1's upload
+    // lane has its own stream, staging pool, merge parts and result rows, so query i + 1's upload
     // and launch need not wait for query i's launch to end: its workgroups fill the CUs that query
     // i's last blocks leave idle.  The caller's stream waits for a lane's launch and copies its
-    // row out, in call order; a lane is reused after that copy (ev_freed).
+    // row out, in call order.  A lane's result rows are used in turn and one is rewritten only
+    // after its copy (freed[r]): with one row per lane, the next launch waited on the copy-out,
+    // a one-workgroup blit queued behind the running launch's workgroups (48-73 us, r8e trace).
+    static constexpr int kLaneRows = 4;
     struct ScanLane {
         hipStream_t st = nullptr;
-        DBuf pool, part, keys;
-        hipEvent_t done = nullptr, freed = nullptr;
-        bool used = false;
+        DBuf pool, part, keys;  // keys: kLaneRows rows of kMaxTopK keys
+        hipEvent_t done = nullptr;
+        hipEvent_t freed[kLaneRows] = {};
+        bool used[kLaneRows] = {};
+        int row = 0;
     };
     ScanLane lane[3];  // two by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 3 adds the aux2 stream)
     int lane_cur = 0;

@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/r8j && mkdir -p $O
+for v in base aux2_prio=1 base aux2_prio=1 aux2_prio=1,lane_upload=0; do
+  E=""; [ $v != base ] && E="$v"
+  timeout -k 10 300 env PF_DEBUG=$E python3 bench.py --steps 200 --warmup 10 --no-pmc --no-cpu-baseline > $O/b.json 2> $O/b.err || exit 2
+  (echo -n "$v "; cat $O/b.json) >> $O/all.txt
+done
+timeout -k 10 300 env PF_DEBUG=aux2_prio=1 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o tr -- python3 bench.py --steps 50 --warmup 5 --no-pmc --no-cpu-baseline > $O/tr.json 2> $O/tr.err || exit 3

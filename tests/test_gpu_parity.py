@@ -602,6 +602,37 @@ def test_sharded_scan_merges_to_single_gpu_result(big):
     eng2.set_shard(0, 1)
 
 
+def test_sharded_single_query_lanes_merge_equals_unsharded(big):
+    """The N > 1 cfg-2 step on one device: one query per call (the scan lanes, every block of a
+    shard's range claimed per XCD group), each shard's keys merged, equal the unsharded scan."""
+    import torch
+    pf = tl.product()
+    c, eng, orc = big
+    q = [3, 8, 1000, 15000, 19999]
+    k = 10
+    ref = eng.recommend_interest_all(q, k)
+    eng2 = tl.engine(c.desc_ptr())
+    s = torch.cuda.Stream()
+    eng2.set_scan_kernel(2)
+    for world in (2, 3, 8):
+        parts = torch.empty((len(q), world, k), dtype=torch.int64, device="cuda")
+        for r in range(world):
+            eng2.set_shard(r, world)
+            for i, u in enumerate(q):
+                eng2.scan_keys_async(np.array([u], np.int32), k, parts[i, r].data_ptr(), s.cuda_stream)
+        out = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
+        for i in range(len(q)):
+            eng2.merge_keys_async(parts[i].data_ptr(), world, 1, k, out[i].data_ptr(), s.cuda_stream)
+        s.synchronize()
+        keys = out.cpu().numpy().view(np.uint64)
+        for i in range(len(q)):
+            uids, scores = pf.decode_keys(keys[i])
+            assert list(uids) == list(ref[i][0]), (world, q[i])
+            assert np.array_equal(scores.view(np.uint32), ref[i][1].view(np.uint32)), (world, q[i])
+    eng2.set_shard(0, 1)
+    eng2.set_scan_kernel(0)
+
+
 @pytest.fixture(scope="module")
 def full():
     """The BASELINE cfg 2 / cfg 3 corpus: 1,632,803 synthetic Pokec-shaped users (seed 1, the

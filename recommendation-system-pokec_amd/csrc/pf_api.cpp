@@ -293,8 +293,9 @@ uint32_t slice_mode() {
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
 // candidates/s.  Round 4 (static block rounds with a claimed tail, the rounds table built once
 // per block): r4t/r4v, one box: 2 -> 1.07e10, 4 -> 1.11e10, 8 -> 1.14e10, 16 -> 1.162e10,
-// 32 -> 1.162e10, 64 -> 1.14e10, 128 -> 1.09e10.
-constexpr int kBatchBlocksPerWgDefault = 16;
+// 32 -> 1.162e10, 64 -> 1.14e10, 128 -> 1.09e10.  Round 5 final tree (r8q, one box, alternating):
+// 8 -> 1.411e10, 16 -> 1.424-1.428e10, 24 -> 1.435e10, 32 -> 1.432-1.438e10.
+constexpr int kBatchBlocksPerWgDefault = 32;
 // PF_DEBUG k5_batch_blocks=N (A/B)
 int batch_blocks_per_wg() {
     static const int n = (int)std::max(1L, pf::debug_long("k5_batch_blocks", kBatchBlocksPerWgDefault));

@@ -10,7 +10,7 @@
 //   k5_block=N            postings-scan block size in candidates (kBlockCands, 512; tests)
 //   k5_transposed=1       batched postings scans on the query-fastest grid (A/B; measured slower)
 //   k5_static=1           one-query postings scans with the static block hand-out (A/B)
-//   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 16; A/B)
+//   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 32; A/B)
 //   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; A/B)
 //   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
 //   scan_lanes=N          single-query scans on a caller's stream: 0 or 1 launch on that stream (A/B);

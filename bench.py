@@ -901,6 +901,10 @@ def main():
                     help="cfg2/cfg4 analysis only (not the workload): every query of every step is the first "
                          "query of the stream, so a batch's lists are all shared (bounds what a query-tiled "
                          "batch could save; the line's config says so)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="cfg2/cfg4 at WORLD_SIZE=1: run the N > 1 step anyway (scan into the local keys, an RCCL "
+                         "all_gather_into_tensor on the scan stream, pf_merge_keys_async), so the communicator, "
+                         "the collective and its stream ordering execute on one GPU (not a scaling run)")
     ap.add_argument("--n1-steps", type=int, default=5,
                     help="N > 1: steps rank 0 times the same workload unsharded on its own GPU (n1_same_workload)")
     args = ap.parse_args()
@@ -946,9 +950,11 @@ def main():
             if args.workload in ("cfg2", "cfg4"):
                 # the timed launches: the last `steps` before the isolated-launch sample (cfg 2 at N = 1:
                 # min(steps, 20) launches after the timed region)
+                # cfg 2 at N = 1: the isolated launches, the ones the line's roofline divides by (the
+                # counter pass serialises dispatches anyway); otherwise the timed launches
                 iso = min(args.steps, 20) if (args.workload == "cfg2" and args.queries_per_gpu == 1) else 0
-                sel[want_kernel] = (lambda v, k=args.steps, i=iso: v[len(v) - k - i:len(v) - i]
-                                    if len(v) >= k + i else [])
+                sel[want_kernel] = ((lambda v, k=args.steps, i=iso: v[len(v) - i:] if len(v) >= k + i else [])
+                                    if iso else (lambda v, k=args.steps: v[len(v) - k:] if len(v) >= k else []))
             if args.workload == "cfg3" or sub3:
                 # every K1' dispatch; the timed stages' ones are picked later by the engines'
                 # dispatch counters (pair_stage_traffic)
@@ -961,7 +967,13 @@ def main():
     import torch
     local = local % max(1, torch.cuda.device_count())  # --dist-backend gloo: ranks may share a GPU
     torch.cuda.set_device(local)
-    dist = Comm(args.dist_backend, local) if world > 1 else None
+    # --force-dist: the collective path at world 1 (before any other GPU work of this process)
+    use_dist = world > 1 or (args.force_dist and args.workload in ("cfg2", "cfg4"))
+    if use_dist and world == 1:
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
+    dist = Comm(args.dist_backend, local) if use_dist else None
     import pokec_fas as pf
 
     t2 = time.time()
@@ -995,11 +1007,11 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     local_keys = torch.empty((Q, k), dtype=torch.int64, device="cuda")
-    gathered = torch.empty((world, Q, k), dtype=torch.int64, device="cuda") if world > 1 else None
+    gathered = torch.empty((world, Q, k), dtype=torch.int64, device="cuda") if use_dist else None
     final = torch.empty((Q, k), dtype=torch.int64, device="cuda")
 
     def step(i):
-        if world == 1:  # the scan's fused merge already yields the final top-k
+        if not use_dist:  # the scan's fused merge already yields the final top-k
             eng.scan_keys_async(qstream[i], k, final.data_ptr(), sptr)
             return
         eng.scan_keys_async(qstream[i], k, local_keys.data_ptr(), sptr)
@@ -1066,7 +1078,7 @@ def main():
     # After the timed region, the same queries once more one at a time (synchronised, untimed by
     # the step clock) give the kernel's isolated launch time beside it.
     isolated = None
-    if Q == 1 and world == 1:
+    if Q == 1 and not use_dist:
         eng.profile_sample(1)
         eng.profile_reset()
         n_iso = min(steps, 20)
@@ -1111,8 +1123,11 @@ def main():
     shard_frac = 1.0 / world
     alg_bytes = lay.alg_bytes * shard_frac * Q
 
+    def rate_ms(b, ms):  # GB/s of b bytes over ms
+        return None if (b is None or not ms) else b / (ms * 1e-3) / 1e9
+
     def rate(b):  # GB/s over the average launch
-        return None if (b is None or not avg_launch_ms) else b / (avg_launch_ms * 1e-3) / 1e9
+        return rate_ms(b, avg_launch_ms)
 
     achieved = rate(phys_per_launch)
     alg_eff = rate(alg_bytes)
@@ -1141,7 +1156,9 @@ def main():
         "config": {"workload": wl_name + (" [ANALYSIS: --same-query, every query the same user]" if args.same_query else ""),
                    "workload_key": workload + ("_samequery" if args.same_query else ""), "n_users": args.users,
                    "queries_per_step": Q, "topk": k,
-                   "parallelism": f"candidate-shard x{world}" + (" + all_gather" if world > 1 else "")},
+                   "parallelism": f"candidate-shard x{world}" + (" + all_gather" if use_dist else ""),
+                   **({"force_dist": "the N > 1 step (local keys, RCCL all-gather, device merge) at world 1: a "
+                                     "code-path check, not a scaling point"} if use_dist and world == 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": None if achieved is None else achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "avg_launch_ms": avg_launch_ms,
@@ -1163,12 +1180,31 @@ def main():
         "topk_selfcheck": consistent,
         "host_enqueue_ms_per_step": t_submitted * 1e3 / steps,
     }
-    if isolated is not None:
-        if phys_per_launch:
-            iso_bytes = float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in range(isolated["launches"])]))
-            isolated["achieved_gbs"] = iso_bytes / (isolated["avg_launch_ms"] * 1e-3) / 1e9
-            isolated["frac"] = isolated["achieved_gbs"] / HBM_PEAK_GBS
-        rec["roofline"]["isolated_launch"] = isolated
+    if isolated is not None and phys_per_launch:
+        # one query per step overlaps consecutive launches on the scan lanes, so the timed launches'
+        # events span their neighbours' tails: the roofline divides the kernel's bytes by its
+        # isolated launch (the same queries again, one at a time) and keeps the overlapped figures
+        # and the per-step rate as named fields beside it
+        iso_bytes = float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in range(isolated["launches"])]))
+        iso_gbs = iso_bytes / (isolated["avg_launch_ms"] * 1e-3) / 1e9
+        R = rec["roofline"]
+        R["overlapped_launch"] = {"avg_launch_ms": avg_launch_ms, "timed_launches": launches,
+                                  "bytes_per_launch": phys_per_launch, "achieved": achieved,
+                                  "frac": None if achieved is None else achieved / HBM_PEAK_GBS,
+                                  "note": "the timed region's launches, each overlapping its neighbours on the "
+                                          "scan lanes (HIP events span the overlap)"}
+        step_gbs = phys_per_launch / (rec["ms_per_step"] * 1e-3) / 1e9
+        R["per_step"] = {"achieved": step_gbs, "frac": step_gbs / HBM_PEAK_GBS,
+                         "note": "bytes per launch / ms_per_step (the steady-state rate of the timed region)"}
+        R.update({"achieved": iso_gbs, "frac": iso_gbs / HBM_PEAK_GBS, "avg_launch_ms": isolated["avg_launch_ms"],
+                  "timed_launches": isolated["launches"], "bytes_per_launch": iso_bytes,
+                  "launch_basis": "isolated (one launch at a time, HIP events on the lane stream)",
+                  "dram_gbs": rate_ms(traffic, isolated["avg_launch_ms"]),
+                  "dram_frac": (None if traffic is None else rate_ms(traffic, isolated["avg_launch_ms"]) / HBM_PEAK_GBS),
+                  "d3_equiv_gbs": rate_ms(alg_bytes, isolated["avg_launch_ms"])})
+        R["d3_equiv_x_peak"] = R["d3_equiv_gbs"] / HBM_PEAK_GBS
+        isolated["achieved_gbs"], isolated["frac"] = iso_gbs, iso_gbs / HBM_PEAK_GBS
+        R["isolated_launch"] = isolated
     if n1 is not None:
         rec["n1_same_workload"] = n1
     if per_rank is not None:

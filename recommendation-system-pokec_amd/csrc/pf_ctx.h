@@ -183,7 +183,8 @@ struct JobsState {
         std::function<void(std::vector<Job>&)> done; // the driver's results from the finished jobs
     } carry;
     uint64_t carry_done = 0;                     // the last carried ticket finished
-    int carry_rc = PF_OK;                        // its status (an error drops the call's results)
+    // carried tickets that failed (an error drops the call's results), until pf_eval_wait reads them
+    std::unordered_map<uint64_t, int> carry_fail;
     // pf_jobs_stats: pair counts / bytes (device counters) and pair-kernel time (HIP events)
     bool stats_on = false;                       // pair-kernel events (pf_jobs_stats_reset bit 0)
     bool stats_count = false;                    // pair counters (bit 1)

@@ -711,8 +711,13 @@ __global__ __launch_bounds__(kJobThreads) void collab_kernel(const DevJob* __res
     const int nb = (J.cap + kCollabCands - 1) / kCollabCands;
     uint64_t* jp = parts + (size_t)blockIdx.y * gridDim.x * k;
     // Hand-off (pf_device.h take_ticket): ONE wave stores its list sc1 and waits for the stores,
-    // its lane 0 takes an acquire-release agent-scope ticket, and the block whose ticket came last
-    // reads every list with sc1 loads in that same wave after the ticket returned.
+    // its lane 0 takes an agent-scope ticket, and the block whose ticket came last reads every list
+    // with sc1 loads in that same wave after the ticket returned.  Under the default
+    // PF_TICKET_MODE 0 the ticket is relaxed with no fence: the hand-off rests on the hardware's
+    // issue order (the stores drained before the ticket issues, the reads data-dependent on its
+    // return) and the sc1 write-through, not on the HIP memory model; a compiler or ISA scheduling
+    // change could break it.  PF_TICKET_MODE 1 (release ticket + acquire fence) is the
+    // model-correct form, built and run by tests/gpu_variant_check.py.
     if (cl < k) st_agent64(jp + (size_t)blockIdx.x * k + cl, list);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __atomic_signal_fence(__ATOMIC_SEQ_CST);

@@ -1230,6 +1230,13 @@ int drain_calls(pf_ctx* c) {
     return rc;
 }
 
+// a carried call's status, kept per ticket (a bounded table: tickets nobody waits for age out)
+static void note_carry_rc(JobsState& J, uint64_t ticket, int rc) {
+    if (rc == PF_OK) return;
+    if (J.carry_fail.size() >= 64) J.carry_fail.clear();
+    J.carry_fail[ticket] = rc;
+}
+
 // The carried driver call: wait for its last chunk, unpack it, hand the jobs to its driver.
 int finish_carry(pf_ctx* c) {
     auto& J = c->jb;
@@ -1239,7 +1246,7 @@ int finish_carry(pf_ctx* c) {
     int rc = finish_chunk(c, cr.jobs, J.ws[cr.slot], nullptr);
     if (rc == PF_OK && cr.done) cr.done(cr.jobs);
     J.carry_done = cr.ticket;
-    J.carry_rc = rc;
+    note_carry_rc(J, cr.ticket, rc);
     return rc;
 }
 
@@ -1313,7 +1320,7 @@ int run_all(pf_ctx* c, std::vector<Job>& jobs, bool raw, std::vector<std::vector
         for (auto& w : J.ws) w.active = false;
         if (J.carry.on) {  // its results are dropped; pf_eval_wait reports the error
             J.carry_done = J.carry.ticket;
-            J.carry_rc = code;
+            note_carry_rc(J, J.carry.ticket, code);
             J.carry = JobsState::Carry{};
         }
         return code;
@@ -1388,8 +1395,13 @@ uint64_t next_call_ticket(pf_ctx* c) { return c->jb.next_ticket++; }
 
 int carry_wait(pf_ctx* c, uint64_t ticket) {
     auto& J = c->jb;
-    if (J.carry.on && J.carry.ticket <= ticket) return finish_carry(c);
-    return J.carry_done >= ticket ? J.carry_rc : PF_OK;
+    if (J.carry.on && J.carry.ticket <= ticket) (void)finish_carry(c);  // its status lands in carry_fail
+    // only this ticket's own status: an earlier call's failure is not reported for a later one
+    const auto it = J.carry_fail.find(ticket);
+    if (it == J.carry_fail.end()) return PF_OK;
+    const int r = it->second;
+    J.carry_fail.erase(it);
+    return r;
 }
 
 // An asynchronous call: planned and launched now into a free workspace slot (the oldest pending
@@ -1405,8 +1417,10 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
     (void)hipSetDevice(c->device);
     for (size_t i = 0; i < jobs.size(); ++i) oc[i] = 0;
     if (jobs.empty() || topk == 0) return PF_OK;
-    if (J.pending.size() >= (size_t)kJobSlots) {
-        const int r = finish_pending(c);
+    // the carried driver call (pf_eval_recommendation_tests_async) holds a workspace slot too: with
+    // every slot taken the oldest pending call is unpacked, or the carried call finished
+    while (J.pending.size() + (J.carry.on ? 1 : 0) >= (size_t)kJobSlots) {
+        const int r = J.pending.empty() ? finish_carry(c) : finish_pending(c);
         if (r != PF_OK) return r;
     }
     int rc = sync_nodes(c);
@@ -1437,9 +1451,9 @@ int run_jobs_async(pf_ctx* c, std::vector<Job>&& jobs, int32_t topk, int32_t* ou
         }
         return PF_OK;
     }
-    int slot = 0;  // a slot no pending call holds
+    int slot = 0;  // a slot neither a pending call nor the carried call holds
     for (bool used = true; used; ++slot) {
-        used = false;
+        used = J.carry.on && J.carry.slot == slot;
         for (const auto& q : J.pending) used |= q.slot == slot;
         if (!used) break;
     }

@@ -1352,7 +1352,9 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const int tail = (mode & 1u) ? blk_begin + max(1, (blk_end - blk_begin) / nbx) * nbx : blk_end;
     const uint32_t B = (uint32_t)ps.bsize;
     const uint32_t cend = min((uint32_t)blk_end * B, (uint32_t)ps.n);  // the range's end
-    const uint32_t tbs = (tail_bs > 0u && tail_bs < B) ? tail_bs : B;
+    // (mode bit 3 counts every block in whole B-candidate blocks: finer tail blocks apply to the
+    // static-rounds mode only)
+    const uint32_t tbs = (tail_bs > 0u && tail_bs < B && !(mode & 8u)) ? tail_bs : B;
     const uint32_t cst = min((uint32_t)tail * B, cend);                 // the claimed part's start
     int blk_last = tail + (int)((cend - cst + tbs - 1) / tbs);
     const bool short_excl = H.n_excl <= kPostThreads;

@@ -478,13 +478,15 @@ class Dataset:
 
 
     class EvalPending:
-        def __init__(self, hits, club, n, ticket):
-            self.hits, self.club, self.n, self.ticket = hits, club, n, ticket
+        # ds: the Dataset the carried call's driver reads when it finishes (at pf_wait or the
+        # engine's next job call), kept alive with the output arrays while the call is in flight
+        def __init__(self, hits, club, n, ticket, ds):
+            self.hits, self.club, self.n, self.ticket, self.ds = hits, club, n, ticket, ds
 
     def eval_recommendation_tests_async(self, eng, sample_size, topk, shard=0, nshards=1, batch=128):
         """pf_eval_recommendation_tests_async: returns at once with the last chunk on the device;
         eval_wait(eng, p) gives eval_recommendation_tests's (hits, club).  The engine keeps the output
-        arrays alive until the call completes."""
+        arrays and this Dataset alive until the call completes."""
         cap = max(int(sample_size), 1)
         hits = np.full((cap, 3), -1, np.int8)
         club = np.full((cap, 2), np.nan)
@@ -494,7 +496,7 @@ class Dataset:
                                                         hits.ctypes.data, club.ctypes.data, cap, ctypes.byref(n),
                                                         ctypes.byref(t))
         eng._check(rc, "pf_eval_recommendation_tests_async")
-        p = Dataset.EvalPending(hits, club, n.value, t.value)
+        p = Dataset.EvalPending(hits, club, n.value, t.value, self)
         eng._inflight[p.ticket] = p
         return p
 

@@ -351,21 +351,47 @@ def test_big_top64_vs_oracle(big, kernel):
                                  {"PF_DEBUG": "scan=postings,k5_block=64"},
                                  {"PF_DEBUG": "scan=postings,k5_block=333"},
                                  {"PF_DEBUG": "scan=postings,k5_static=1,k5_transposed=1"},
-                                 {"PF_DEBUG": "resident_images=0"}],
+                                 {"PF_DEBUG": "resident_images=0"},
+                                 {"PF_DEBUG": "scan=postings,k5_wgs=16"},
+                                 {"PF_DEBUG": "scan=postings,k5_wgs=40"},
+                                 {"PF_LIB_PATH": "variants/ticket1/libpokec_fas.so"}],
                          ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings",
                               "postings-block64", "postings-block333", "postings-static-transposed",
-                              "per-call-images"])
+                              "per-call-images", "postings-16wg-claims", "postings-40wg-claims",
+                              "ticket-mode-1"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
     query of the batch has tables above 1 KiB (the whole launch then probes global);
-    records split over up to 64 lanes (tiles capped at 3 or 1 steps)."""
+    records split over up to 64 lanes (tiles capped at 3 or 1 steps); one-query K5 launches of 16
+    or 40 workgroups, so every workgroup claims several blocks from its XCD group's counter (the
+    20k corpus has 40 blocks); the library built with PF_TICKET_MODE 1 (release tickets and the
+    acquire fence: the memory-model-ordered cross-workgroup hand-off, pf_device.h)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(env)
+    if "PF_LIB_PATH" in env:
+        env["PF_LIB_PATH"] = os.path.join(tl.ROOT, "recommendation-system-pokec_amd", env["PF_LIB_PATH"])
+        assert os.path.exists(env["PF_LIB_PATH"]), "make -C recommendation-system-pokec_amd builds the variant"
     r = subprocess.run([sys.executable, os.path.join(here, "gpu_variant_check.py")], env={**os.environ, **env},
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_rccl_world1_merge():
+    """The multi-GPU step's collective on hardware: init_process_group("nccl") (RCCL) at world size 1,
+    local keys all-gathered on the scan stream and merged by pf_merge_keys_async equal the unsharded
+    scan (tests/gpu_dist_check.py, in its own process so the communicator does not outlive it)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_dist_check.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok: world 1" in r.stdout, r.stdout
 
 
 def test_api_cli_transcript_matches_reference():
@@ -709,6 +735,49 @@ def test_full_size_kernels_agree(full):
             assert np.array_equal(scores.view(np.uint32), post[i][1].view(np.uint32)), (world, kern, q[i])
 
 
+def test_full_size_single_query_lanes(full):
+    """The exact launch bench.py times for cfg 2 (BASELINE configs[1]) at full size: one query per
+    pf_scan_keys_async call on a caller's stream (bench.py `step`), so every launch runs on the scan
+    lanes in post_mode(1) with its 3,189 blocks claimed per XCD group by ~1,024 workgroups, half of
+    them with the bench's HIP events.  The bench's own seeded query stream (seed 2); every row equals
+    the record-stream scan K1 (an independent kernel) on the same queries, ids and score bits, and
+    two rows equal the oracle (the reference algorithm, recommender_graph.cpp:46-52,97-101)."""
+    import torch
+    pf = tl.product()
+    c, eng, oracle = full
+    q = [int(x) for x in np.random.default_rng(2).integers(1, 1632804, size=(24, 1))[:, 0]]
+    k = 10
+    st = torch.cuda.Stream()
+    outs = torch.empty((len(q), k), dtype=torch.int64, device="cuda")
+    eng.set_scan_kernel(2)
+    try:
+        for i, u in enumerate(q):
+            eng.profile_sample(1 if i >= len(q) // 2 else 0)
+            if i == len(q) // 2:
+                eng.profile_reset()
+            eng.scan_keys_async(np.array([u], np.int32), k, outs[i].data_ptr(), st.cuda_stream)
+        st.synchronize()
+        ms, n = eng.profile_read()
+        assert n == len(q) - len(q) // 2 and ms > 0.0, (n, ms)
+    finally:
+        eng.profile_sample(0)
+        eng.set_scan_kernel(0)
+    keys = outs.cpu().numpy().view(np.uint64)
+    eng.set_scan_kernel(1)
+    try:
+        ref = eng.recommend_interest_all(q, k)
+    finally:
+        eng.set_scan_kernel(0)
+    for u, kr, r in zip(q, keys, ref):
+        uids, scores = pf.decode_keys(kr)
+        assert len(uids) == k and list(uids) == list(r[0]), u
+        assert np.array_equal(np.asarray(scores, np.float32).view(np.uint32), r[1].view(np.uint32)), u
+    for u, kr, r in zip(q[:2], keys[:2], oracle().interest(q[:2], k, tl.PF_MODE_ALL, 0)):
+        uids, scores = pf.decode_keys(kr)
+        assert list(uids) == list(r[0]), u
+        assert np.array_equal(np.asarray(scores, np.float32).view(np.uint32), r[1].view(np.uint32)), u
+
+
 def test_full_size_batch_1024(full):
     """BASELINE cfg 4's launch shape at full size: ONE batched postings-scan call of 1,024 seeded
     queries over the 1,632,803-user corpus (the query-major batch grid, LDS-class launches) against
@@ -871,6 +940,18 @@ def test_async_driver_calls_equal_sync():
         p3 = ds.eval_recommendation_tests_async(eng, n, 10, 0, 1, batch)
         eng.recommend_collaborative([1, 2, 3], 10, 1000)  # a synchronous job call completes p3 first
         assert same(ds.eval_wait(eng, p3), ref), (n, batch)
+        # asynchronous recommender calls launched while a driver call is carried take the other
+        # workspace slots (one used to overwrite the carried call's slot)
+        want_c = eng.recommend_collaborative([1, 2, 3], 10, 1000)
+        want_i = eng.recommend_interest([4, 5], 10, pf.PF_MODE_FOF, 1000)
+        p4 = ds.eval_recommendation_tests_async(eng, n, 10, 0, 1, batch)
+        h1 = eng.recommend_collaborative_async([1, 2, 3], 10, 1000)
+        h2 = eng.recommend_interest_async([4, 5], 10, 1000)
+        h3 = eng.recommend_collaborative_async([1, 2, 3], 10, 1000)  # every slot taken: one finishes first
+        assert same(ds.eval_wait(eng, p4), ref), (n, batch)
+        for h, w in ((h1, want_c), (h2, want_i), (h3, want_c)):
+            for x, y in zip(eng.wait(h), w):
+                assert list(x[0]) == list(y[0]) and np.array_equal(x[1].view(np.uint32), y[1].view(np.uint32))
         for nsh in (2, 3):  # shards, each carried in turn
             ps = [ds.eval_recommendation_tests_async(eng, n, 10, s, nsh, batch) for s in range(nsh)]
             parts = [ds.eval_wait(eng, p) for p in ps]

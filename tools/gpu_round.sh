@@ -9,6 +9,7 @@
 #   cfgN         bench.py --workload cfgN               -> cfgN.json
 #   quick        cfg 2, 100 steps, no CPU baseline / PMC -> quick.json
 #   quick4       cfg 4, 3 steps, no CPU baseline / PMC   -> quick4.json
+#   forcedist    cfg 2 through the N > 1 step at world 1 (RCCL communicator + all-gather) -> forcedist.json
 #   quickv:V / quick4v:V  the same with the variant library vlib/V (tools/build_variant.sh)
 #   cfg5c1       cfg 5 at one context with the host stage clocks (PF_DEBUG host_prof=1) -> cfg5c1.err
 #   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> vlib/k5t) per-phase K5 clocks -> k5t.err
@@ -70,6 +71,9 @@ for S in "$@"; do
         # cfg 4 quick line under a PF_DEBUG setting, e.g. quick4e:k5_query_major=1
         E=${S#quick4e:}
         timeout -k 10 300 env PF_DEBUG=$E python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4e_${E//[=,]/_}.json 2> $O/quick4e.err || exit 6 ;;
+    forcedist)
+        # the N > 1 cfg-2 step (local keys, RCCL all-gather on the scan stream, device merge) at world 1
+        timeout -k 10 300 python3 bench.py --force-dist --steps 50 --warmup 5 --no-cfg3 $Q > $O/forcedist.json 2> $O/forcedist.err || exit 12 ;;
     quick4)
         timeout -k 10 300 python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4.json 2> $O/quick4.err || exit 6 ;;
     cfg5c:*)

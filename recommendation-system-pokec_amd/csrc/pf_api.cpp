@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -282,12 +283,6 @@ uint32_t tail_block_cands() {
     return (uint32_t)std::max(0L, n);
 }
 
-// K5s mode word: bit 0 = claimed slices past each wave's first (PF_DEBUG k5s_static=1: static)
-uint32_t slice_mode() {
-    static const bool st = pf::debug_long("k5s_static", 0) != 0;
-    return st ? 0u : 1u;
-}
-
 // Blocks per workgroup of a batched postings scan: a workgroup stages its query's tables once
 // for them (blocks w, w + n/4, ... of one query, so the query's neighbouring blocks still run
 // side by side and share its lists in L2).  cfg 4, r2bs: 1 -> 9.36e9, 2 -> 9.62e9, 4 -> 9.87e9
@@ -302,25 +297,12 @@ int batch_blocks_per_wg() {
     return n;
 }
 
-// The postings-scan kernel: K5s (wave-private slices) when PF_DEBUG k5_slice=1, else K5
-bool use_slice() {
-    static const bool on = pf::debug_long("k5_slice", 0) != 0;
-    return on;
-}
-// dynamic LDS of one image's postings scan, for the kernel in use
+// dynamic LDS of one image's postings scan (K5)
 uint32_t post_image_lds(const pf::QPostHead* h) {
-    const int nl = h->n_tok + h->n_club + h->n_friend;
-    return use_slice() ? pf::slice_lds(h->n_tok, nl) : pf::post_lds(pf::post_var_lds(h->n_tok, nl));
+    return pf::post_lds(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend));
 }
 int post_image_per_cu(const pf::QPostHead* h) {
-    const int nl = h->n_tok + h->n_club + h->n_friend;
-    return use_slice() ? pf::slice_blocks_per_cu(pf::slice_lds(h->n_tok, nl))
-                       : pf::post_blocks_per_cu(pf::post_var_lds(h->n_tok, nl));
-}
-// Slices per wave of a batched K5s launch (PF_DEBUG k5s_batch_slices=N, A/B)
-int batch_slices_per_wave() {
-    static const int n = (int)std::max(1L, pf::debug_long("k5s_batch_slices", 16));
-    return n;
+    return pf::post_blocks_per_cu(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend));
 }
 
 // Workgroups of a one-query postings scan: one resident round (PF_DEBUG k5_wgs=N overrides it, A/B)
@@ -365,6 +347,59 @@ int scan_events(pf_ctx* c, bool& timed, hipEvent_t& e0, hipEvent_t& e1) {
     return PF_OK;
 }
 
+// A single query on a caller's stream runs on the next scan lane (pf_ctx.h ScanLane).  lane_begin
+// picks the lane and its next result row (the lane's stream waits for the copies of a ring group
+// only when it wraps back to it); lane_end has the caller's stream wait for the launch's stop event
+// and copy the row out, and records the group's freed event after its last row's copy.
+struct LaneUse {
+    pf_ctx::ScanLane* ln = nullptr;
+    int row = 0;
+    uint64_t* keys = nullptr;  // the lane's result row
+};
+
+int scan_lanes() {
+    static const int n = (int)std::min(3L, pf::debug_long("scan_lanes", 2));
+    return n;
+}
+
+int lane_begin(pf_ctx* c, hipStream_t caller, LaneUse& u) {
+    u = LaneUse{};
+    const int nlanes = scan_lanes();
+    if (nlanes < 2 || caller == c->stream) return PF_OK;
+    const int li = c->lane_cur;
+    pf_ctx::ScanLane* ln = &c->lane[li];
+    c->lane_cur = (li + 1) % nlanes;
+    if (!ln->done) {
+        HIPCHK(c, hipEventCreate(&ln->done));  // a launch's stop event (bound to its dispatch)
+        for (hipEvent_t& e : ln->freed) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // the lanes run on the context's stream and the job pipeline's aux streams (created at open):
+    // streams of their own would share the process's four hardware queues with them
+    // (PF_DEBUG lazy_aux=1: no aux streams yet, every lane on the context's stream)
+    const hipStream_t ls[3] = {c->stream, c->jb.aux, c->jb.aux2};
+    ln->st = ls[li] ? ls[li] : c->stream;
+    const int r = ln->row;
+    ln->row = (r + 1) % pf_ctx::kLaneRows;
+    const int g = r / pf_ctx::kLaneGroupRows;
+    if (r % pf_ctx::kLaneGroupRows == 0 && ln->used[g]) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed[g], 0));
+    HIPCHK(c, ln->keys.ensure((size_t)pf_ctx::kLaneRows * pf::kMaxTopK * sizeof(uint64_t)));  // once
+    u.ln = ln;
+    u.row = r;
+    u.keys = ln->keys.as<uint64_t>() + (size_t)r * pf::kMaxTopK;
+    return PF_OK;
+}
+
+int lane_end(pf_ctx* c, const LaneUse& u, hipEvent_t stop, hipStream_t caller, uint64_t* dst, int k) {
+    HIPCHK(c, hipStreamWaitEvent(caller, stop, 0));
+    HIPCHK(c, hipMemcpyAsync(dst, u.keys, (size_t)k * sizeof(uint64_t), hipMemcpyDeviceToDevice, caller));
+    if (u.row % pf_ctx::kLaneGroupRows == pf_ctx::kLaneGroupRows - 1) {
+        const int g = u.row / pf_ctx::kLaneGroupRows;
+        HIPCHK(c, hipEventRecord(u.ln->freed[g], caller));
+        u.ln->used[g] = true;
+    }
+    return PF_OK;
+}
+
 // K5: the postings scan of prebuilt images (pf_types.h QPostHead layout) into d_keys rows
 // `rows`.  Staging: [image offsets | rows | sync | images], one async copy.
 int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, const std::vector<int32_t>& rows, int k,
@@ -379,7 +414,7 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     std::vector<int> pcu(nq), order(nq);
     for (int q = 0; q < nq; ++q) {
         const pf::QPostHead* h = reinterpret_cast<const pf::QPostHead*>(imgs[q]->data() + sizeof(pf::QConst));
-        vl[q] = use_slice() ? post_image_lds(h) : pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
+        vl[q] = pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend);
         pcu[q] = post_image_per_cu(h);
         order[q] = q;
     }
@@ -400,49 +435,26 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // cover a few queries at a time and share their lists and cells in L2; with one resident
     // round looping over every query's range instead, 256 queries run at once and L2 hits
     // collapse (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
-    const int64_t cand_begin = std::min<int64_t>((int64_t)c->wb_begin * c->ps.bsize, c->ps.n);
-    const int64_t cand_end = std::min<int64_t>((int64_t)c->wb_end * c->ps.bsize, c->ps.n);
-    const int64_t nslices = (cand_end - cand_begin + pf::slice_cands() - 1) / pf::slice_cands();
-    int blocks;
-    if (use_slice()) {
-        const int64_t waves = (nslices + batch_slices_per_wave() - 1) / batch_slices_per_wave();
-        blocks = nq == 1 ? std::max(1, one_query_wgs(c->num_cus * per_cu))
-                         : (int)std::max<int64_t>(1, (waves + pf::slice_waves() - 1) / pf::slice_waves());
-    } else {
-        blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
-                         : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
-    }
+    const int blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
+                               : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t sync_b = (size_t)nq * sizeof(pf::ScanSync);
     const size_t total = offs_b + rows_b + sync_b + pool_b;
-    // a single query on a caller's stream goes to the next scan lane (pf_ctx.h ScanLane): its
-    // upload and launch on the lane's stream, its row copied out on the caller's stream
-    pf_ctx::ScanLane* ln = nullptr;
-    int lrow = 0;
-    static const int nlanes = (int)std::min(3L, pf::debug_long("scan_lanes", 2));
+    // a single query on a caller's stream goes to the next scan lane: its upload and launch on the
+    // lane's stream, its row copied out on the caller's stream
+    LaneUse lu;
+    if (nq == 1) {
+        const int rc = lane_begin(c, s, lu);
+        if (rc != PF_OK) return rc;
+    }
+    pf_ctx::ScanLane* ln = lu.ln;
     const hipStream_t caller = s;
     uint64_t* out_keys = d_keys;
-    int32_t out_row0 = rows[order[0]];
-    if (nlanes >= 2 && nq == 1 && s != c->stream) {
-        const int li = c->lane_cur;
-        ln = &c->lane[li];
-        c->lane_cur = (li + 1) % nlanes;
-        if (!ln->done) {
-            HIPCHK(c, hipEventCreateWithFlags(&ln->done, hipEventDisableTiming));
-            for (hipEvent_t& e : ln->freed) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        // the lanes run on the context's stream and the job pipeline's aux streams (created at open):
-        // streams of their own would share the process's four hardware queues with them
-        // (PF_DEBUG lazy_aux=1: no aux streams yet, every lane on the context's stream)
-        const hipStream_t ls[3] = {c->stream, c->jb.aux, c->jb.aux2};
-        ln->st = ls[li] ? ls[li] : c->stream;
-        lrow = ln->row;
-        ln->row = (lrow + 1) % pf_ctx::kLaneRows;
-        if (ln->used[lrow]) HIPCHK(c, hipStreamWaitEvent(ln->st, ln->freed[lrow], 0));  // the row was copied out
-        HIPCHK(c, ln->keys.ensure((size_t)pf_ctx::kLaneRows * pf::kMaxTopK * sizeof(uint64_t)));  // once
+    const int32_t out_row0 = rows[order[0]];
+    if (ln) {
         s = ln->st;
-        out_keys = ln->keys.as<uint64_t>() + (size_t)lrow * pf::kMaxTopK;
+        out_keys = lu.keys;
         orows[0] = 0;  // the lane's own one-row result
     }
     DBuf& pool_buf = ln ? ln->pool : c->d_pool;
@@ -471,35 +483,153 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
         int q1 = q0;
         uint32_t vmax = 0;
         while (q1 < nq && pcu[order[q1]] == pcu[order[q0]]) vmax = std::max(vmax, vl[order[q1++]]);
-        if (use_slice())
-            HIPCHK(c, pf::launch_slice(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
-                                       nq == 1 ? wave_lds : vmax, q1 - q0, (int)cand_begin, (int)cand_end, k, blocks,
-                                       part_buf.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
-                                       reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, out_keys,
-                                       reinterpret_cast<const int32_t*>(base + offs_b) + q0, slice_mode(),
-                                       (timed && q0 == 0) ? e0 : nullptr, (timed && q1 == nq) ? e1 : nullptr, s));
-        else
-            HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
-                                      nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
-                                      part_buf.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
-                                      reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, out_keys,
-                                      reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
-                                      tail_block_cands(), (timed && q0 == 0) ? e0 : nullptr,
-                                      (timed && q1 == nq) ? e1 : nullptr, s));
+        HIPCHK(c, pf::launch_post(c->ps, base + offs_b + rows_b + sync_b, reinterpret_cast<const uint32_t*>(base) + q0,
+                                  nq == 1 ? wave_lds : vmax, q1 - q0, c->wb_begin, c->wb_end, k, blocks,
+                                  part_buf.as<uint64_t>() + (size_t)q0 * (blocks + 8) * k,
+                                  reinterpret_cast<pf::ScanSync*>(base + offs_b + rows_b) + q0, out_keys,
+                                  reinterpret_cast<const int32_t*>(base + offs_b) + q0, post_mode(nq),
+                                  tail_block_cands(), (timed && q0 == 0) ? e0 : nullptr,
+                                  (timed && q1 == nq) ? e1 : (ln ? ln->done : nullptr), s));
         q0 = q1;
     }
-    if (ln) {  // the caller's stream: wait for the lane's launch, copy its row out, free the lane
-        HIPCHK(c, hipEventRecord(ln->done, s));
-        HIPCHK(c, hipStreamWaitEvent(caller, ln->done, 0));
-        HIPCHK(c, hipMemcpyAsync(d_keys + (size_t)out_row0 * k, out_keys, (size_t)k * sizeof(uint64_t),
-                                 hipMemcpyDeviceToDevice, caller));
-        HIPCHK(c, hipEventRecord(ln->freed[lrow], caller));
-        ln->used[lrow] = true;
+    if (ln) {  // the caller's stream: wait for the lane's launch (its stop event), copy its row out
+        rc = lane_end(c, lu, (timed ? e1 : ln->done), caller, d_keys + (size_t)out_row0 * k, k);
+        if (rc != PF_OK) return rc;
     }
     if (timed) {
         c->last_ev0 = e0;
         c->last_ev1 = e1;
     }
+    return PF_OK;
+}
+
+// K5 for ONE query from the resident images (pf_ctx.h ResidentPost): no host image build and no
+// upload.  The image part and its QConst (the user's resident K1' image) are already in HBM, the
+// ScanSync is the lane's own (or the context's, on its own stream), zeroed once and left zeroed by
+// every launch (post_tail), and the merge writes the lane's result row.  HIP calls per step on a
+// caller's stream: the launch (its stop event bound to the dispatch), the caller's wait on it and
+// the row copy (+ one event record per ring group of eight rows).
+bool resident_ok(const pf_ctx* c, int32_t i) {
+    const auto& R = c->rp;
+    return R.on && R.var_lds[i] != 0 && !R.stale[i] && pf::post_lds(R.var_lds[i]) <= kK5LdsCap;
+}
+
+int scan_post_resident(pf_ctx* c, int32_t i, int32_t row, int k, uint64_t* d_keys, hipStream_t s, bool timed) {
+    auto& R = c->rp;
+    const uint32_t vl = R.var_lds[i];
+    const int per_cu = pf::post_blocks_per_cu(vl);
+    const int nwb = c->wb_end - c->wb_begin;
+    const int blocks = std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)));
+    LaneUse lu;
+    int rc = lane_begin(c, s, lu);
+    if (rc != PF_OK) return rc;
+    pf_ctx::ScanLane* ln = lu.ln;
+    const hipStream_t ls = ln ? ln->st : s;
+    DBuf& part_buf = ln ? ln->part : c->d_part;
+    DBuf& sync_buf = ln ? ln->sync : R.d_sync;
+    if (!sync_buf.p) {  // once: every launch leaves it zeroed
+        HIPCHK(c, sync_buf.ensure(sizeof(pf::ScanSync)));
+        HIPCHK(c, hipMemsetAsync(sync_buf.p, 0, sizeof(pf::ScanSync), ls));
+    }
+    HIPCHK(c, part_buf.ensure((size_t)(blocks + 8) * k * sizeof(uint64_t)));  // + 8 group lists (post_tail)
+    hipEvent_t e0, e1;
+    rc = scan_events(c, timed, e0, e1);
+    if (rc != PF_OK) return rc;
+    hipEvent_t stop = timed ? e1 : (ln ? ln->done : nullptr);
+    uint64_t* out = ln ? lu.keys : d_keys + (size_t)row * k;
+    const uint8_t* img = R.d_pool.as<uint8_t>() + R.off[i] - sizeof(pf::QConst);
+    const uint8_t* qc = c->jb.d_pimg.as<uint8_t>() + c->jb.pimg_off[i];
+    HIPCHK(c, pf::launch_post(c->ps, img, R.d_zero.as<uint32_t>(), vl, 1, c->wb_begin, c->wb_end, k, blocks,
+                              part_buf.as<uint64_t>(), sync_buf.as<pf::ScanSync>(), out, R.d_zero.as<int32_t>(),
+                              post_mode(1), tail_block_cands(), timed ? e0 : nullptr, stop, ls, qc));
+    if (ln) {
+        rc = lane_end(c, lu, stop, s, d_keys + (size_t)row * k, k);
+        if (rc != PF_OK) return rc;
+    }
+    if (timed) {
+        c->last_ev0 = e0;
+        c->last_ev1 = e1;
+    }
+    return PF_OK;
+}
+
+// Every user's K5 image part (ResidentPost) built once at open: host threads write the parts of a
+// chunk of users into a pinned buffer (build_query_post_part, the per-call builder's own code, so
+// the bytes equal a per-call image's), one async copy per chunk, two buffers in turn.  Needs the
+// job pipeline's resident K1' images (their QConst) and the postings store; when the parts do not
+// fit a third of the free HBM, or PF_DEBUG resident_post=0, every call builds its image as before.
+int build_resident_post(pf_ctx* c) {
+    auto& R = c->rp;
+    R.on = false;
+    const auto& hc = c->hc;
+    const auto& J = c->jb;
+    if (!c->hp.ok || !J.pimg || pf::debug_long("resident_post", 1) == 0 || hc.n == 0) return PF_OK;
+    const int32_t n = hc.n;
+    std::vector<const std::vector<int32_t>*> adj((size_t)n, nullptr);
+    std::vector<int64_t> off((size_t)n + 1, 0);
+    par_jobs((size_t)n, [&](size_t i) {
+        auto it = hc.adj.find(hc.uid[i]);
+        if (it != hc.adj.end()) adj[i] = &it->second;
+        // users without a resident K1' image (outside the device tables' limits) get none either
+        off[i + 1] = J.img_lg[i] ? (int64_t)pf::post_part_bound(hc, (int32_t)i, (adj[i] ? adj[i]->size() : 0) + 1) : 0;
+    }, 1 << 14);
+    off[0] = sizeof(pf::QConst);  // the first image's QConst-sized lead stays inside the pool
+    for (int32_t i = 0; i < n; ++i) off[i + 1] += off[i];
+    const size_t total = (size_t)off[n];
+    size_t freeb = 0, totb = 0;
+    if (hipMemGetInfo(&freeb, &totb) != hipSuccess || total > freeb / 3) return PF_OK;
+    if (R.d_pool.p) (void)hipFree(R.d_pool.p);
+    R.d_pool.p = nullptr;
+    R.d_pool.cap = 0;
+    HIPCHK(c, hipMalloc(&R.d_pool.p, total));
+    R.d_pool.cap = total;
+    R.var_lds.assign((size_t)n, 0);
+    R.stale.assign((size_t)n, 0);
+    constexpr size_t kChunkBytes = (size_t)256 << 20;
+    PinBuf pin[2];
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (auto& e : ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int rc = PF_OK;
+    std::atomic<int> bad{0};
+    int b = 0;
+    for (int32_t i0 = 0; i0 < n && rc == PF_OK; b ^= 1) {
+        int32_t i1 = i0 + 1;
+        while (i1 < n && (size_t)(off[i1 + 1] - off[i0]) <= kChunkBytes) ++i1;
+        const size_t bytes = (size_t)(off[i1] - off[i0]);
+        if (hipEventSynchronize(ev[b]) != hipSuccess || pin[b].ensure(std::max<size_t>(bytes, 16)) != hipSuccess) {
+            rc = c->fail(PF_ENOMEM, "resident postings images: pinned staging failed");
+            break;
+        }
+        uint8_t* h = pin[b].as<uint8_t>();
+        par_jobs((size_t)(i1 - i0), [&](size_t j) {
+            const int32_t i = i0 + (int32_t)j;
+            const size_t cap = (size_t)(off[i + 1] - off[i]);
+            if (cap == 0) return;
+            std::vector<int32_t> ex;
+            if (adj[i]) ex = *adj[i];
+            ex.push_back(hc.uid[i]);
+            uint8_t* dst = h + (off[i] - off[i0]);
+            if (pf::build_query_post_part(hc, c->hp, i, ex, dst, cap) == 0) {
+                bad.fetch_add(1);
+                return;
+            }
+            pf::QPostHead hd;
+            std::memcpy(&hd, dst, sizeof hd);
+            R.var_lds[(size_t)i] = pf::post_var_lds(hd.n_tok, hd.n_tok + hd.n_club + hd.n_friend);
+        }, 256);
+        if (hipMemcpyAsync(R.d_pool.as<uint8_t>() + off[i0], h, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(ev[b], c->stream) != hipSuccess)
+            rc = c->fail(PF_ENODEV, "resident postings images: upload failed");
+        i0 = i1;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess && rc == PF_OK) rc = c->fail(PF_ENODEV, "resident postings images");
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (rc != PF_OK) return rc;
+    if (bad.load()) return c->fail(PF_EINTERNAL, "resident postings image larger than its bound");
+    HIPCHK(c, R.d_zero.ensure(64));
+    HIPCHK(c, hipMemset(R.d_zero.p, 0, 64));
+    R.off.swap(off);
+    R.on = true;
     return PF_OK;
 }
 
@@ -569,6 +699,14 @@ int scan_all(pf_ctx* c, const std::vector<int32_t>& idx, const std::vector<int32
     if (!c->use_post()) return scan_stream(c, idx, rows, k, d_keys, s, timed);
     pf::HpLap lp;  // PF_DEBUG host_prof=1: image build / staging + launch clocks
     if (pf::host_prof().on) pf::host_prof().ns[pf::kHpScanCalls] += 1000000000LL;
+    // one query from the resident images: on the context's stream or a scan lane (another stream
+    // without lanes takes the upload path: the resident ScanSync of the context's stream is not
+    // shared with a stream it is not ordered against)
+    if (idx.size() == 1 && resident_ok(c, idx[0]) && (s == c->stream || scan_lanes() >= 2)) {
+        const int rc = scan_post_resident(c, idx[0], rows[0], k, d_keys, s, timed);
+        lp.lap(pf::kHpScanLaunch);
+        return rc;
+    }
     // the query images (host, ~35 us each) on threads for a batch
     std::vector<std::vector<uint8_t>> imgs(idx.size());
     std::vector<uint8_t> fits(idx.size(), 1);
@@ -812,6 +950,10 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
     rc = pf::jobs_open(c);  // device graph + image-builder tables (the recommenders' pipeline)
     if (rc != PF_OK) return bail(rc);
     stage("job pipeline (graph, image tables)");
+    rc = build_resident_post(c);  // every user's K5 image part (the one-query scans' resident images)
+    if (rc != PF_OK) return bail(rc);
+    stage(c->rp.on ? ("resident postings images, " + std::to_string(c->rp.d_pool.cap >> 20) + " MiB").c_str()
+                   : "resident postings images (off)");
     *out = c;
     return PF_OK;
 }
@@ -1014,7 +1156,13 @@ int pf_fof_candidates(pf_ctx* c, int32_t uid, int32_t limit, int32_t flavour, in
 
 int pf_set_adj(pf_ctx* c, int32_t uid, const int32_t* nbrs, int32_t n) {
     if (!c || (n > 0 && !nbrs)) return PF_EINVAL;
-    return pf::jobs_set_adj(c, uid, nbrs, n);
+    const int rc = pf::jobs_set_adj(c, uid, nbrs, n);
+    // the user's exclusions (adj_list row + self) changed: its resident K5 image is stale for good
+    if (rc == PF_OK && c->rp.on) {
+        const int32_t x = c->hc.idx_of(uid);
+        if (x >= 0) c->rp.stale[(size_t)x] = 1;
+    }
+    return rc;
 }
 
 int pf_set_shard(pf_ctx* c, int32_t shard, int32_t nshards) {

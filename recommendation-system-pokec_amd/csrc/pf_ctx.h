@@ -263,17 +263,35 @@ struct pf_ctx {
     // row out, in call order.  A lane's result rows are used in turn and one is rewritten only
     // after its copy (freed[r]): with one row per lane, the next launch waited on the copy-out,
     // a one-workgroup blit queued behind the running launch's workgroups (48-73 us, r8e trace).
-    static constexpr int kLaneRows = 4;
+    // The ring holds kLaneRows rows in kLaneGroups groups: the lane waits for a group's copies
+    // (freed[g], recorded after the copy of its last row) only when it wraps back to it, so a
+    // step costs no event pair of its own.
+    static constexpr int kLaneRows = 32, kLaneGroups = 4, kLaneGroupRows = kLaneRows / kLaneGroups;
     struct ScanLane {
         hipStream_t st = nullptr;
         DBuf pool, part, keys;  // keys: kLaneRows rows of kMaxTopK keys
-        hipEvent_t done = nullptr;
-        hipEvent_t freed[kLaneRows] = {};
-        bool used[kLaneRows] = {};
+        DBuf sync;              // the resident one-query launches' ScanSync (zeroed once; K5 leaves it zeroed)
+        hipEvent_t done = nullptr;  // the stop event of an untimed launch (bound to the kernel's dispatch)
+        hipEvent_t freed[kLaneGroups] = {};
+        bool used[kLaneGroups] = {};
         int row = 0;
     };
     ScanLane lane[3];  // two by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 3 adds the aux2 stream)
     int lane_cur = 0;
+    // Resident postings-scan images (pf_api.cpp build_resident_post): every user's K5 image part
+    // after its QConst (QPostHead | tokens | columns | set lists | exclusions = adj_list row + self),
+    // built once at open; a one-query scan launches from it with the QConst of the user's resident
+    // K1' image (jb.d_pimg), so the call builds and uploads nothing.  A user whose adj_list row
+    // pf_set_adj changed (its exclusions) takes the per-call image again (stale).
+    struct ResidentPost {
+        bool on = false;
+        DBuf d_pool;
+        std::vector<int64_t> off;        // per idx: byte offset of its part in d_pool
+        std::vector<uint32_t> var_lds;   // per idx: post_var_lds of its image (0: no resident image)
+        std::vector<uint8_t> stale;      // per idx: exclusions changed since open
+        DBuf d_zero;                     // zero words: img_off / out_rows of a one-query launch
+        DBuf d_sync;                     // ScanSync of a one-query launch on the context's own stream
+    } rp;
     // scan-kernel timing pool (pf_profile_*)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
     size_t prof_used = 0;

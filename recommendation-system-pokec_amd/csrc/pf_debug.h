@@ -24,10 +24,11 @@
 //   k5_xcd=0|1            K5: contiguous block ranges per XCD in each static round (default 1; A/B)
 //   k5_tail=N             K5: candidates per claimed block past a one-query launch's static rounds
 //                         (default 0 = whole blocks; A/B)
-//   k5_slice=1            the all-candidates postings scan on K5s, the wave-private slice kernel
+//   k5_slice=1            K5s, the wave-private slice kernel: only in the variant build
+//                         PATCH=tools/k5_exp/k5s_slice.patch tools/build_variant.sh k5s
 //                         (A/B: bit-exact, slower)
-//   k5s_static=1          K5s: static slice hand-out instead of claimed slices (A/B)
-//   k5s_batch_slices=N    K5s: slices per wave of a batched launch (default 16; A/B)
+//   k5s_static=1          K5s (variant build): static slice hand-out instead of claimed slices (A/B)
+//   k5s_batch_slices=N    K5s (variant build): slices per wave of a batched launch (default 16; A/B)
 //   chunk_plan=W1:W2:..   relative chunk sizes of large job-pipeline calls (default 1:1:1; A/B)
 //   load_threads=N        loader threads (default: min(16, hardware threads))
 //   resident_images=0     the job pipeline builds its query images per call (K6) instead of

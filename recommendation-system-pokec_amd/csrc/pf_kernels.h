@@ -38,21 +38,15 @@ int scan_blocks_per_cu(bool packed, bool gtab, uint32_t lds);
 // offsets img_off[] into pool); var_lds = post_var_lds(max n_tok, max lists of an image)
 uint32_t post_var_lds(int n_tok, int n_lists);
 uint32_t post_lds(uint32_t var_lds);
-// tail_bs: a one-query launch's claimed blocks past its static rounds take tail_bs candidates each
+// tail_bs: a one-query launch's claimed blocks past its static rounds take tail_bs candidates each.
+// qconst: nullptr (each image starts with its QConst) or, for a one-query launch from the resident
+// images, the user's QConst elsewhere (its K1' resident image); img = the resident part's start
+// minus sizeof(QConst).  The launch leaves each query's ScanSync zeroed (post_tail).
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
                        const int32_t* out_rows, uint32_t mode, uint32_t tail_bs, hipEvent_t e0, hipEvent_t e1,
-                       hipStream_t s);
+                       hipStream_t s, const uint8_t* qconst = nullptr);
 int post_blocks_per_cu(uint32_t var_lds);
-// K5s wave-private slice scan over candidates [cand_begin, cand_end) (pf_kernels.hip
-// fas_slice_kernel); lds = max slice_lds over the launch's images; grid (blocks, nq)
-uint32_t slice_lds(int n_tok, int n_lists);
-hipError_t launch_slice(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t lds, int nq,
-                        int cand_begin, int cand_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                        const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s);
-int slice_blocks_per_cu(uint32_t lds);
-int slice_cands();
-int slice_waves();
 // plain merge of key lists (cross-shard merge after the all-gather)
 hipError_t launch_merge(const uint64_t* in, int nparts, int64_t part_stride, int64_t query_stride, int nq, int k,
                         uint64_t* out, hipStream_t s);

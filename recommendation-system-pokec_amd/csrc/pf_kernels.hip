@@ -951,6 +951,12 @@ __device__ __forceinline__ void post_tail(uint64_t list, int k, uint64_t* sc, Sc
     const uint64_t fin = merge_lists([&](int w) { return qparts + (size_t)(nbx + w) * k; }, ng, k, sc, lane);
     const int row = out_rows ? out_rows[qy] : qy;
     if (lane < k) out[(size_t)row * k + lane] = fin;
+    // the query's rendezvous left zeroed for the next launch that uses it (a one-query launch from
+    // the resident images reuses its lane's ScanSync with no upload): every workgroup of the query
+    // took its group ticket after its last block claim, and every group its done ticket, so nothing
+    // reads, claims or counts from it any more (plain vector stores; the next launch sees them)
+    uint4* z = reinterpret_cast<uint4*>(sy);
+    for (int i = lane; i < (int)(sizeof(ScanSync) / 16); i += 64) z[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 template <bool PACKED, bool GTAB>
@@ -1274,7 +1280,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
                                                               int32_t blk_end, int32_t k, uint64_t* __restrict__ parts,
                                                               ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
                                                               const int32_t* __restrict__ out_rows, uint32_t mode,
-                                                              uint32_t tail_bs) {
+                                                              uint32_t tail_bs, const uint8_t* __restrict__ qconst) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // mode bit 1 (batches): the grid is transposed, blockIdx.x = the query and blockIdx.y = the block
     // group, so the workgroups resident at once are many queries on the same candidate blocks and
@@ -1284,6 +1290,10 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     const int bx = tr ? (int)blockIdx.y : (int)blockIdx.x;
     const int nbx = tr ? (int)gridDim.y : (int)gridDim.x;
     const uint8_t* img = pool + img_off[qy];
+    // the query's QConst: the image's own prefix, or (qconst given: one-query launches from the
+    // resident images) the job pipeline's resident K1' image of the same user, whose QConst K6
+    // builds from the same tables; the image's own part then starts sizeof(QConst) past img
+    const uint8_t* qcp = qconst ? qconst : img;
     const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
     const QTok* toks = reinterpret_cast<const QTok*>(img + H.tok_off);
     const QCol* cols = reinterpret_cast<const QCol*>(img + H.col_off);
@@ -1317,7 +1327,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     uint8_t* mapc = reinterpret_cast<uint8_t*>(base + kLdsMapC);
     uint64_t* lmk = reinterpret_cast<uint64_t*>(base + kLdsLmk);
     uint64_t* cpre = reinterpret_cast<uint64_t*>(base + kLdsCpre);
-    stage(smem, img, sizeof(QConst));
+    stage(smem, qcp, sizeof(QConst));
     for (int j = tid; j < H.n_act; j += kPostThreads) {
         const QCol c = cols[j];
         scol[j] = c;
@@ -1329,7 +1339,7 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
         cpre[H.n_act] = m;
     }
     for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kPostThreads)
-        ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(img)->n_cols);
+        ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(qcp)->n_cols);
     for (int j = tid; j < H.n_tok; j += kPostThreads) {
         const QTok t = toks[j];
         pt[j] = PTok{t.wq, t.idf};
@@ -1832,499 +1842,6 @@ __global__ __launch_bounds__(kPostThreads, PF_K5_MINB) void fas_post_kernel(Post
     post_tail(best, k, sc, sync, parts, out, out_rows, qy, bx, nbx);
 }
 
-// ---------------------------------------------------------------- K5s: wave-private slice scan
-// The postings scan (A13) with no workgroup barrier between its phases.  Each WAVE owns a slice
-// of kSliceCands consecutive candidates at a time and runs K5's phases on it alone: headers and
-// the slice's sub-range of every list the query names (one memory round trip), exclusions, the
-// clubs / friends counters, the fixed terms, then the text columns in rounds of <= 64 tokens /
-// <= kSliceRcap list entries (walk -> hit masks, hit slots by a wave prefix, place, dense FP64
-// term items, owner sums in ascending column order), FAS and the wave top-k.  LDS accesses of one
-// wave are served in order, so a phase hand-off is a wave_sync (no s_barrier); a wave waiting on
-// its loads leaves the SIMD to the other waves instead of holding a 4-wave block at a barrier
-// (K5: 56 % of wave cycles waiting, ~4 barriers per 512-candidate round).  The workgroup shares
-// only the staged query (QConst, tokens, list descriptors, columns).  Slices: group g = bx mod 8
-// (with round-robin dispatch, one XCD) owns a contiguous eighth of the candidate range, so the
-// slices in flight on one L2 are neighbours and share their lists' cache lines; each wave takes
-// its first slice statically and claims the next one from its group's counter one slice ahead.
-// Arithmetic and summation order are K5's (recommender_similarity.cpp:38-123, recommender.cpp:
-// 74-128): bit-identical scores.
-#ifndef PF_K5S_RCAP
-#define PF_K5S_RCAP 8
-#endif
-#ifndef PF_K5S_MINB
-#define PF_K5S_MINB 3  // waves per SIMD the register budget is sized for (LDS holds 3 workgroups of 4)
-#endif
-constexpr int kSliceCpl = 2;                             // candidates per lane
-constexpr int kSliceCands = kSliceCpl * kWave;           // candidates of a slice
-constexpr int kSliceRcap = PF_K5S_RCAP * kWave;          // list entries (= hit slots) of a round
-constexpr int kSliceU = kSliceRcap / kWave;
-constexpr int kSliceWaves = 4;
-constexpr int kSliceThreads = kSliceWaves * kWave;
-constexpr int kSMapWords = kSliceRcap / 64;
-static_assert(kSliceRcap >= kSliceCands, "a one-token round's hits fit the slots");
-static_assert(kSliceCands <= 1024, "walk keys pack the candidate in 10 bits");
-static_assert(kSliceCands * 4 + kSliceCands / 8 <= 8 * kSliceRcap, "set counters alias the slots");
-static_assert(kSliceWaves * kMaxTopK * 8 + 16 <= 8 * kSliceCands + 8 * kSliceRcap, "post_tail scratch in wave 0's masks + slots");
-
-// per-wave LDS
-constexpr uint32_t kWsMask = 0;                                      // u64 [S] hit masks
-constexpr uint32_t kWsSlot = kWsMask + 8 * kSliceCands;              // f64 [Rcap] norm / product -> term
-constexpr uint32_t kWsCnt = kWsSlot;                                 // u32 [S] set counters (read before any slot write)
-constexpr uint32_t kWsExb = kWsCnt + 4 * kSliceCands;                // u32 [S / 32] excluded
-constexpr uint32_t kWsHit = kWsSlot + 8 * kSliceRcap;                // u16 [Rcap] hits
-constexpr uint32_t kWsItem = kWsHit + 2 * kSliceRcap;                // u16 [Rcap] term items
-constexpr uint32_t kWsHbase = kWsItem + 2 * kSliceRcap;              // u16 [S] first slot
-constexpr uint32_t kWsSeg = (kWsHbase + 2 * kSliceCands + 15) & ~15u;  // u32 [64] token segments
-constexpr uint32_t kWsMapN = kWsSeg + 4 * kRoundToks;                // uint2 [64] list map
-constexpr uint32_t kWsMapB = kWsMapN + 8 * kRoundToks;               // u64 [kSMapWords]
-constexpr uint32_t kWsMapC = kWsMapB + 8 * kSMapWords;               // u8 [kSMapWords]
-constexpr uint32_t kWsFixed = (kWsMapC + kSMapWords + 15) & ~15u;    // then rng uint2 [nl], gpre u32 [n_tok + 1], spre u32 [nsets + 1]
-// shared LDS after QConst
-constexpr uint32_t kSsCols = 0;                                      // QCol [48]
-constexpr uint32_t kSsColj = kSsCols + 16 * kPostMaxCols;            // u32 [48] token range per column number
-constexpr uint32_t kSsCpre = kSsColj + 4 * kPostMaxCols;             // u64 [49] active-column prefix masks
-constexpr uint32_t kSsFtab = kSsCpre + 8 * (kPostMaxCols + 1);       // f64 [56] F by used
-constexpr uint32_t kSsFixed = (kSsFtab + 8 * (kNumFixed + kPostMaxCols + 1) + 15) & ~15u;  // then PTok [n_tok], PList [nl], colof u8 [n_tok]
-
-__host__ __device__ inline uint32_t slice_shared_var(int n_tok, int nl) {
-    return (16u * (uint32_t)n_tok + 16u * (uint32_t)nl + (uint32_t)n_tok + 15u) & ~15u;
-}
-__host__ __device__ inline uint32_t slice_wave_bytes(int n_tok, int nl) {
-    return (kWsFixed + 8u * (uint32_t)nl + 4u * (uint32_t)(nl + 2) + 15u) & ~15u;
-}
-
-__global__ __launch_bounds__(kSliceThreads, PF_K5S_MINB) void fas_slice_kernel(
-    PostStore ps, const uint8_t* __restrict__ pool, const uint32_t* __restrict__ img_off, int32_t cand_begin,
-    int32_t cand_end, int32_t k, uint64_t* __restrict__ parts, ScanSync* __restrict__ sync, uint64_t* __restrict__ out,
-    const int32_t* __restrict__ out_rows, uint32_t mode) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int qy = (int)blockIdx.y, bx = (int)blockIdx.x, nbx = (int)gridDim.x;
-    const uint8_t* img = pool + img_off[qy];
-    const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));
-    const QTok* toks = reinterpret_cast<const QTok*>(img + H.tok_off);
-    const QCol* cols = reinterpret_cast<const QCol*>(img + H.col_off);
-    const PList* sets = reinterpret_cast<const PList*>(img + H.set_off);
-    const uint32_t* excl = reinterpret_cast<const uint32_t*>(img + H.excl_off);
-    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nsets = H.n_club + H.n_friend, nl = H.n_tok + nsets;
-    char* sh = smem + sizeof(QConst);
-    QCol* scol = reinterpret_cast<QCol*>(sh + kSsCols);
-    uint32_t* colj = reinterpret_cast<uint32_t*>(sh + kSsColj);
-    uint64_t* cpre = reinterpret_cast<uint64_t*>(sh + kSsCpre);
-    double* ftab = reinterpret_cast<double*>(sh + kSsFtab);
-    PTok* pt = reinterpret_cast<PTok*>(sh + kSsFixed);
-    PList* pl = reinterpret_cast<PList*>(pt + H.n_tok);
-    uint8_t* colof = reinterpret_cast<uint8_t*>(pl + nl);
-    char* wbase0 = sh + kSsFixed + slice_shared_var(H.n_tok, nl);
-    char* wb = wbase0 + (size_t)wave * slice_wave_bytes(H.n_tok, nl);
-    stage(smem, img, sizeof(QConst));
-    for (int j = tid; j < H.n_act; j += kSliceThreads) {
-        const QCol c = cols[j];
-        scol[j] = c;
-        colj[c.t] = (uint32_t)c.j0 | (uint32_t)c.j1 << 16;
-        for (int x = c.j0; x < c.j1; ++x) colof[x] = (uint8_t)j;
-    }
-    if (tid == 0) {
-        uint64_t m = 0;
-        for (int j = 0; j < H.n_act; ++j) { cpre[j] = m; m |= 1ull << cols[j].t; }
-        cpre[H.n_act] = m;
-    }
-    for (int j = tid; j <= kNumFixed + kPostMaxCols; j += kSliceThreads)
-        ftab[j] = (double)j / (double)(kNumFixed + reinterpret_cast<const QConst*>(img)->n_cols);
-    for (int j = tid; j < H.n_tok; j += kSliceThreads) {
-        const QTok t = toks[j];
-        pt[j] = PTok{t.wq, t.idf};
-        pl[j] = t.l;
-    }
-    for (int j = tid; j < nsets; j += kSliceThreads) pl[H.n_tok + j] = sets[j];
-    __syncthreads();
-    const QConst& q = *reinterpret_cast<const QConst*>(smem);
-    uint64_t* mask = reinterpret_cast<uint64_t*>(wb + kWsMask);
-    double* slot = reinterpret_cast<double*>(wb + kWsSlot);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(wb + kWsCnt);
-    uint32_t* exb = reinterpret_cast<uint32_t*>(wb + kWsExb);
-    uint16_t* hit = reinterpret_cast<uint16_t*>(wb + kWsHit);
-    uint16_t* item = reinterpret_cast<uint16_t*>(wb + kWsItem);
-    uint16_t* hbase = reinterpret_cast<uint16_t*>(wb + kWsHbase);
-    uint32_t* seg = reinterpret_cast<uint32_t*>(wb + kWsSeg);
-    uint2* mapn = reinterpret_cast<uint2*>(wb + kWsMapN);
-    uint64_t* mapb = reinterpret_cast<uint64_t*>(wb + kWsMapB);
-    uint8_t* mapc = reinterpret_cast<uint8_t*>(wb + kWsMapC);
-    uint2* rng = reinterpret_cast<uint2*>(wb + kWsFixed);
-    uint32_t* gpre = reinterpret_cast<uint32_t*>(rng + nl);  // token lists' prefix [n_tok + 1]
-    uint32_t* spre = gpre + H.n_tok + 1;                      // set lists' prefix [nsets + 1]
-
-    // the query's slices: group g takes a contiguous range, its waves take slices statically
-    // first, then (mode bit 0) claim the next from the group's counter one slice ahead
-    const uint32_t cb = (uint32_t)cand_begin, ce = (uint32_t)cand_end;
-    const uint32_t ns = ce > cb ? (ce - cb + kSliceCands - 1) / kSliceCands : 0u;
-    const int ng = min(8, nbx), g = bx % ng;
-    const uint32_t s_lo = (uint32_t)((uint64_t)ns * g / ng), s_hi = (uint32_t)((uint64_t)ns * (g + 1) / ng);
-    const uint32_t nw_g = (uint32_t)((nbx - g + ng - 1) / ng) * kSliceWaves;
-    const uint32_t lw = (uint32_t)(bx / ng) * kSliceWaves + (uint32_t)wave;
-    unsigned int* ctr = &sync[qy].xcd_next[g * 16];
-    const bool dyn = (mode & 1u) != 0u;
-    uint64_t best = ~0ull;
-    uint32_t excur = 0;  // the exclusion cursor: the wave's slices ascend
-#ifdef PF_K5_TIMERS
-    uint64_t tacc[14] = {0};
-    uint64_t tprev = clock64();
-    const uint64_t tstart = tprev;
-#endif
-    for (uint32_t s = s_lo + lw; s < s_hi;) {
-        uint32_t claim = 0;
-        if (dyn && lane == 0) claim = atomicAdd(ctr, 1u);
-        const uint32_t c0 = cb + s * kSliceCands;
-        const uint32_t cl = min(c0 + kSliceCands, ce) - 1;  // last candidate of the slice
-        const uint32_t nS = cl - c0 + 1;
-        // 1. headers, every list's sub-range and the exclusion window: one memory round trip
-        uint4 ha[kSliceCpl], hb[kSliceCpl];
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) {
-            const uint32_t c = min(c0 + kk * kWave + lane, cl);
-            ha[kk] = ps.hdr[2 * (size_t)c];
-            hb[kk] = ps.hdr[2 * (size_t)c + 1];
-        }
-        for (int j = lane; j < nl; j += kWave) rng[j] = list_range(ps, pl[j], c0, cl);
-        const uint32_t nex = (uint32_t)H.n_excl;
-        uint32_t ex = excur + (uint32_t)lane < nex ? excl[excur + lane] : ~0u;
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) {
-            const int p = kk * kWave + lane;
-            if ((uint32_t)p >= nS) {
-                ha[kk] = make_uint4(0, 0, 0, 0);
-                hb[kk] = make_uint4(0, 0, 0, 0);
-            }
-            cnt[p] = 0u;
-            mask[p] = 0ull;
-        }
-        if (lane < kSliceCands / 32) exb[lane] = 0u;
-        K5T(0);
-        wave_sync();
-        wave_prefix(gpre, rng, H.n_tok, lane);
-        wave_prefix(spre, rng + H.n_tok, nsets, lane);
-        // 2. exclusions (sorted idx of adj[q] + {q}) from the cursor (the wave's slices ascend)
-        for (uint32_t b0 = excur;;) {
-            const uint32_t p = ex - c0;
-            if (p < nS) atomicOr(&exb[p >> 5], 1u << (p & 31u));
-            excur = b0 + (uint32_t)__popcll(__ballot(ex < c0));
-            if (__popcll(__ballot(ex <= cl)) < kWave) break;
-            b0 += kWave;
-            ex = b0 + (uint32_t)lane < nex ? excl[b0 + lane] : ~0u;
-        }
-        K5T(1);
-        wave_sync();
-        // the text rounds: plan (greedy whole columns, <= 64 tokens / kSliceRcap entries), list
-        // map and token segments; then every entry of the round in flight at once
-        int ci = 0, jcur = 0;
-        Round R{0, 0, 0, 0};
-        uint32_t g0 = 0, F = 0;
-        int js[kSliceU];
-        uint32_t ent[kSliceU];
-        double kn[kSliceU];
-        auto plan = [&]() {
-            R = next_round<kSliceRcap>(scol, gpre, H.n_act, ci, jcur);
-            g0 = gpre[R.ja];
-            F = gpre[R.jb] - g0;
-            if (F > 0) {
-                build_map<kSliceRcap>(mapb, mapc, mapn, gpre, rng, R.ja, R.jb, lane);
-                if (lane < R.jb - R.ja) {
-                    const int j = R.ja + lane;
-                    const QCol c = scol[colof[j]];
-                    const int lo = max(c.j0, R.ja) - R.ja, hi = min(c.j1, R.jb) - R.ja;
-                    seg[lane] = (uint32_t)lo | (uint32_t)hi << 8 | (uint32_t)c.t << 16 |
-                                ((c.j0 < R.ja || c.j1 > R.jb) ? kSegSplit : 0u);
-                }
-                wave_sync();
-            }
-        };
-        auto issue = [&]() {
-            uint32_t xs[kSliceU];
-#pragma unroll
-            for (int u = 0; u < kSliceU; ++u) {
-                const uint32_t f = (uint32_t)(lane + kWave * u);
-                js[u] = -1;
-                xs[u] = 0u;
-                if (f < F) {
-                    const uint32_t w = f >> 6;
-                    const uint32_t kx = (uint32_t)mapc[w] + (uint32_t)__popcll(mapb[w] & low_bits((f & 63u) + 1u)) - 1u;
-                    const uint2 L = mapn[kx];
-                    js[u] = R.ja + (int)L.y;
-                    xs[u] = L.x + f;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kSliceU; ++u) {
-                ent[u] = js[u] >= 0 ? ps.post[K5CHK(xs[u], ps.n_tok_entries, 4)] : 0u;
-                kn[u] = js[u] >= 0 ? ps.pnorm[K5CHK(xs[u], ps.n_tok_entries, 5)] : 0.0;
-            }
-        };
-        const bool any_round = H.n_act > 0;
-        if (any_round) {
-            plan();
-            if (F > 0) issue();
-        }
-        K5T(2);
-        // 3. clubs / friends (their loads in flight beside the first round's)
-        {
-            const uint32_t tot = spre[nsets];
-            for (uint32_t f0 = 0; f0 < tot; f0 += 2 * kWave) {
-                int sj[2];
-                uint32_t se[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const uint32_t f = f0 + (uint32_t)lane + kWave * u;
-                    sj[u] = -1;
-                    uint32_t x = 0;
-                    if (f < tot) {
-                        sj[u] = set_list(spre, nsets, f);
-                        x = rng[H.n_tok + sj[u]].x + (f - spre[sj[u]]);
-                    }
-                    se[u] = sj[u] >= 0 ? ps.post[K5CHK(x, ps.n_post, 10)] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const uint32_t p = (se[u] >> 8) - c0;
-                    if (sj[u] >= 0 && p < nS) atomicAdd(&cnt[p], (se[u] & 0xFFu) << (sj[u] < H.n_club ? 0 : 16));
-                }
-            }
-        }
-        wave_sync();
-        K5T(3);
-        // 4. fixed terms, recommender_similarity.cpp:38-91
-        double sum[kSliceCpl];
-        uint32_t used = 0;  // byte kk: terms used by candidate kk
-        uint64_t pend[kSliceCpl];
-        uint32_t skip = 0;  // bit kk: candidate kk absent or excluded
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) {
-            const int p = kk * kWave + lane;
-            const uint32_t ct = cnt[p];
-            if ((uint32_t)p >= nS || ((exb[p >> 5] >> (p & 31)) & 1u)) skip |= 1u << kk;
-            const uint64_t cm = (uint64_t)ha[kk].x | ((uint64_t)(ha[kk].y & 0xFFFFu) << 32);
-            pend[kk] = cm & q.colmask;
-            double sm = 0.0;
-            int u = 0;
-            const uint32_t pbc = (ha[kk].y >> 16) & 0xFFu, gbc = ha[kk].y >> 24;
-            if (q.pubcode != kCodeMissing && pbc != kCodeMissing) { sm += q.sig_pub[pbc == q.pubcode]; ++u; }
-            if (q.gencode != kCodeMissing && gbc != kCodeMissing) { sm += q.sig_gen[gbc == q.gencode]; ++u; }
-            const int cbv = (int)(int16_t)(ha[kk].z & 0xFFFFu), abv = (int)(int16_t)(ha[kk].z >> 16);
-            if (q.comp > 0 && cbv > 0) { sm += cbv <= kValTab ? q.sig_comp[cbv] : ratio_term(q, PF_F_COMPLETION, q.comp, cbv); ++u; }
-            if (q.age > 0 && abv > 0) { sm += abv <= kValTab ? q.sig_age[abv] : ratio_term(q, PF_F_AGE, q.age, abv); ++u; }
-            const int r0 = (int)hb[kk].x, r1 = (int)hb[kk].y, r2 = (int)hb[kk].z;
-            const int bcnt = (r0 >= 0) + (r1 >= 0) + (r2 >= 0);
-            if (q.a_regcnt > 0 && bcnt > 0) {
-                const int m = (r0 >= 0 && r0 == q.reg[0]) + (r1 >= 0 && r1 == q.reg[1]) + (r2 >= 0 && r2 == q.reg[2]);
-                sm += q.sig_reg[bcnt][m];
-                ++u;
-            }
-            const uint32_t nc = ha[kk].w & 0xFFFFu, nf = ha[kk].w >> 16;
-            const int ic = (int)(ct & 0xFFFFu), ifr = (int)(ct >> 16);
-            if (q.n_clubs > 0 && nc > 0) { sm += ic == 0 ? q.sig0_clubs : set_term(q, PF_F_CLUBS, ic, (int)nc, q.sqrt_clubs); ++u; }
-            if (q.n_friends > 0 && nf > 0) { sm += ifr == 0 ? q.sig0_friends : set_term(q, PF_F_FRIENDS, ifr, (int)nf, q.sqrt_friends); ++u; }
-            sum[kk] = sm;
-            used |= (uint32_t)(u + __popcll(pend[kk])) << (8 * kk);
-        }
-        wave_sync();  // the rounds' slots overwrite the set counters
-        K5T(4);
-        // 5. text columns in rounds (ascending tokens = ascending columns, then tids)
-        double cdot[kSliceCpl], cnrm[kSliceCpl];  // a split column's dot / norm so far
-        uint32_t chit = 0;                        // bit kk: the split column has a hit
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) { cdot[kk] = 0.0; cnrm[kk] = 0.0; }
-        for (bool first_round = true; any_round; first_round = false) {
-            if (!first_round) {
-                if (ci >= H.n_act) break;
-                plan();
-                if (F > 0) issue();
-            }
-            const int ja = R.ja, jb = R.jb;
-            K5T(5);
-            if (F > 0) {
-                // a. walk: one hit-mask bit per hit
-                uint32_t kp[kSliceU];  // p | token << 10 | tf << 16, or ~0
-#pragma unroll
-                for (int u = 0; u < kSliceU; ++u) {
-                    const uint32_t p = (ent[u] >> 8) - c0;
-                    kp[u] = ~0u;
-                    if (js[u] >= 0 && p < nS) {
-                        const uint32_t jr = (uint32_t)(js[u] - ja);
-                        kp[u] = p | jr << 10 | (ent[u] & 0xFFu) << 16;
-                        atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << jr);
-                    }
-                }
-                for (uint32_t f = (uint32_t)lane + kSliceRcap; f < F; f += kWave) {  // one-token rounds past the cap
-                    const int j = round_list(gpre, ja, jb, g0 + f);
-                    const uint32_t p = (ps.post[K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 6)] >> 8) - c0;
-                    if (p < nS) atomicOr(reinterpret_cast<unsigned long long*>(&mask[p]), 1ull << (j - ja));
-                }
-                wave_sync();
-                K5T(6);
-                // b. hit slots: the candidates' hits in one contiguous range per lane
-                uint32_t nk[kSliceCpl], tot = 0;
-#pragma unroll
-                for (int kk = 0; kk < kSliceCpl; ++kk) {
-                    nk[kk] = (uint32_t)__popcll(mask[kk * kWave + lane]);
-                    tot += nk[kk];
-                }
-                uint32_t incl = tot;
-                incl = wave_incl_scan(incl);
-                const uint32_t wn = wave_last(incl);
-                {
-                    uint32_t h0 = incl - tot;
-#pragma unroll
-                    for (int kk = 0; kk < kSliceCpl; ++kk) {
-                        hbase[kk * kWave + lane] = (uint16_t)h0;
-                        h0 += nk[kk];
-                    }
-                }
-                wave_sync();
-                K5T(7);
-                // c. place every hit at its slot, the column's first hit with its norm
-#pragma unroll
-                for (int u = 0; u < kSliceU; ++u) {
-                    if (kp[u] == ~0u) continue;
-                    const uint32_t p = kp[u] & 1023u, jr = (kp[u] >> 10) & 63u, tf = kp[u] >> 16;
-                    const uint64_t below = mask[p] & low_bits(jr);
-                    const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kSliceRcap, 8);
-                    const bool first = (below >> (seg[jr] & 0xFFu)) == 0ull;
-                    hit[r] = (uint16_t)(tf | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
-                    slot[r] = first ? kn[u] : tok_product(pt, ja + (int)jr, tf);
-                }
-                for (uint32_t f = (uint32_t)lane + kSliceRcap; f < F; f += kWave) {
-                    const int j = round_list(gpre, ja, jb, g0 + f);
-                    const uint32_t x = K5CHK(rng[j].x + (g0 + f - gpre[j]), ps.n_tok_entries, 7);
-                    const uint32_t e = ps.post[x];
-                    const uint32_t p = (e >> 8) - c0;
-                    if (p >= nS) continue;
-                    const uint32_t jr = (uint32_t)(j - ja);
-                    const uint64_t below = mask[p] & low_bits(jr);
-                    const uint32_t r = K5CHK(hbase[p] + (uint32_t)__popcll(below), (uint32_t)kSliceRcap, 9);
-                    const uint32_t sg = seg[jr];
-                    const bool first = (below >> (sg & 0xFFu)) == 0ull;
-                    hit[r] = (uint16_t)((e & 0xFFu) | jr << 8 | (first ? kHitFirst : 0u) | (below == 0ull ? kHitCand : 0u));
-                    slot[r] = first ? ps.pnorm[x] : tok_product(pt, ja + (int)jr, e & 0xFFu);
-                    if (first) item[r] = (uint16_t)hit_run(mask[p], sg & 0xFFu, (sg >> 8) & 0xFFu);
-                }
-                wave_sync();
-                K5T(8);
-                // d. terms: one (candidate, column) item per lane over the compacted first hits
-                uint32_t ni = 0;
-                for (uint32_t r0 = 0; r0 < wn; r0 += kWave) {
-                    const uint32_t r = r0 + (uint32_t)lane;
-                    bool is = false;
-                    if (r < wn) {
-                        const uint32_t h = hit[r];
-                        is = (h & kHitFirst) && !(seg[(h >> 8) & 63u] & kSegSplit);
-                    }
-                    const uint64_t bal = __ballot(is);
-                    if (is) item[ni + (uint32_t)__popcll(bal & low_bits((uint32_t)lane))] = (uint16_t)r;
-                    ni += (uint32_t)__popcll(bal);
-                }
-                wave_sync();
-                K5T(9);
-                for (uint32_t i = (uint32_t)lane; i < ni; i += kWave) {
-                    const uint32_t r = item[i];
-                    const uint32_t h = hit[r];
-                    const uint32_t jr = (h >> 8) & 63u, sg = seg[jr];
-                    const uint32_t hi = (sg >> 8) & 0xFFu;
-                    const int t = (int)((sg >> 16) & 0xFFu);
-                    double dot = tok_product(pt, ja + (int)jr, h & 0xFFu);
-                    for (uint32_t r2 = r + 1; r2 < wn; ++r2) {  // the column's further hits, tid ascending
-                        const uint32_t h2 = hit[r2];
-                        const uint32_t j2 = (h2 >> 8) & 63u;
-                        if ((h2 & kHitCand) || j2 >= hi) break;
-                        dot += slot[r2];
-                    }
-                    slot[r] = dot == 0.0 ? q.sig0_col[t] : text_term(q, t, dot, slot[r]);
-                }
-                wave_sync();
-                K5T(10);
-            }
-            // e. the owners add the round's common columns in ascending order
-            const uint64_t rtm = cpre[R.ce] & ~cpre[R.ca];
-#pragma unroll
-            for (int kk = 0; kk < kSliceCpl; ++kk) {
-                const int p = kk * kWave + lane;
-                uint64_t mr = F > 0 ? mask[p] : 0ull;
-                uint32_t rr = F > 0 ? hbase[p] : 0u;
-                for (uint64_t pr = pend[kk] & rtm; pr; pr &= pr - 1) {
-                    const int t = __ffsll((unsigned long long)pr) - 1;
-                    const uint32_t cj = colj[t];
-                    const int cj0 = (int)(cj & 0xFFFFu), cj1 = (int)(cj >> 16);
-                    const uint64_t lm = low_bits((uint32_t)(min(cj1, jb) - ja));
-                    const uint64_t h = mr & lm;
-                    mr &= ~lm;
-                    const uint32_t r0 = rr;
-                    rr += (uint32_t)__popcll(h);
-                    if (cj0 >= ja && cj1 <= jb) {
-                        sum[kk] += h ? slot[r0] : q.sig0_col[t];
-                        continue;
-                    }
-                    // split column (rare): the dot over its segments in ascending order
-                    if (h) {
-                        uint64_t v = h;
-                        uint32_t r = r0;
-                        while (v) {
-                            const int jr = __ffsll((unsigned long long)v) - 1;
-                            v &= v - 1;
-                            cdot[kk] += tok_product(pt, ja + jr, hit[r++] & 0xFFu);
-                        }
-                        cnrm[kk] = slot[r0];
-                        chit |= 1u << kk;
-                    }
-                    if (cj1 <= jb) {
-                        const bool hh = (chit >> kk) & 1u;
-                        sum[kk] += (hh && cdot[kk] != 0.0) ? text_term(q, t, cdot[kk], cnrm[kk]) : q.sig0_col[t];
-                        cdot[kk] = 0.0;
-                        chit &= ~(1u << kk);
-                    }
-                }
-                if (F > 0) mask[p] = 0ull;
-            }
-            wave_sync();  // the next round rewrites the masks, slots, segments and map
-            K5T(11);
-        }
-        // 6. FAS (recommender_similarity.cpp:114-123) and the wave top-k
-        uint64_t keys[kSliceCpl];
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) {
-            uint64_t key = ~0ull;
-            if (!((skip >> kk) & 1u)) {
-                float f = 0.0f;
-                const int uk = (int)((used >> (8 * kk)) & 0xFFu);
-                if (uk > 0) {
-                    const double S = sum[kk] / (double)uk;
-                    const double Fv = ftab[uk];
-                    f = (S <= 0.0 && Fv <= 0.0) ? 0.0f : (float)((2.0 * S * Fv) / (S + Fv));
-                }
-                key = score_key(f, (int32_t)(c0 + kk * kWave + lane));
-            }
-            keys[kk] = key;
-        }
-        static_assert(kSliceCpl == 2, "2-key sort");
-        if (keys[1] < keys[0]) { const uint64_t x = keys[0]; keys[0] = keys[1]; keys[1] = x; }
-#pragma unroll
-        for (int kk = 0; kk < kSliceCpl; ++kk) topk_push(best, keys[kk], k, lane);
-        s = dyn ? s_lo + nw_g + (uint32_t)__shfl((int)claim, 0) : s + nw_g;
-        K5T(12);
-    }
-#ifdef PF_K5_TIMERS
-    tacc[13] = clock64() - tstart;
-    if (lane == 0) {
-        for (int i = 0; i < 14; ++i) atomicAdd(&g_k5t[i], (unsigned long long)tacc[i]);
-        atomicAdd(&g_k5t[15], 1ull);
-    }
-#endif
-    // idx -> uid in the wave's list (the same order: uid ascending == idx ascending)
-    if (lane < k && best != ~0ull) {
-        const uint32_t idx = (uint32_t)best ^ 0x80000000u;
-        best = (best & 0xFFFFFFFF00000000ull) | (ps.hdr[2 * (size_t)idx + 1].w ^ 0x80000000u);
-    }
-    uint64_t* sc = reinterpret_cast<uint64_t*>(wbase0 + kWsMask);  // wave 0's masks + slots (post_tail syncs first)
-    post_tail(best, k, sc, sync, parts, out, out_rows, qy, bx, nbx);
-}
-
 // ---------------------------------------------------------------- K2: merge
 // Key lists in[part * part_stride + q * query_stride + j] (j < k) -> out[q * k + j]
 // (the cross-shard merge after the all-gather; one block per query, every wave pushes
@@ -2511,13 +2028,13 @@ static void blog_report(int nbx) {
 hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t var_lds, int nq,
                        int blk_begin, int blk_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
                        const int32_t* out_rows, uint32_t mode, uint32_t tail_bs, hipEvent_t e0, hipEvent_t e1,
-                       hipStream_t s) {
+                       hipStream_t s, const uint8_t* qconst) {
     if (nq <= 0) return hipSuccess;
     // timed launches (e0, e1 given): the kernel's own start and end timestamps, taken from its
     // dispatch (hipExtLaunchKernelGGL), instead of two marker packets around it
     const dim3 grid = (mode & 2u) ? dim3(nq, blocks) : dim3(blocks, nq);
     hipExtLaunchKernelGGL(fas_post_kernel, grid, dim3(kPostThreads), post_lds(var_lds), s, e0, e1, 0u, ps, pool, img_off,
-                          blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs);
+                          blk_begin, blk_end, k, parts, sync, out, out_rows, mode, tail_bs, qconst);
 #ifdef PF_K5_BLOCKLOG
     {
         static int calls = 0;
@@ -2547,54 +2064,6 @@ hipError_t launch_post(const PostStore& ps, const uint8_t* pool, const uint32_t*
 #endif
     return hipGetLastError();
 }
-
-// K5s dynamic LDS: QConst | shared tables | PTok[n_tok] PList[n_lists] colof[n_tok] | per wave: fixed
-// arrays, ranges[n_lists], token and set prefixes
-uint32_t slice_lds(int n_tok, int n_lists) {
-    return (uint32_t)sizeof(QConst) + kSsFixed + slice_shared_var(n_tok, n_lists) +
-           kSliceWaves * slice_wave_bytes(n_tok, n_lists);
-}
-
-hipError_t launch_slice(const PostStore& ps, const uint8_t* pool, const uint32_t* img_off, uint32_t lds, int nq,
-                        int cand_begin, int cand_end, int k, int blocks, uint64_t* parts, ScanSync* sync, uint64_t* out,
-                        const int32_t* out_rows, uint32_t mode, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
-    if (nq <= 0) return hipSuccess;
-    hipExtLaunchKernelGGL(fas_slice_kernel, dim3(blocks, nq), dim3(kSliceThreads), lds, s, e0, e1, 0u, ps, pool, img_off,
-                          cand_begin, cand_end, k, parts, sync, out, out_rows, mode);
-#ifdef PF_K5_TIMERS
-    {
-        static int calls = 0;
-        unsigned long long t[16];
-        hipStreamSynchronize(s);
-        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_k5t), sizeof(t));
-        static const char* nm[14] = {"hdr+ranges", "prefix+excl", "plan0+issue0", "sets", "fixed", "plan+issue", "walk",
-                                     "slots", "place", "compact", "terms", "owner", "fas+topk", "total"};
-        if (++calls % 10 == 0) {
-            fprintf(stderr, "k5st per wave (clock64):");
-            for (int i = 0; i < 14; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double)t[i] / (double)t[15]);
-            fprintf(stderr, "\n");
-        }
-        const unsigned long long z[16] = {0};
-        hipMemcpyToSymbol(HIP_SYMBOL(g_k5t), z, sizeof(z));
-    }
-#endif
-    return hipGetLastError();
-}
-
-int slice_blocks_per_cu(uint32_t lds) {
-    static thread_local std::unordered_map<uint32_t, int> memo;
-    auto it = memo.find(lds);
-    if (it != memo.end()) return it->second;
-    int nb = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fas_slice_kernel, kSliceThreads, lds);
-    nb = (e == hipSuccess && nb > 0) ? nb : 1;
-    if (memo.size() > 4096) memo.clear();
-    memo.emplace(lds, nb);
-    return nb;
-}
-
-int slice_cands() { return kSliceCands; }
-int slice_waves() { return kSliceWaves; }
 
 int post_blocks_per_cu(uint32_t var_lds) {
     // per thread, by LDS bytes (a batch asks once per query: the occupancy API once per size)

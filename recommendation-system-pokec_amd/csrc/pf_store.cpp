@@ -889,11 +889,12 @@ void build_postings(const HostCorpus& hc, HostPost& hp) {
     hp.ok = true;
 }
 
-void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const std::vector<int32_t>& excl,
-                      std::vector<uint8_t>& img) {
+// The image's part after its QConst: QPostHead | QTok | QCol | PList | excl, offsets from the image
+// start (part start - sizeof(QConst)); written to out (out_cap bytes, zero-filled past the data).
+// Returns the part's size, or 0 when it exceeds out_cap.
+size_t build_query_post_part(const HostCorpus& hc, const HostPost& hp, int32_t i, const std::vector<int32_t>& excl,
+                             uint8_t* out, size_t out_cap) {
     const int T = hc.T;
-    QConst c;
-    fill_qconst(hc, true, i, c);
     std::vector<QTok> toks;
     std::vector<QCol> cols;
     for (int t = 0; t < T; ++t) {
@@ -947,13 +948,38 @@ void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const
     o = a16(o + sets.size() * sizeof(PList));
     h.excl_off = (int32_t)o;
     o = a16(o + ex.size() * 4);
-    img.assign(o, 0);
+    const size_t part = o - sizeof(QConst);
+    if (part > out_cap) return 0;
+    auto at = [&](int32_t img_off) { return out + ((size_t)img_off - sizeof(QConst)); };  // offsets: from the image start
+    std::memset(out, 0, out_cap);
+    std::memcpy(out, &h, sizeof h);
+    if (!toks.empty()) std::memcpy(at(h.tok_off), toks.data(), toks.size() * sizeof(QTok));
+    if (!cols.empty()) std::memcpy(at(h.col_off), cols.data(), cols.size() * sizeof(QCol));
+    if (!sets.empty()) std::memcpy(at(h.set_off), sets.data(), sets.size() * sizeof(PList));
+    if (!ex.empty()) std::memcpy(at(h.excl_off), ex.data(), ex.size() * 4);
+    return part;
+}
+
+size_t post_part_bound(const HostCorpus& hc, int32_t i, size_t n_excl) {
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const int T = hc.T;
+    const size_t ntok = (size_t)(hc.tok_off[(size_t)(i + 1) * T] - hc.tok_off[(size_t)i * T]);
+    size_t nact = 0;
+    for (int t = 0; t < T; ++t) nact += hc.tok_off[(size_t)i * T + t + 1] != hc.tok_off[(size_t)i * T + t];
+    const size_t nset = (size_t)(hc.club_off[i + 1] - hc.club_off[i]) + (size_t)(hc.friend_off[i + 1] - hc.friend_off[i]);
+    return a16(sizeof(QPostHead)) + a16(ntok * sizeof(QTok)) + a16(nact * sizeof(QCol)) + a16(nset * sizeof(PList)) +
+           a16(n_excl * 4);
+}
+
+void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t i, const std::vector<int32_t>& excl,
+                      std::vector<uint8_t>& img) {
+    QConst c;
+    fill_qconst(hc, true, i, c);
+    const size_t cap = post_part_bound(hc, i, excl.size());
+    img.assign(sizeof(QConst) + cap, 0);
     std::memcpy(img.data(), &c, sizeof c);
-    std::memcpy(img.data() + sizeof(QConst), &h, sizeof h);
-    if (!toks.empty()) std::memcpy(img.data() + h.tok_off, toks.data(), toks.size() * sizeof(QTok));
-    if (!cols.empty()) std::memcpy(img.data() + h.col_off, cols.data(), cols.size() * sizeof(QCol));
-    if (!sets.empty()) std::memcpy(img.data() + h.set_off, sets.data(), sets.size() * sizeof(PList));
-    if (!ex.empty()) std::memcpy(img.data() + h.excl_off, ex.data(), ex.size() * 4);
+    const size_t part = build_query_post_part(hc, hp, i, excl, img.data() + sizeof(QConst), cap);
+    img.resize(sizeof(QConst) + part);
 }
 
 }  // namespace pf

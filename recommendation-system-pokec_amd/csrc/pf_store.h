@@ -153,6 +153,11 @@ void build_postings(const HostCorpus& hc, HostPost& hp);
 // Postings query image of candidate idx (pf_types.h layout); excl = uids to exclude
 void build_query_post(const HostCorpus& hc, const HostPost& hp, int32_t idx, const std::vector<int32_t>& excl,
                       std::vector<uint8_t>& img);
+// The part of build_query_post's image after its QConst (offsets from the image start), into
+// out[0, out_cap); returns its size (0: larger than out_cap).  post_part_bound(i, |excl|) bounds it.
+size_t build_query_post_part(const HostCorpus& hc, const HostPost& hp, int32_t idx, const std::vector<int32_t>& excl,
+                             uint8_t* out, size_t out_cap);
+size_t post_part_bound(const HostCorpus& hc, int32_t idx, size_t n_excl);
 int build_store(const HostCorpus& hc, HostStore& hs, std::string& err);
 // excl: uids to exclude (all-candidates mode), may be null
 // returns false when the cuckoo table cannot be built within kMaxHashLog2

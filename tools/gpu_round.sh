@@ -14,6 +14,11 @@
 #   cfg5c1       cfg 5 at one context with the host stage clocks (PF_DEBUG host_prof=1) -> cfg5c1.err
 #   k5t          profiling build (tools/build_variant.sh k5t K5T=1 -> vlib/k5t) per-phase K5 clocks -> k5t.err
 #   pmc:NAME:C1,C2..  one rocprofv3 --pmc pass over a 20-step cfg-2 run -> pmc_NAME/
+#   ab:W:N:R:A/B  alternating A/B bench lines (replaces the per-run tools/r*.sh scripts of rounds 4-5):
+#                 workload W (cfg2..cfg5), N timed steps, R pairs; A and B are each "-" (the default
+#                 tree), a PF_DEBUG setting (e.g. k5_dyn=0), or lib=V (the variant library vlib/V);
+#                 every line appended to ab_W.txt as "A|B <json>"
+#   trace:N       rocprofv3 kernel trace (csv, no stats) of an N-step cfg-2 run -> trace/
 set -o pipefail
 TAG=$1
 shift
@@ -115,6 +120,20 @@ for S in "$@"; do
     pmc:*)
         R=${S#pmc:}; N=${R%%:*}; C=${R#*:}
         timeout -s KILL 120 rocprofv3 --pmc ${C//,/ } -d $O/pmc_$N -o run -- python3 bench.py --steps 20 --warmup 5 $Q > $O/pmc_$N.json 2> $O/pmc_$N.err || exit 8 ;;
+    ab:*)
+        IFS=: read -r _ W N R AB <<< "$S"
+        for ((i = 0; i < R; i++)); do
+            for V in "${AB%%/*}" "${AB#*/}"; do
+                E=(env)
+                if [[ $V == lib=* ]]; then E+=(PF_LIB_PATH=$PWD/vlib/${V#lib=}/libpokec_fas.so)
+                elif [[ $V != - ]]; then E+=(PF_DEBUG=$V); fi
+                timeout -k 10 600 "${E[@]}" python3 bench.py --workload $W --steps $N --warmup 10 $Q > $O/ab.json 2> $O/ab.err || exit 13
+                (echo -n "$V "; tail -1 $O/ab.json) >> $O/ab_$W.txt
+            done
+        done ;;
+    trace:*)
+        N=${S#trace:}
+        timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o tr -- python3 bench.py --steps $N --warmup 5 $Q > $O/trace.json 2> $O/trace.err || exit 3 ;;
     *)
         echo "unknown step $S"; exit 9 ;;
     esac

@@ -5,7 +5,7 @@ import sys
 p = os.path.join(sys.argv[1], "pf_kernels.hip")
 s = open(p).read()
 k0 = s.index("void fas_post_kernel(")
-k1 = s.index("// ---------------------------------------------------------------- K5s: wave-private slice scan")
+k1 = s.index("// ---------------------------------------------------------------- K2: merge")
 k = s[k0:k1]
 a = "        if (tid < 64) {  // read after the barrier below\n            wave_prefix(gpre, rng, H.n_tok, lane);"
 assert k.count(a) == 1

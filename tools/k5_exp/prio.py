@@ -6,7 +6,7 @@ import sys
 p = os.path.join(sys.argv[1], "pf_kernels.hip")
 s = open(p).read()
 k0 = s.index("void fas_post_kernel(")
-k1 = s.index("// ---------------------------------------------------------------- K5s: wave-private slice scan")
+k1 = s.index("// ---------------------------------------------------------------- K2: merge")
 k = s[k0:k1]
 a = "    const uint8_t* img = pool + img_off[qy];\n    const QPostHead H = *reinterpret_cast<const QPostHead*>(img + sizeof(QConst));"
 assert k.count(a) == 1

@@ -7,7 +7,7 @@ d = sys.argv[1]
 p = os.path.join(d, "pf_kernels.hip")
 s = open(p).read()
 a = s.index("void fas_post_kernel(")
-b = s.index("// ---------------------------------------------------------------- K5s: wave-private slice scan")
+b = s.index("// ---------------------------------------------------------------- K2: merge")
 k = s[a:b]
 
 

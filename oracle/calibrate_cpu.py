@@ -70,7 +70,7 @@ def main():
            "reference": {"seconds": round(ref_s, 3), "candidates_per_s": ref_n / ref_s,
                          "binary": "oracle/_ref/ref_timing (reference sources, g++ -O3)"},
            "port": {"seconds": round(port_s, 3), "candidates_per_s": ref_n / port_s,
-                    "binary": "oracle/librefcpu.so (oracle/refcpu.cpp, g++ -O2)"},
+                    "binary": "oracle/librefcpu.so (oracle/refcpu.cpp, g++ -O3, oracle/Makefile)"},
            "port_over_reference": (ref_n / port_s) / (ref_n / ref_s),
            "top10_identical": bool(same)}
     s = json.dumps(out)

@@ -234,6 +234,14 @@ int pf_set_scan_kernel(pf_ctx* ctx, int32_t kind);
  * serialised on ONE stream (the context's own calls use its internal stream and
  * synchronise before returning, so mixing them with this call is safe only after
  * the caller has synchronised `stream`).
+ * nq = 1 on a stream other than the context's runs on the context's scan lanes:
+ * the launch goes to the next lane's stream (the context's stream and its two aux
+ * streams in turn; three quarters of a resident round of workgroups each) without waiting for work the caller queued on `stream`
+ * earlier, and `stream` waits for it and copies its row into d_keys, in call
+ * order; so consecutive single-query calls overlap on the device.  A single
+ * query whose resident postings image is current (built at pf_open; a
+ * pf_set_adj of that user makes it stale) builds and uploads nothing: one
+ * launch, one wait, one row copy.
  */
 int pf_scan_keys_async(pf_ctx* ctx, const int32_t* query_uid, int32_t nq,
                        int32_t topk, uint64_t* d_keys, void* stream);

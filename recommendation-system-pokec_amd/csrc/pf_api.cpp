@@ -305,10 +305,17 @@ int post_image_per_cu(const pf::QPostHead* h) {
     return pf::post_blocks_per_cu(pf::post_var_lds(h->n_tok, h->n_tok + h->n_club + h->n_friend));
 }
 
-// Workgroups of a one-query postings scan: one resident round (PF_DEBUG k5_wgs=N overrides it, A/B)
-int one_query_wgs(int resident) {
+int scan_lanes();
+
+// Workgroups of a one-query postings scan: one resident round, or three quarters of one on the
+// scan lanes, where consecutive queries' launches share the CUs and a launch of fewer workgroups
+// (more blocks each: fewer image stagings and merge lists per block) lets the next one start
+// sooner: cfg 2 1.209 / 1.205 / 1.200e10 (1,024) -> 1.216 / 1.229 / 1.214e10 (768) candidates/s
+// with three lanes, alternating on one box (r9j; 896: 1.224 / 1.202e10, 640: 1.211 / 1.217e10;
+// with two lanes 768 lost, r9i).  PF_DEBUG k5_wgs=N overrides it (A/B).
+int one_query_wgs(int resident, bool lanes) {
     static const long n = pf::debug_long("k5_wgs", 0);
-    return n > 0 ? (int)n : resident;
+    return n > 0 ? (int)n : (lanes && scan_lanes() >= 3 ? ((resident * 3 / 4) & ~7) : resident);
 }
 
 // Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
@@ -358,7 +365,9 @@ struct LaneUse {
 };
 
 int scan_lanes() {
-    static const int n = (int)std::min(3L, pf::debug_long("scan_lanes", 2));
+    // three by default (the context's stream and both aux streams): 1.204 / 1.205 / 1.206e10 vs
+    // 1.202 / 1.195 / 1.192e10 with two, alternating on one box (r9d, resident images)
+    static const int n = (int)std::min(3L, pf::debug_long("scan_lanes", 3));
     return n;
 }
 
@@ -435,7 +444,8 @@ int scan_post(pf_ctx* c, const std::vector<const std::vector<uint8_t>*>& imgs, c
     // cover a few queries at a time and share their lists and cells in L2; with one resident
     // round looping over every query's range instead, 256 queries run at once and L2 hits
     // collapse (per-query time 0.2 ms at 4 queries per launch, 0.68 ms at 1024).
-    const int blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)))
+    const bool on_lane = nq == 1 && scan_lanes() >= 2 && s != c->stream;  // lane_begin's choice, below
+    const int blocks = nq == 1 ? std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu, on_lane)))
                                : std::max(1, (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg());
     const size_t offs_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
     const size_t rows_b = ((size_t)nq * 4 + 15) & ~(size_t)15;
@@ -519,11 +529,11 @@ int scan_post_resident(pf_ctx* c, int32_t i, int32_t row, int k, uint64_t* d_key
     const uint32_t vl = R.var_lds[i];
     const int per_cu = pf::post_blocks_per_cu(vl);
     const int nwb = c->wb_end - c->wb_begin;
-    const int blocks = std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu)));
     LaneUse lu;
     int rc = lane_begin(c, s, lu);
     if (rc != PF_OK) return rc;
     pf_ctx::ScanLane* ln = lu.ln;
+    const int blocks = std::max(1, std::min(nwb, one_query_wgs(c->num_cus * per_cu, ln != nullptr)));
     const hipStream_t ls = ln ? ln->st : s;
     DBuf& part_buf = ln ? ln->part : c->d_part;
     DBuf& sync_buf = ln ? ln->sync : R.d_sync;
@@ -1276,7 +1286,7 @@ int pf_scan_bytes(pf_ctx* c, const int32_t* q, int32_t nq, int64_t* out) {
     }
     // workgroups that stage a query's image, as scan_post launches the fitting queries
     const int nwb = c->wb_end - c->wb_begin;
-    const int wgs = nfit == 1 ? one_query_wgs(c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists)))
+    const int wgs = nfit == 1 ? one_query_wgs(c->num_cus * pf::post_blocks_per_cu(pf::post_var_lds(max_tok, max_lists)), true)
                               : (nwb + batch_blocks_per_wg() - 1) / batch_blocks_per_wg();
     par_jobs((size_t)nq, [&](size_t i) {
         out[i] = kind[i] == 0 ? 0 : (kind[i] == 2 ? k1 : post_query_bytes(c, imgs[i], wgs));

@@ -276,7 +276,7 @@ struct pf_ctx {
         bool used[kLaneGroups] = {};
         int row = 0;
     };
-    ScanLane lane[3];  // two by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 3 adds the aux2 stream)
+    ScanLane lane[3];  // three by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 2 without the aux2 stream)
     int lane_cur = 0;
     // Resident postings-scan images (pf_api.cpp build_resident_post): every user's K5 image part
     // after its QConst (QPostHead | tokens | columns | set lists | exclusions = adj_list row + self),

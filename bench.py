@@ -1089,9 +1089,9 @@ def main():
         eng.profile_sample(0)
         if iso_n:
             isolated = {"launches": iso_n, "avg_launch_ms": iso_ms / iso_n,
-                        "note": "the first timed queries again, one at a time after the timed region: the "
-                                "kernel's own duration (avg_launch_ms above spans the overlap of consecutive "
-                                "launches on the scan lanes)"}
+                        "note": "the first timed queries again, one at a time after the timed region (the same launch "
+                                "shape: three quarters of a resident round of workgroups); the roofline's avg_launch_ms is the "
+                                "steady-state time per launch"}
 
 
     value = Q * n_cand * steps / elapsed
@@ -1181,10 +1181,12 @@ def main():
         "host_enqueue_ms_per_step": t_submitted * 1e3 / steps,
     }
     if isolated is not None and phys_per_launch:
-        # one query per step overlaps consecutive launches on the scan lanes, so the timed launches'
-        # events span their neighbours' tails: the roofline divides the kernel's bytes by its
-        # isolated launch (the same queries again, one at a time) and keeps the overlapped figures
-        # and the per-step rate as named fields beside it
+        # One query per step: consecutive launches overlap on the scan lanes (up to three in flight),
+        # so a timed launch's HIP events span its neighbours' work and no launch runs alone.  The
+        # roofline divides a launch's bytes by the steady-state time per launch, ms_per_step (the
+        # timed region's launch-to-launch interval; rocprofv3's trace of the same run gives the same
+        # span over its K5 dispatches, profiles/r9*_k5_trace_summary.json), and keeps the overlapped
+        # events and an isolated launch (the same queries once more, one at a time) as named fields
         iso_bytes = float(np.mean([phys[i * Q:(i + 1) * Q].sum() for i in range(isolated["launches"])]))
         iso_gbs = iso_bytes / (isolated["avg_launch_ms"] * 1e-3) / 1e9
         R = rec["roofline"]
@@ -1193,17 +1195,18 @@ def main():
                                   "frac": None if achieved is None else achieved / HBM_PEAK_GBS,
                                   "note": "the timed region's launches, each overlapping its neighbours on the "
                                           "scan lanes (HIP events span the overlap)"}
-        step_gbs = phys_per_launch / (rec["ms_per_step"] * 1e-3) / 1e9
-        R["per_step"] = {"achieved": step_gbs, "frac": step_gbs / HBM_PEAK_GBS,
-                         "note": "bytes per launch / ms_per_step (the steady-state rate of the timed region)"}
-        R.update({"achieved": iso_gbs, "frac": iso_gbs / HBM_PEAK_GBS, "avg_launch_ms": isolated["avg_launch_ms"],
-                  "timed_launches": isolated["launches"], "bytes_per_launch": iso_bytes,
-                  "launch_basis": "isolated (one launch at a time, HIP events on the lane stream)",
-                  "dram_gbs": rate_ms(traffic, isolated["avg_launch_ms"]),
-                  "dram_frac": (None if traffic is None else rate_ms(traffic, isolated["avg_launch_ms"]) / HBM_PEAK_GBS),
-                  "d3_equiv_gbs": rate_ms(alg_bytes, isolated["avg_launch_ms"])})
+        step_ms = rec["ms_per_step"]
+        step_gbs = phys_per_launch / (step_ms * 1e-3) / 1e9
+        R.update({"achieved": step_gbs, "frac": step_gbs / HBM_PEAK_GBS, "avg_launch_ms": step_ms,
+                  "launch_basis": "steady state: the timed region's time per launch (ms_per_step; launches overlap "
+                                  "on the scan lanes)",
+                  "dram_gbs": rate_ms(traffic, step_ms),
+                  "dram_frac": (None if traffic is None else rate_ms(traffic, step_ms) / HBM_PEAK_GBS),
+                  "d3_equiv_gbs": rate_ms(alg_bytes, step_ms)})
         R["d3_equiv_x_peak"] = R["d3_equiv_gbs"] / HBM_PEAK_GBS
+        isolated["bytes_per_launch"] = iso_bytes
         isolated["achieved_gbs"], isolated["frac"] = iso_gbs, iso_gbs / HBM_PEAK_GBS
+        isolated["dram_frac"] = None if traffic is None else rate_ms(traffic, isolated["avg_launch_ms"]) / HBM_PEAK_GBS
         R["isolated_launch"] = isolated
     if n1 is not None:
         rec["n1_same_workload"] = n1

@@ -578,6 +578,53 @@ def test_scan_lanes_match_synchronous_calls(big):
                               np.asarray(r[1], np.float32).view(np.uint32)), q
 
 
+def test_resident_image_follows_adj_edits(big):
+    """A single query scans from its resident postings image (built at pf_open, its exclusions =
+    the open-time adj_list row + self) until pf_set_adj edits that user's row; the query then
+    builds its image per call with the edited exclusions.  Both the synchronous all-candidates call
+    and one-query calls on a caller's stream (the scan lanes) equal the oracle under the same
+    edits (recommender_graph.cpp:46-52: adj[q] and q are never recommended), and other users keep
+    their resident images."""
+    import torch
+    pf = tl.product()
+    c, eng, orc = big
+    u, v = 777, 778
+    base = tl.corpus_from_desc(c.desc_ptr())
+    ref = orc.interest([u, v], 10, tl.PF_MODE_ALL, 0)
+    # the edit excludes u's current top-3 and drops its old row
+    row = [int(x) for x in ref[0][0][:3]]
+    s = torch.cuda.Stream()
+    outs = torch.empty((2, 10), dtype=torch.int64, device="cuda")
+
+    def lanes():
+        for i, q in enumerate((u, v)):
+            eng.scan_keys_async(np.array([q], np.int32), 10, outs[i].data_ptr(), s.cuda_stream)
+        s.synchronize()
+        keys = outs.cpu().numpy().view(np.uint64)
+        return [pf.decode_keys(keys[i]) for i in range(2)]
+
+    def same(got, want):
+        for (gu, gs), (wu, ws) in zip(got, want):
+            assert list(gu) == list(wu)
+            assert np.array_equal(np.asarray(gs, np.float32).view(np.uint32), np.asarray(ws, np.float32).view(np.uint32))
+
+    same(lanes(), ref)
+    i = int(np.nonzero(base.adj_uid == u)[0][0]) if (base.adj_uid == u).any() else -1
+    r0 = base.adj_nbr[base.adj_off[i]:base.adj_off[i + 1]] if i >= 0 else None
+    try:
+        eng.set_adj(u, row)
+        orc.set_adj(u, row)
+        want = orc.interest([u, v], 10, tl.PF_MODE_ALL, 0)
+        assert not set(row) & set(int(x) for x in want[0][0])
+        same(lanes(), want)
+        same(eng.recommend_interest_all([u, v], 10), want)
+        same(eng.recommend_interest_all([u], 10), want[:1])
+    finally:
+        eng.set_adj(u, r0)
+        orc.set_adj(u, r0)
+    same(lanes(), ref)
+
+
 def test_profile_sampling_counts_and_results(big):
     """pf_profile_sample: with every = 3, launches 0, 3, 6 of nine are timed (positive device
     time), the untimed ones return the same keys as timed ones; every = 1 times all."""

@@ -167,9 +167,10 @@ int pf_eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t samp
  * on the device; out_hits / out_club are written when pf_wait(ctx, *ticket) returns, or when the
  * next call on the context that uses the job pipeline completes it first (that call plans and
  * launches its own first chunk before, so one context overlaps step i + 1's host planning with
- * step i's last device chunk).  The caller keeps the output buffers AND ds alive until then (the
- * call's driver reads ds's profiles when its last chunk is unpacked); *n_plan is written before
- * this returns.  pf_dataset_free does not wait for such a call. */
+ * step i's last device chunk).  The caller keeps the output buffers alive until then; the call
+ * holds ds (its driver reads ds's profiles when its last chunk is unpacked), so a pf_dataset_free
+ * meanwhile defers the delete until the call completes or its context is closed.  *n_plan is
+ * written before this returns. */
 int pf_eval_recommendation_tests_async(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk,
                                        int32_t shard, int32_t nshards, int32_t batch, int8_t* out_hits,
                                        double* out_club, int32_t cap, int32_t* n_plan, uint64_t* ticket);

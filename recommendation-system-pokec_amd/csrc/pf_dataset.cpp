@@ -107,6 +107,12 @@ struct Row {
 }  // namespace
 
 struct pf_dataset {
+    // a carried pf_eval_recommendation_tests_async call reads rows / profiles when its last chunk is
+    // unpacked: it holds the dataset (DsHold), and pf_dataset_free of a held dataset defers the delete
+    // to the last holder
+    std::mutex hold_mu;
+    int holds = 0;
+    bool free_pending = false;
     std::vector<std::string> cols;
     std::vector<Row> rows;                             // slot = first appearance of the uid
     std::unordered_map<int, int32_t> profiles;         // uid -> slot, built like out_profiles
@@ -734,7 +740,17 @@ int pf_dataset_load_cached(const char* root, int64_t max_lines, const char* cach
     return PF_OK;
 }
 
-void pf_dataset_free(pf_dataset* ds) { delete ds; }
+void pf_dataset_free(pf_dataset* ds) {
+    if (!ds) return;
+    {
+        std::lock_guard<std::mutex> g(ds->hold_mu);
+        if (ds->holds > 0) {  // a carried call still reads it: its last holder deletes it
+            ds->free_pending = true;
+            return;
+        }
+    }
+    delete ds;
+}
 
 const pf_corpus_desc* pf_dataset_desc(const pf_dataset* ds) { return ds ? &ds->desc : nullptr; }
 
@@ -1292,6 +1308,26 @@ int eval_holdout_friends(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size,
     return PF_OK;
 }
 
+// The carried call's hold on its dataset (pf_dataset::holds): released when the call's closure is
+// destroyed (finished, failed or dropped by pf_close), deleting a dataset freed meanwhile.
+struct DsHold {
+    pf_dataset* ds;
+    explicit DsHold(const pf_dataset* d) : ds(const_cast<pf_dataset*>(d)) {
+        std::lock_guard<std::mutex> g(ds->hold_mu);
+        ++ds->holds;
+    }
+    ~DsHold() {
+        bool del = false;
+        {
+            std::lock_guard<std::mutex> g(ds->hold_mu);
+            del = --ds->holds == 0 && ds->free_pending;
+        }
+        if (del) delete ds;
+    }
+    DsHold(const DsHold&) = delete;
+    DsHold& operator=(const DsHold&) = delete;
+};
+
 int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_size, int32_t topk, int32_t shard,
                               int32_t nshards, int32_t batch, int8_t* out_hits, double* out_club, uint64_t* digest,
                               int32_t cap, int32_t* n_plan, uint64_t* ticket = nullptr) {
@@ -1362,9 +1398,11 @@ int eval_recommendation_tests(pf_ctx* ctx, const pf_dataset* ds, int32_t sample_
                 J.view.own_row = &pe.newf;
             }
         }
-        if (ticket && e == mine->size())  // the last batch stays on the device (its results: pf_wait)
+        if (ticket && e == mine->size()) {  // the last batch stays on the device (its results: pf_wait)
+            auto hold = std::make_shared<DsHold>(ds);  // ds outlives the carried call (pf_dataset_free defers)
             return pf::run_jobs_carry(ctx, std::move(jobs), *ticket,
-                                      [score, b, e](std::vector<pf::Job>& js) { score(js, b, e); });
+                                      [score, b, e, hold](std::vector<pf::Job>& js) { score(js, b, e); });
+        }
         const int rc = pf::run_jobs(ctx, jobs);
         if (rc != PF_OK) return rc;
         score(jobs, b, e);

@@ -1005,6 +1005,15 @@ def test_async_driver_calls_equal_sync():
             assert np.array_equal(pf.merge_shards([h for h, _ in parts]), ref[0]), (n, batch, nsh)
     _, rect = tl.golden_digests("A", "rectests_digest.txt")
     assert np.array_equal(ds.recommendation_tests_digest(eng, m["digest_rectest"], 10), rect)
+    # pf_dataset_free of a dataset a carried call still reads defers the delete to the call's end
+    n = m["digest_rectest"]
+    ref = ds.eval_recommendation_tests(eng, n, 10, 0, 1, 128)
+    with tempfile.TemporaryDirectory() as d:
+        tl.regen_reference_dir("A", d)
+        ds2 = pf.Dataset(d)
+    p = ds2.eval_recommendation_tests_async(eng, n, 10, 0, 1, 128)
+    ds2.close()
+    assert same(ds.eval_wait(eng, p), ref)
     eng.close()
 
 

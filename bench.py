@@ -901,6 +901,11 @@ def main():
                     help="cfg2/cfg4 analysis only (not the workload): every query of every step is the first "
                          "query of the stream, so a batch's lists are all shared (bounds what a query-tiled "
                          "batch could save; the line's config says so)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="analysis: hardware queues for this process (GPU_MAX_HW_QUEUES, set before HIP starts; 0 = "
+                         "the environment's, HIP's default 4); pair with PF_DEBUG scan_lanes=N.  16 queues with 15 "
+                         "lanes read +3-5 %% over 200 steps but degrade with the backlog of longer runs "
+                         "(profiles/r9_ab.txt r9x-r9ze), so the default line keeps four")
     ap.add_argument("--force-dist", action="store_true",
                     help="cfg2/cfg4 at WORLD_SIZE=1: run the N > 1 step anyway (scan into the local keys, an RCCL "
                          "all_gather_into_tensor on the scan stream, pf_merge_keys_async), so the communicator, "
@@ -920,6 +925,8 @@ def main():
         args.steps = 200 if args.workload == "cfg2" else 50
     if args.contexts is None:
         args.contexts = 1
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, args.hw_queues))  # before any HIP call
     if args.workload == "cfg5":
         return run_cfg5(args, world, rank, local)
     import synth
@@ -1090,7 +1097,7 @@ def main():
         if iso_n:
             isolated = {"launches": iso_n, "avg_launch_ms": iso_ms / iso_n,
                         "note": "the first timed queries again, one at a time after the timed region (the same launch "
-                                "shape: three quarters of a resident round of workgroups); the roofline's avg_launch_ms is the "
+                                "shape: seven eighths of a resident round of workgroups); the roofline's avg_launch_ms is the "
                                 "steady-state time per launch"}
 
 
@@ -1157,6 +1164,7 @@ def main():
                    "workload_key": workload + ("_samequery" if args.same_query else ""), "n_users": args.users,
                    "queries_per_step": Q, "topk": k,
                    "parallelism": f"candidate-shard x{world}" + (" + all_gather" if use_dist else ""),
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
                    **({"force_dist": "the N > 1 step (local keys, RCCL all-gather, device merge) at world 1: a "
                                      "code-path check, not a scaling point"} if use_dist and world == 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

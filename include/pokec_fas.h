@@ -236,7 +236,7 @@ int pf_set_scan_kernel(pf_ctx* ctx, int32_t kind);
  * the caller has synchronised `stream`).
  * nq = 1 on a stream other than the context's runs on the context's scan lanes:
  * the launch goes to the next lane's stream (the context's stream and its two aux
- * streams in turn; three quarters of a resident round of workgroups each) without waiting for work the caller queued on `stream`
+ * streams in turn; seven eighths of a resident round of workgroups each) without waiting for work the caller queued on `stream`
  * earlier, and `stream` waits for it and copies its row into d_keys, in call
  * order; so consecutive single-query calls overlap on the device.  A single
  * query whose resident postings image is current (built at pf_open; a

@@ -307,15 +307,23 @@ int post_image_per_cu(const pf::QPostHead* h) {
 
 int scan_lanes();
 
-// Workgroups of a one-query postings scan: one resident round, or three quarters of one on the
+// Workgroups of a one-query postings scan: one resident round, or seven eighths of one on the
 // scan lanes, where consecutive queries' launches share the CUs and a launch of fewer workgroups
-// (more blocks each: fewer image stagings and merge lists per block) lets the next one start
-// sooner: cfg 2 1.209 / 1.205 / 1.200e10 (1,024) -> 1.216 / 1.229 / 1.214e10 (768) candidates/s
-// with three lanes, alternating on one box (r9j; 896: 1.224 / 1.202e10, 640: 1.211 / 1.217e10;
-// with two lanes 768 lost, r9i).  PF_DEBUG k5_wgs=N overrides it (A/B).
+// lets the next one start sooner.  Over 200-step lines three quarters read best (cfg 2 1.209 /
+// 1.205 / 1.200e10 at 1,024 -> 1.216 / 1.229 / 1.214e10 at 768 with three lanes, r9j; 896: 1.224 /
+// 1.202e10), but in the driver's 20-step line, where the first and last launches of the timed
+// region run with no neighbour, 768 lost 1.5 % (r9zf) and 896 is the best of 1,024 / 896 / two
+// lanes of 1,024 (1.199 vs 1.190 / 1.196e10, six runs each, r9zg).  PF_DEBUG k5_wgs=N overrides it.
+// More lanes (more hardware queues, scan_lanes) take smaller launches still: 15 lanes of 192 (3/16 of
+// a round) 1.273 / 1.277e10, of 256 1.238-1.267e10, of 320 1.256 / 1.265e10; 7 lanes of 512 or 384
+// 1.235-1.251e10 (r9x-r9z, tools/hwq_probe.sh).
 int one_query_wgs(int resident, bool lanes) {
     static const long n = pf::debug_long("k5_wgs", 0);
-    return n > 0 ? (int)n : (lanes && scan_lanes() >= 3 ? ((resident * 3 / 4) & ~7) : resident);
+    if (n > 0) return (int)n;
+    if (!lanes) return resident;
+    const int nl = scan_lanes();
+    const int w = nl >= 12 ? resident * 3 / 16 : (nl >= 6 ? resident / 2 : (nl >= 3 ? resident * 7 / 8 : resident));
+    return std::max(8, w & ~7);
 }
 
 // Timing events of one scan launch (the profiling pool when pf_profile_reset is on).  A
@@ -366,8 +374,13 @@ struct LaneUse {
 
 int scan_lanes() {
     // three by default (the context's stream and both aux streams): 1.204 / 1.205 / 1.206e10 vs
-    // 1.202 / 1.195 / 1.192e10 with two, alternating on one box (r9d, resident images)
-    static const int n = (int)std::min(3L, pf::debug_long("scan_lanes", 3));
+    // 1.202 / 1.195 / 1.192e10 with two, alternating on one box (r9d, resident images).  More lanes run
+    // on streams of their own and need a process with more hardware queues (GPU_MAX_HW_QUEUES): 15
+    // lanes on 16 queues read +3-5 % over 200 steps but degrade as the backlog grows (1,000 steps
+    // 1.17e10, 2,000 1.06-1.08e10, against 1.24e10 for three lanes on four queues at either length,
+    // r9zd / r9ze; past 16 queues the process oversubscribes the hardware queue slots, r9za), so
+    // they stay an A/B (PF_DEBUG scan_lanes=N, up to 16)
+    static const int n = (int)std::min((long)pf_ctx::kMaxLanes, pf::debug_long("scan_lanes", 3));
     return n;
 }
 
@@ -386,7 +399,8 @@ int lane_begin(pf_ctx* c, hipStream_t caller, LaneUse& u) {
     // streams of their own would share the process's four hardware queues with them
     // (PF_DEBUG lazy_aux=1: no aux streams yet, every lane on the context's stream)
     const hipStream_t ls[3] = {c->stream, c->jb.aux, c->jb.aux2};
-    ln->st = ls[li] ? ls[li] : c->stream;
+    ln->st = li < 3 ? ls[li] : c->lane_st[li];
+    if (!ln->st) ln->st = c->stream;
     const int r = ln->row;
     ln->row = (r + 1) % pf_ctx::kLaneRows;
     const int g = r / pf_ctx::kLaneGroupRows;
@@ -870,6 +884,11 @@ int pf_open(const pf_corpus_desc* desc, int device, pf_ctx** out) {
         c->err = "stream/event creation failed";
         return bail(PF_ENODEV);
     }
+    for (int l = 3; l < scan_lanes(); ++l)  // lanes past the context's and the aux streams
+        if (hipStreamCreateWithFlags(&c->lane_st[l], hipStreamNonBlocking) != hipSuccess) {
+            c->err = "stream creation failed";
+            return bail(PF_ENODEV);
+        }
     auto& hs = c->hs;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = upload(c, c->d_stream, hs.stream);
@@ -976,12 +995,14 @@ void pf_close(pf_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->jb.aux2) (void)hipStreamSynchronize(c->jb.aux2);
     for (auto& e : c->prof_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
-    for (auto& ln : c->lane) {  // (their streams are the context's and the aux streams)
+    for (auto& ln : c->lane) {  // (their streams are the context's, the aux streams and lane_st)
         if (ln.st) (void)hipStreamSynchronize(ln.st);
         if (ln.done) (void)hipEventDestroy(ln.done);
         for (hipEvent_t e : ln.freed)
             if (e) (void)hipEventDestroy(e);
     }
+    for (hipStream_t st : c->lane_st)
+        if (st) (void)hipStreamDestroy(st);
     for (auto& st : c->stage) {
         if (st.done) (void)hipEventDestroy(st.done);
         if (st.p) (void)hipHostFree(st.p);

@@ -276,7 +276,13 @@ struct pf_ctx {
         bool used[kLaneGroups] = {};
         int row = 0;
     };
-    ScanLane lane[3];  // three by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 2 without the aux2 stream)
+    // three by default (PF_DEBUG scan_lanes=N: 0 / 1 off, 2 without the aux2 stream); lanes past the
+    // third run on streams of their own (lane_st, created at open when scan_lanes asks for them):
+    // with the process's default four hardware queues they would share them (an A/B for processes
+    // that raise GPU_MAX_HW_QUEUES; pf_api.cpp scan_lanes)
+    static constexpr int kMaxLanes = 16;
+    ScanLane lane[kMaxLanes];
+    hipStream_t lane_st[kMaxLanes] = {};
     int lane_cur = 0;
     // Resident postings-scan images (pf_api.cpp build_resident_post): every user's K5 image part
     // after its QConst (QPostHead | tokens | columns | set lists | exclusions = adj_list row + self),

@@ -11,12 +11,13 @@
 //   k5_transposed=1       batched postings scans on the query-fastest grid (A/B; measured slower)
 //   k5_static=1           one-query postings scans with the static block hand-out (A/B)
 //   k5_batch_blocks=N     blocks per workgroup of a batched postings scan (default 32; A/B)
-//   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round, three
-//                         quarters of one on the scan lanes; A/B)
+//   k5_wgs=N              workgroups of a one-query postings scan (default: one resident round; on the
+//                         scan lanes 7/8 of one with 3-5 lanes, 1/2 with 6-11, 3/16 with 12-15; A/B)
 //   lazy_aux=1            create the job pipeline's aux streams at the first job call, not at open (A/B)
 //   scan_lanes=N          single-query scans on a caller's stream: 0 or 1 launch on that stream (A/B);
-//                         default 3 lanes (the context's stream, aux, aux2), so consecutive queries'
-//                         launches overlap; 2 leaves out aux2
+//                         default 3 (the context's stream, aux, aux2), so consecutive queries' launches
+//                         overlap; 2 leaves out aux2; 4..16 add lanes on streams of their own (for a
+//                         process with more hardware queues, GPU_MAX_HW_QUEUES)
 //   k5_dyn=0              K5: one-query launches in static block rounds, the tail claimed (A/B;
 //                         default: every block claimed per XCD group)
 //   chunk_pingpong=0      the job pipeline's chunks all gather on the aux stream and score on the

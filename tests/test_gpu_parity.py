@@ -354,18 +354,20 @@ def test_big_top64_vs_oracle(big, kernel):
                                  {"PF_DEBUG": "resident_images=0"},
                                  {"PF_DEBUG": "scan=postings,k5_wgs=16"},
                                  {"PF_DEBUG": "scan=postings,k5_wgs=40"},
-                                 {"PF_LIB_PATH": "variants/ticket1/libpokec_fas.so"}],
+                                 {"PF_LIB_PATH": "variants/ticket1/libpokec_fas.so"},
+                                 {"GPU_MAX_HW_QUEUES": "16", "PF_DEBUG": "scan_lanes=15"}],
                          ids=["global-tables", "threshold-1k", "split-records", "split-records-global", "postings",
                               "postings-block64", "postings-block333", "postings-static-transposed",
                               "per-call-images", "postings-16wg-claims", "postings-40wg-claims",
-                              "ticket-mode-1"])
+                              "ticket-mode-1", "hw-queues-16"])
 def test_kernel_variants(env):
     """Forced variants: query tables probed in global memory, always, or whenever one
     query of the batch has tables above 1 KiB (the whole launch then probes global);
     records split over up to 64 lanes (tiles capped at 3 or 1 steps); one-query K5 launches of 16
     or 40 workgroups, so every workgroup claims several blocks from its XCD group's counter (the
     20k corpus has 40 blocks); the library built with PF_TICKET_MODE 1 (release tickets and the
-    acquire fence: the memory-model-ordered cross-workgroup hand-off, pf_device.h)."""
+    acquire fence: the memory-model-ordered cross-workgroup hand-off, pf_device.h); 16 hardware
+    queues with 15 scan lanes (streams of their own, launches of 3/16 of a round each)."""
     import os
     import subprocess
     import sys

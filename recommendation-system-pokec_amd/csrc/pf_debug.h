@@ -34,6 +34,8 @@
 //   k5s_batch_slices=N    K5s (variant build): slices per wave of a batched launch (default 16; A/B)
 //   chunk_plan=W1:W2:..   relative chunk sizes of large job-pipeline calls (default 1:1:1; A/B)
 //   load_threads=N        loader threads (default: min(16, hardware threads))
+//   resident_post=0       one-query all-candidates scans build and upload their K5 image per call
+//                         instead of launching from the postings images built at open (A/B)
 //   resident_images=0     the job pipeline builds its query images per call (K6) instead of
 //                         referencing the ones built for every user at open
 //   host_prof=1           host stage clocks on stderr (pf_open, the loaders, the job pipeline)

@@ -605,7 +605,11 @@ int build_resident_post(pf_ctx* c) {
     if (R.d_pool.p) (void)hipFree(R.d_pool.p);
     R.d_pool.p = nullptr;
     R.d_pool.cap = 0;
-    HIPCHK(c, hipMalloc(&R.d_pool.p, total));
+    if (hipMalloc(&R.d_pool.p, total) != hipSuccess) {  // no room after all: every call builds its image
+        R.d_pool.p = nullptr;
+        (void)hipGetLastError();
+        return PF_OK;
+    }
     R.d_pool.cap = total;
     R.var_lds.assign((size_t)n, 0);
     R.stale.assign((size_t)n, 0);
@@ -621,7 +625,7 @@ int build_resident_post(pf_ctx* c) {
         while (i1 < n && (size_t)(off[i1 + 1] - off[i0]) <= kChunkBytes) ++i1;
         const size_t bytes = (size_t)(off[i1] - off[i0]);
         if (hipEventSynchronize(ev[b]) != hipSuccess || pin[b].ensure(std::max<size_t>(bytes, 16)) != hipSuccess) {
-            rc = c->fail(PF_ENOMEM, "resident postings images: pinned staging failed");
+            rc = PF_ENOMEM;  // pinned staging refused: the resident images stay off (below)
             break;
         }
         uint8_t* h = pin[b].as<uint8_t>();
@@ -648,6 +652,12 @@ int build_resident_post(pf_ctx* c) {
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == PF_OK) rc = c->fail(PF_ENODEV, "resident postings images");
     for (auto& e : ev) (void)hipEventDestroy(e);
+    if (rc == PF_ENOMEM) {  // not fatal: the per-call images serve every query
+        (void)hipFree(R.d_pool.p);
+        R.d_pool.p = nullptr;
+        R.d_pool.cap = 0;
+        return PF_OK;
+    }
     if (rc != PF_OK) return rc;
     if (bad.load()) return c->fail(PF_EINTERNAL, "resident postings image larger than its bound");
     HIPCHK(c, R.d_zero.ensure(64));

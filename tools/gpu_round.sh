@@ -57,6 +57,13 @@ for S in "$@"; do
     quickv:*)
         V=${S#quickv:}
         timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --steps 100 --warmup 10 $Q > $O/quick_$V.json 2> $O/quick_$V.err || exit 5 ;;
+    varchk:*)
+        # varchk:V  tests/gpu_variant_check.py (oracle-checked batched and one-query calls) with vlib/V,
+        # at the default launch and with 16-workgroup one-query launches (several claimed blocks each)
+        V=${S#varchk:}
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 tests/gpu_variant_check.py > $O/varchk_$V.log 2>&1 &&
+        timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so PF_DEBUG=k5_wgs=16 python3 tests/gpu_variant_check.py >> $O/varchk_$V.log 2>&1 || exit 14
+        echo "varchk $V ok" >> $O/varchk_$V.log ;;
     quick4v:*)
         V=${S#quick4v:}
         timeout -k 10 300 env PF_LIB_PATH=$PWD/vlib/$V/libpokec_fas.so python3 bench.py --workload cfg4 --steps 3 --warmup 1 $Q > $O/quick4_$V.json 2> $O/quick4_$V.err || exit 6 ;;
